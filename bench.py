@@ -1,0 +1,159 @@
+#!/usr/bin/env python3
+"""Benchmark: batched kinematic LTV-MPC solves/s on MI355X (BASELINE.json metric).
+
+One step = one fused predict -> linearize -> condense -> interior-point solve of
+every problem of this rank's batch (vc_solve, csrc/kin_ltv.hip), inputs resident
+in HBM.  Default workload: BASELINE config 2 -- B = 1024 kinematic-bicycle
+problems, N = 20, fp64, per GPU.  With --gpus N under torchrun each rank solves
+its own batch (weak scaling, no data-path collective); rank 0 prints one JSON line.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-cpu-baseline]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "vehicle-control_amd"))
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+FP64_VALU_PEAK_TFS = 78.6      # MI355X FP64 vector (spec), SURVEY 8(d)
+N_HORIZON, NX, NU = 20, 6, 2
+# Compulsory HBM bytes per solve: in x0 + kappa + ds + ubar, out
+# u* + x* + u0 (fp64) + status + iters.
+BYTES_PER_SOLVE = (NX + N_HORIZON + N_HORIZON + N_HORIZON * NU) * 8 + \
+                  (N_HORIZON * NU + (N_HORIZON + 1) * NX + NU) * 8 + 8
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=1024, help="problems per GPU (config 2: 1024)")
+    ap.add_argument("--seed", type=int, default=31)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=1024, help="problems in the CPU-baseline sample")
+    return ap.parse_args()
+
+
+def cpu_baseline(batch, sample):
+    """The numpy oracle (oracle/ltv_qp.py + oracle/qp.py) on one host thread, on the
+    first `sample` problems of this rank's workload: the build's CPU 'port' of the
+    reference path (the reference's CasADi/IPOPT cannot run)."""
+    from threadpoolctl import threadpool_limits
+
+    from oracle import ltv_qp as Q
+    from vcmpc.config import load_config
+    W = Q.kin_weights(load_config("kinematic_mpc"))
+    d = {k: v[:sample] for k, v in batch.items()}
+    with threadpool_limits(limits=1):
+        t0 = time.perf_counter()
+        Q.kin_ltv_solve(d["x0"], d["ubar"], d["kappa"], d["ds"], 2.5, W)
+        dt = time.perf_counter() - t0
+    cpu = platform.processor() or platform.machine()
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": len(d["x0"]) / dt, "unit": "solves/s", "cores": 1, "kind": "port",
+            "sample": f"{len(d['x0'])} problems of the C2 workload, one oracle pass (PDIP + active-set polish, "
+                      f"numpy fp64, 1 thread) in {dt:.2f} s on {cpu}"}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+
+    from vcmpc import Context, _abi, dist
+    from vcmpc.config import load_config
+    from vcmpc.workload import kinematic_batch
+
+    rank, local, world = dist.env_rank()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist.init("nccl", dev)
+
+    B = args.batch
+    data = kinematic_batch(B, N=N_HORIZON, seed=args.seed + 7919 * rank)
+    t = {k: torch.from_numpy(v).to(dev) for k, v in data.items()}
+    ubar0 = t["ubar"].clone()
+    ctx = Context(model=_abi.VC_MODEL_KINEMATIC, N=N_HORIZON, max_batch=B, device=local,
+                  kin_car=load_config("kinematic_car"), kin_mpc=load_config("kinematic_mpc"))
+    stream = torch.cuda.current_stream(dev)
+    ctx.set_stream(stream.cuda_stream)
+    xbar = torch.empty((B, N_HORIZON + 1, NX), dtype=torch.float64, device=dev)
+    u0 = torch.empty((B, NU), dtype=torch.float64, device=dev)
+    status = torch.empty((B,), dtype=torch.int32, device=dev)
+    iters = torch.empty((B,), dtype=torch.int32, device=dev)
+
+    def step(ev=None):
+        t["ubar"].copy_(ubar0)  # every step solves the same problems from the same warm start
+        if ev is not None:
+            ev[0].record(stream)
+        ctx.solve(t["x0"], t["kappa"], t["ds"], t["ubar"], xbar, u0, status, iters)
+        if ev is not None:
+            ev[1].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(events[i])
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    st = status.cpu().numpy()
+    it = iters.cpu().numpy()
+    solves, elapsed_max, kern_ms_max = dist.aggregate(float(B * args.steps), elapsed, kern_ms, dev)
+
+    if rank == 0:
+        value = solves / elapsed_max
+        achieved = BYTES_PER_SOLVE * B / (kern_ms / 1e3) / 1e9
+        out = {
+            "metric": "MPC solves/sec (batched, N=20)",
+            "value": value,
+            "unit": "solves/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded C2 sampler, vcmpc/workload.py)",
+            "config": {"workload": f"C2 kinematic-bicycle LTV-MPC, B={B} per GPU, N={N_HORIZON}, fp64",
+                       "batch_per_gpu": B, "global_batch": B * world, "horizon": N_HORIZON,
+                       "parallelism": f"dp{world} (independent shards)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "kin_ltv_kernel<20>", "kernel_ms": kern_ms,
+                         "bytes_per_solve": BYTES_PER_SOLVE},
+            "solver": {"solved_frac": float((st == 0).mean()), "iters_mean": float(it.mean()),
+                       "iters_max": int(it.max())},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(data, min(args.cpu_sample, B))
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    dist.shutdown()
+
+
+if __name__ == "__main__":
+    main()

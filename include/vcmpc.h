@@ -1,0 +1,152 @@
+/*
+ * vcmpc.h -- C ABI of the MI355X-native batched MPC solve path (libvcmpc.so).
+ *
+ * Drop-in boundary for the per-step predict -> linearize -> QP-solve loop of
+ * neverorfrog/vehicle-control (reference @ 2024-12-20).  Each entry point names
+ * the reference interface it replaces (paths relative to the reference checkout):
+ *
+ *   vc_create        KinematicMPC.__init__            vehicle_control/controllers/mpc/kinematic_mpc.py:15-30
+ *                    (the once-only NLP transcription + IPOPT setup, :39-52)
+ *   vc_solve         KinematicMPC.command             kinematic_mpc.py:160-168 (opti.solve at :162)
+ *   vc_rollout       KinematicCar.spatial_transition  vehicle_control/models/kinematic_car.py:61-64,70-72,
+ *                    applied along the horizon        (the dynamics rows of kinematic_mpc.py:95-99)
+ *   vc_linearize     CasADi AD of the dynamics inside IPOPT ("expand": True, kinematic_mpc.py:51)
+ *   vc_condense      the condensed-QP Hessian/gradient of the build's LTV-QP contract
+ *                    (restates the NLP cost kinematic_mpc.py:101-158 linearised)
+ *   vc_plant_step    RacingCar.drive / Robot.transition  vehicle_control/models/racing_car.py:34-46,
+ *                    kinematic_car.py:34-45,66-68 (Euler), dynamic_car.py:144-167,193-195 (RK4)
+ *   vc_spatial_step  <Model>.spatial_transition       kinematic_car.py:70-72, dynamic_car.py:169-199
+ *
+ * Conventions
+ *   - All arrays are C-contiguous, batch-outermost ("AoS"):
+ *       x0[B][nx], kappa[B][N], ds[B][N], ubar[B][N][nu], xbar[B][N+1][nx], u0[B][nu].
+ *     The reference stores state_prediction as (nx, N+1) and action_prediction as
+ *     (nu, N) (kinematic_mpc.py:59-67); the Python mirror transposes.
+ *   - State / action orderings are the reference FancyVector keys:
+ *       kinematic x = [v, delta, s, ey, epsi, t],  u = [a, w]   (kinematic_car.py:81,117)
+ *       dynamic   x = [Ux, Uy, r, delta, s, ey, epsi, t], u = [Fx, w] (dynamic_car.py:209,247)
+ *   - flags = VC_HOST_PTRS: pointers are host memory; the call copies in, runs and
+ *     copies out, and returns when the results are in the caller's buffers.
+ *     flags = VC_DEVICE_PTRS: pointers are device memory on the context's device;
+ *     the call only enqueues work on the context stream (vc_set_stream) and
+ *     returns immediately; call vc_synchronize() before reading results.
+ *   - Return value: 0 on success, a negative VC_E* code on an API or HIP error
+ *     (message via vc_last_error).  Per-problem outcomes are reported in status[b]
+ *     (VC_SOLVED, VC_MAX_ITER, VC_NONFINITE); no exception-style failure, unlike the
+ *     reference simulator's catch-all (simulation/racing.py:416-423).
+ *   - Threading: one context per device per host thread; calls on one context
+ *     are serialised on its stream.
+ */
+#ifndef VCMPC_H
+#define VCMPC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VCMPC_ABI_VERSION 1
+
+typedef struct vc_ctx vc_ctx;
+
+enum vc_model { VC_MODEL_KINEMATIC = 0, VC_MODEL_DYNAMIC = 1 };
+enum vc_dtype { VC_F64 = 0, VC_F32 = 1 };
+enum vc_flags { VC_HOST_PTRS = 0, VC_DEVICE_PTRS = 1 };
+enum vc_tyre { VC_TYRE_FIALA = 0, VC_TYRE_LINEAR = 1 };
+enum vc_status { VC_SOLVED = 0, VC_MAX_ITER = 1, VC_NONFINITE = 2 };
+enum vc_error {
+  VC_OK = 0,
+  VC_E_ARG = -1,      /* bad argument / dimension */
+  VC_E_HIP = -2,      /* HIP runtime error (launch, copy, OOM) */
+  VC_E_UNSUPPORTED = -3 /* model/dtype/horizon combination not built */
+};
+
+/* Kinematic bicycle (config/models/kinematic_car.yaml). */
+typedef struct vc_kin_car {
+  double l; /* wheelbase car.l [m] (kinematic_car.py:39,53 via racing_car.py:27) */
+} vc_kin_car;
+
+/* Dynamic bicycle (config/models/dynamic_car.yaml, dynamic_car.py:62-151). */
+typedef struct vc_dyn_car {
+  double l, m, Izz, a, b, h, eps, Peng;
+  double Xdf, Xdr, Xbf, Xbr; /* drive / brake force distribution */
+  double Caf, Car;           /* cornering stiffness front / rear */
+  double Cd, muf, mur, theta, phi, Av2, Frr;
+  int32_t tyre;              /* enum vc_tyre */
+  int32_t pad_;
+} vc_dyn_car;
+
+/* Kinematic MPC weights and bounds (config/controllers/kinematic.yaml). */
+typedef struct vc_kin_mpc {
+  double w_time, w_ey, w_epsi, w_v, w_w, w_a, w_dev, w_b; /* cost_weights */
+  double a_min, a_max, w_min, w_max;                      /* input_constraints */
+  double v_min, v_max, delta_min, delta_max, ey_min, ey_max; /* state_constraints */
+} vc_kin_mpc;
+
+/* The build's LTV-QP contract knobs (no reference counterpart). */
+typedef struct vc_qp {
+  double prox;      /* proximal weight: + prox * ||u - ubar||^2 */
+  double tol;       /* interior-point stopping tolerance (scaled) */
+  int32_t max_iter; /* interior-point iteration cap */
+  int32_t polish;   /* active-set polish rounds after the interior point (0 = off) */
+} vc_qp;
+
+typedef struct vc_params {
+  vc_kin_car kin_car;
+  vc_dyn_car dyn_car;
+  vc_kin_mpc kin_mpc;
+  vc_qp qp;
+} vc_params;
+
+int vc_abi_version(void);
+/* sizeof(vc_params): lets an FFI binding check its struct mirror. */
+int vc_params_sizeof(void);
+
+/* Create a solve context on `device` for `model` with horizon N and workspace for
+ * up to max_batch problems.  Returns NULL on failure (reason: vc_last_error(NULL)).
+ * Built combinations: (VC_MODEL_KINEMATIC, VC_F64, N = 20) for vc_solve /
+ * vc_condense; every N >= 1 for vc_rollout / vc_linearize / vc_plant_step /
+ * vc_spatial_step. */
+vc_ctx* vc_create(int device, int model, int N, int max_batch, int dtype, const vc_params* params);
+void vc_destroy(vc_ctx* ctx);
+const char* vc_last_error(const vc_ctx* ctx);
+
+/* Use an external HIP stream (hipStream_t passed as void*; NULL = the context's
+ * own stream).  Lets a caller time the work with events on that stream. */
+int vc_set_stream(vc_ctx* ctx, void* stream);
+int vc_synchronize(vc_ctx* ctx);
+
+/* One LTV-MPC step for B problems (B <= max_batch):
+ *   in:     x0[B][nx], kappa[B][N], ds[B][N], ubar[B][N][nu] (warm start)
+ *   out:    ubar <- u*[B][N][nu], xbar <- x*[B][N+1][nx], u0[B][nu] = u*[:,0],
+ *           status[B] (enum vc_status), iters[B] (interior-point iterations).
+ * xbar is output only: the prediction is re-rolled from (x0, ubar). */
+int vc_solve(vc_ctx* ctx, int B, const void* x0, const void* kappa, const void* ds,
+             void* xbar, void* ubar, void* u0, int32_t* status, int32_t* iters, int flags);
+
+/* Predict: xbar[B][N+1][nx] from x0[B][nx] and ubar[B][N][nu] (spatial step). */
+int vc_rollout(vc_ctx* ctx, int B, const void* x0, const void* ubar, const void* kappa,
+               const void* ds, void* xbar, int flags);
+
+/* Linearize: A[B][N][nx][nx], Bm[B][N][nx][nu] of the spatial step at (xbar_k, ubar_k). */
+int vc_linearize(vc_ctx* ctx, int B, const void* xbar, const void* ubar, const void* kappa,
+                 const void* ds, void* A, void* Bm, int flags);
+
+/* Condense: the LTV-QP Hessian H[B][nu*N][nu*N] and gradient g[B][nu*N]. */
+int vc_condense(vc_ctx* ctx, int B, const void* x0, const void* ubar, const void* kappa,
+                const void* ds, void* H, void* g, int flags);
+
+/* Plant step x_next = transition(x, u, kappa, dt) (temporal ODE), one per problem:
+ * x[B][nx], u[B][nu], kappa[B], x_next[B][nx]. */
+int vc_plant_step(vc_ctx* ctx, int B, const void* x, const void* u, const void* kappa,
+                  double dt, void* x_next, int flags);
+
+/* Spatial step x_next = spatial_transition(x, u, kappa, ds): ds[B]. */
+int vc_spatial_step(vc_ctx* ctx, int B, const void* x, const void* u, const void* kappa,
+                    const void* ds, void* x_next, int flags);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VCMPC_H */

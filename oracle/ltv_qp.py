@@ -1,0 +1,177 @@
+"""Oracle restatement of the LTV-QP contract for the kinematic MPC (TEST INFRASTRUCTURE ONLY).
+
+The reference has no QP: every control step solves the nonlinear program of
+controllers/mpc/kinematic_mpc.py:15-30 with IPOPT.  The build replaces that solve
+by one *linear-time-varying QP step* (SURVEY 8a row A8), defined here once and
+implemented identically by the HIP kernel:
+
+1. predict    x_0 = x0,  x_{k+1} = x_k + ds_k f'(x_k, u_k, kappa_k)
+              (spatial Euler, models/kinematic_car.py:47-64, integrators.py:15-23)
+2. linearize  A_k = dx_{k+1}/dx_k,  B_k = dx_{k+1}/du_k  at (xbar_k, ubar_k)
+3. condense   dx_k = G_k dz  (dx_0 = 0),  dz = [da_0, dw_0, da_1, dw_1, ...]
+4. QP         min 1/2 dz'H dz + g'dz  s.t. input boxes and state rows below,
+              where the cost is the reference NLP cost (kinematic_mpc.py:101-158)
+              written exactly in the linearised states, with every ``if_else``
+              branch frozen at the predicted trajectory, ``obstacles`` off, plus
+              a proximal term  prox * ||dz||^2  (the NLP Hessian is
+              singular along the acceleration directions).
+5. output     u* = ubar + dz*,  x* = xbar + G dz*,  u0 = u*_0.
+
+Cost terms (stage n = 0..N-1, terminal state x_N):
+  w_b ds_n (ey_n - ey_min)^2  if  eybar_n < ey_min          kinematic_mpc.py:110-114
+  w_b ds_n (ey_n - ey_max)^2  if  eybar_n > ey_max          kinematic_mpc.py:116-120
+  w_dev ds_n ey_n^2                                          kinematic_mpc.py:122
+  w_w w_n^2                                                  kinematic_mpc.py:124
+  w_a (a_{n+1} - a_n)^2   for n < N-1                        kinematic_mpc.py:126-128
+  w_v (v_N - v_max)^2     if  vbar_N >= v_max                kinematic_mpc.py:144-148
+  w_time t_N + w_ey ey_N^2 + w_epsi epsi_N^2                 kinematic_mpc.py:149-157
+Constraints:
+  a_min <= a_n <= a_max, w_min <= w_n <= w_max, n = 0..N-1  kinematic_mpc.py:88-93
+  v_n >= v_min, delta_min <= delta_n <= delta_max, n = 1..N-1  kinematic_mpc.py:80-85
+  (n = 0 is the fixed initial state, kinematic_mpc.py:23-25: a constant, dropped.)
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import models as M
+
+IV, ID, IS, IEY, IEP, IT = range(6)
+IA, IW = 0, 1
+
+
+def kin_weights(cfg: dict) -> dict:
+    """Pull the numbers the QP consumes out of a kinematic controller config
+    (reference schema: config/controllers/kinematic.yaml)."""
+    cw, ic, sc = cfg["cost_weights"], cfg["input_constraints"], cfg["state_constraints"]
+    qp = cfg.get("qp", {})
+    return dict(
+        w_time=float(cw["time"]), w_ey=float(cw["ey"]), w_epsi=float(cw["epsi"]),
+        w_v=float(cw["v"]), w_w=float(cw["w"]), w_a=float(cw["a"]),
+        w_dev=float(cw["deviation"]), w_b=float(cw["boundary"]),
+        a_min=float(ic["a_min"]), a_max=float(ic["a_max"]),
+        w_min=float(ic["w_min"]), w_max=float(ic["w_max"]),
+        v_min=float(sc["v_min"]), v_max=float(sc["v_max"]),
+        delta_min=float(sc["delta_min"]), delta_max=float(sc["delta_max"]),
+        ey_min=float(sc["ey_min"]), ey_max=float(sc["ey_max"]),
+        prox=float(qp.get("prox", 1e-4)),
+    )
+
+
+def kin_predict(x0, ubar, kappa, ds, L):
+    """Step 1: roll the warm-start inputs forward.  x0[B,6], ubar[B,N,2] -> xbar[B,N+1,6]."""
+    B, N = ubar.shape[:2]
+    xbar = np.empty((B, N + 1, 6))
+    xbar[:, 0] = x0
+    for k in range(N):
+        xbar[:, k + 1] = M.kin_spatial_transition(xbar[:, k], ubar[:, k], kappa[:, k], ds[:, k], L)
+    return xbar
+
+
+def kin_linearize(xbar, ubar, kappa, ds, L):
+    """Step 2: A[B,N,6,6], Bm[B,N,6,2] along the predicted trajectory."""
+    N = ubar.shape[1]
+    return M.kin_spatial_jacobians(xbar[:, :N], ubar, kappa, ds, L)
+
+
+def kin_condense(A, Bm):
+    """Step 3: G[B,N+1,6,2N] with dx_k = G[:,k] @ dz  (block lower triangular)."""
+    B, N = A.shape[:2]
+    G = np.zeros((B, N + 1, 6, 2 * N))
+    for k in range(N):
+        G[:, k + 1] = np.einsum("bij,bjn->bin", A[:, k], G[:, k])
+        G[:, k + 1, :, 2 * k:2 * k + 2] += Bm[:, k]
+    return G
+
+
+def kin_qp(x0, ubar, kappa, ds, L, W):
+    """Steps 1-4.  Returns dict with xbar, G, H[B,n,n], g[B,n], and the inequality
+    system C[B,m,n] dz <= d[B,m] (one-sided rows, m = 4N + 3(N-1))."""
+    x0 = np.asarray(x0, np.float64)
+    ubar = np.asarray(ubar, np.float64)
+    kappa = np.asarray(kappa, np.float64)
+    ds = np.asarray(ds, np.float64)
+    B, N = ubar.shape[:2]
+    n = 2 * N
+    xbar = kin_predict(x0, ubar, kappa, ds, L)
+    A, Bm = kin_linearize(xbar, ubar, kappa, ds, L)
+    G = kin_condense(A, Bm)
+
+    H = np.zeros((B, n, n))
+    g = np.zeros((B, n))
+
+    def add_square(c, r0, row):
+        # c * (r0 + row.dz)^2  -> H += 2c row row', g += 2c r0 row
+        c = np.broadcast_to(np.asarray(c, np.float64), (B,))
+        H[:] += 2.0 * c[:, None, None] * row[:, :, None] * row[:, None, :]
+        g[:] += 2.0 * (c * r0)[:, None] * row
+
+    # stage costs on ey_n (n = 0 is constant: G[:,0] = 0)
+    for k in range(1, N):
+        ey = xbar[:, k, IEY]
+        row = G[:, k, IEY]
+        add_square(W["w_dev"] * ds[:, k], ey, row)
+        lo = ey < W["ey_min"]
+        hi = ey > W["ey_max"]
+        add_square(np.where(lo, W["w_b"] * ds[:, k], 0.0), ey - W["ey_min"], row)
+        add_square(np.where(hi, W["w_b"] * ds[:, k], 0.0), ey - W["ey_max"], row)
+    # input costs: w_w w^2 and slew w_a (a_{n+1}-a_n)^2
+    for k in range(N):
+        e = np.zeros((B, n)); e[:, 2 * k + IW] = 1.0
+        add_square(W["w_w"], ubar[:, k, IW], e)
+    for k in range(N - 1):
+        e = np.zeros((B, n)); e[:, 2 * (k + 1) + IA] = 1.0; e[:, 2 * k + IA] = -1.0
+        add_square(W["w_a"], ubar[:, k + 1, IA] - ubar[:, k, IA], e)
+    # terminal costs
+    vN = xbar[:, N, IV]
+    add_square(np.where(vN >= W["v_max"], W["w_v"], 0.0), vN - W["v_max"], G[:, N, IV])
+    g += W["w_time"] * G[:, N, IT]
+    add_square(W["w_ey"], xbar[:, N, IEY], G[:, N, IEY])
+    add_square(W["w_epsi"], xbar[:, N, IEP], G[:, N, IEP])
+    # proximal term prox*||dz||^2
+    H += 2.0 * W["prox"] * np.eye(n)
+
+    # inequalities C dz <= d
+    rows, rhs = [], []
+    I = np.eye(n)
+    for k in range(N):
+        for j, (lo, hi) in ((IA, (W["a_min"], W["a_max"])), (IW, (W["w_min"], W["w_max"]))):
+            e = np.broadcast_to(I[2 * k + j], (B, n))
+            rows.append(e); rhs.append(hi - ubar[:, k, j])
+            rows.append(-e); rhs.append(ubar[:, k, j] - lo)
+    for k in range(1, N):
+        rows.append(-G[:, k, IV]); rhs.append(xbar[:, k, IV] - W["v_min"])
+        rows.append(G[:, k, ID]); rhs.append(W["delta_max"] - xbar[:, k, ID])
+        rows.append(-G[:, k, ID]); rhs.append(xbar[:, k, ID] - W["delta_min"])
+    C = np.stack(rows, axis=1)
+    d = np.stack(rhs, axis=1)
+    return dict(xbar=xbar, A=A, Bm=Bm, G=G, H=H, g=g, C=C, d=d)
+
+
+def kin_ltv_solve(x0, ubar, kappa, ds, L, W, **qp_kw):
+    """Steps 1-5 with the exact oracle QP solver.  Returns dict with u_star[B,N,2],
+    x_star[B,N+1,6], u0[B,2], dz, lam, kkt (certificate), plus the QP data."""
+    from .qp import solve_qp_batch
+
+    Q = kin_qp(x0, ubar, kappa, ds, L, W)
+    B, N = np.asarray(ubar).shape[:2]
+    sol = solve_qp_batch(Q["H"], Q["g"], Q["C"], Q["d"], **qp_kw)
+    dz = sol["z"]
+    u_star = np.asarray(ubar, np.float64) + dz.reshape(B, N, 2)
+    x_star = Q["xbar"] + np.einsum("bkin,bn->bki", Q["G"], dz)
+    Q.update(sol)
+    Q.update(dz=dz, u_star=u_star, x_star=x_star, u0=u_star[:, 0].copy())
+    return Q
+
+
+def kin_horizon_params(state, state_prediction, mpc_dt, N, k_of_s):
+    """Host-side parameter construction of ``KinematicMPC._init_horizon``
+    (kinematic_mpc.py:170-187), including its quirks: ds uses the *unshifted*
+    warm-start speeds plus 0.5 m, and the curvature preview is evaluated at
+    s0 + cumsum(ds_traj with ds_traj[0] = 0)[:N] (an off-by-one vs ds).
+    state[6], state_prediction[6, N+1] -> (ds[N], kappa[N])."""
+    ds_traj = np.full(N + 1, mpc_dt) * state_prediction[IV, :] + 0.5
+    ds = ds_traj[:-1].copy()
+    ds_traj[0] = 0.0
+    s_traj = (np.cumsum(ds_traj) + state[IS])[:-1]
+    return ds, np.asarray(k_of_s(s_traj), np.float64)

@@ -1,0 +1,162 @@
+"""Exact dense convex-QP solver for the oracle (TEST INFRASTRUCTURE ONLY).
+
+    min 1/2 z'H z + g'z   s.t.  C z <= d          (H symmetric positive definite)
+
+Algorithm: batched Mehrotra predictor-corrector primal-dual interior point in
+float64, run to a 1e-12 scaled tolerance, followed by an *active-set polish*
+(solve the equality-constrained KKT system on the identified active set, accept
+it when it is primal and dual feasible), and a KKT certificate
+
+    stat = ||H z + g + C'lam||_inf,  pfeas = max(C z - d)_+,
+    dfeas = max(-lam)_+,             comp = max|lam_i (d_i - C_i z)|.
+
+This is *not* the kernel's algorithm restated; it is an independent solver whose
+solutions are certified optimal, so that the GPU path's PDIP is checked against
+the QP's unique optimum (H is positive definite thanks to the proximal term).
+The reference has no QP (its IPOPT + HSL MA27 backend, kinematic_mpc.py:39-52,
+solves the NLP directly); see oracle/ltv_qp.py for the contract.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def _max_step(v, dv):
+    """Largest a in (0, 1] with v + a dv >= 0 (rowwise over the batch)."""
+    with np.errstate(divide="ignore", invalid="ignore"):
+        r = np.where(dv < 0, -v / dv, np.inf)
+    return np.minimum(1.0, r.min(axis=-1))
+
+
+def _chol_batch(Mx, done):
+    """Batched Cholesky; a problem whose matrix has lost definiteness (barrier
+    weights ~1e14 near the end) is frozen at its current iterate."""
+    try:
+        return np.linalg.cholesky(Mx)
+    except np.linalg.LinAlgError:
+        Lc = np.empty_like(Mx)
+        for b in range(len(Mx)):
+            try:
+                Lc[b] = np.linalg.cholesky(Mx[b])
+            except np.linalg.LinAlgError:
+                done[b] = True
+                Lc[b] = np.eye(Mx.shape[1])
+        return Lc
+
+
+def pdip_batch(H, g, C, d, tol=1e-12, max_iter=200):
+    H = np.asarray(H, np.float64); g = np.asarray(g, np.float64)
+    C = np.asarray(C, np.float64); d = np.asarray(d, np.float64)
+    B, n = g.shape
+    m = d.shape[1]
+    z = np.zeros((B, n))
+    s = np.maximum(d, 1.0)
+    lam = np.ones((B, m))
+    iters = np.zeros(B, np.int64)
+    done = np.zeros(B, bool)
+    scale = 1.0 + np.maximum(np.abs(g).max(axis=1), np.abs(d).max(axis=1))
+    for it in range(max_iter):
+        rd = np.einsum("bij,bj->bi", H, z) + g + np.einsum("bmi,bm->bi", C, lam)
+        rp = np.einsum("bmi,bi->bm", C, z) + s - d
+        mu = (s * lam).mean(axis=1)
+        conv = (np.abs(rd).max(1) <= tol * scale) & (np.abs(rp).max(1) <= tol * scale) & (mu <= tol * scale)
+        done |= conv
+        if done.all():
+            break
+        iters += ~done
+        w = np.where(done[:, None], 1.0, lam / s)
+        Mx = H + np.einsum("bmi,bm,bmj->bij", C, w, C)
+        Lc = _chol_batch(Mx, done)
+
+        def solve(rc):
+            # (H + C'WC) dz = -rd - C'(W rp - rc/s)
+            rhs = -rd - np.einsum("bmi,bm->bi", C, w * rp - rc / s)
+            y = np.linalg.solve(Lc, rhs[..., None])
+            dz = np.linalg.solve(np.swapaxes(Lc, 1, 2), y)[..., 0]
+            dlam = w * (np.einsum("bmi,bi->bm", C, dz) + rp) - rc / s
+            ds_ = -rp - np.einsum("bmi,bi->bm", C, dz)
+            return dz, ds_, dlam
+
+        # predictor
+        rc = s * lam
+        dz_a, ds_a, dl_a = solve(rc)
+        a_aff = np.minimum(_max_step(s, ds_a), _max_step(lam, dl_a))
+        mu_aff = ((s + a_aff[:, None] * ds_a) * (lam + a_aff[:, None] * dl_a)).mean(1)
+        sigma = (mu_aff / np.maximum(mu, 1e-300)) ** 3
+        # corrector
+        rc = s * lam + ds_a * dl_a - (sigma * mu)[:, None]
+        dz, ds_, dl = solve(rc)
+        alpha = 0.99 * np.minimum(_max_step(s, ds_), _max_step(lam, dl))
+        alpha = np.minimum(alpha, 1.0)
+        alpha = np.where(done, 0.0, alpha)[:, None]
+        z = z + alpha * dz
+        s = s + alpha * ds_
+        lam = lam + alpha * dl
+        s = np.maximum(s, 1e-300)
+        lam = np.maximum(lam, 1e-300)
+    return z, lam, s, iters, done
+
+
+def kkt_residuals(H, g, C, d, z, lam):
+    stat = np.abs(np.einsum("bij,bj->bi", H, z) + g + np.einsum("bmi,bm->bi", C, lam)).max(1)
+    slack = d - np.einsum("bmi,bi->bm", C, z)
+    pfeas = np.maximum(-slack, 0).max(1)
+    dfeas = np.maximum(-lam, 0).max(1)
+    comp = np.abs(lam * slack).max(1)
+    return dict(stat=stat, pfeas=pfeas, dfeas=dfeas, comp=comp)
+
+
+def polish(H, g, C, d, z, lam, s, max_changes=40):
+    """Active-set polish of one problem; returns (z, lam, ok).
+
+    Starts from the active set the interior-point iterate suggests
+    (lam_i > s_i) and repairs it one constraint at a time (add the most violated
+    inactive constraint, else drop the most negative multiplier) until the
+    equality-constrained KKT solution is primal and dual feasible.  Degenerate
+    constraints (s_i, lam_i -> 0 together), which the interior point only
+    approaches linearly, are settled exactly this way."""
+    act = lam > s
+    dscale = 1.0 + np.abs(d).max()
+    for _ in range(max_changes):
+        zp, lp = _eqp(H, g, C, d, act)
+        if zp is None:
+            return z, lam, False
+        viol = C @ zp - d
+        viol[act] = -np.inf
+        neg = np.where(act, lp, np.inf)
+        if neg.min() < -1e-12 * (1.0 + np.abs(lp).max()):
+            act[np.argmin(neg)] = False
+        elif viol.max() > 1e-12 * dscale:
+            act[np.argmax(viol)] = True
+        else:
+            return zp, np.maximum(lp, 0.0), True
+    return z, lam, False
+
+
+def _eqp(H, g, C, d, act):
+    """Solve min 1/2 z'Hz + g'z s.t. C_act z = d_act via the full KKT matrix."""
+    n = len(g)
+    Ca = C[act]
+    k = Ca.shape[0]
+    K = np.zeros((n + k, n + k))
+    K[:n, :n] = H
+    K[:n, n:] = Ca.T
+    K[n:, :n] = Ca
+    rhs = np.concatenate([-g, d[act]])
+    try:
+        sol = np.linalg.solve(K, rhs)
+    except np.linalg.LinAlgError:
+        return None, None
+    lp = np.zeros(len(d))
+    lp[act] = sol[n:]
+    return sol[:n], lp
+
+
+def solve_qp_batch(H, g, C, d, tol=1e-13, max_iter=200, do_polish=True):
+    z, lam, s, iters, done = pdip_batch(H, g, C, d, tol=tol, max_iter=max_iter)
+    polished = np.zeros(len(g), bool)
+    if do_polish:
+        for b in range(len(g)):
+            z[b], lam[b], polished[b] = polish(H[b], g[b], C[b], d[b], z[b], lam[b], s[b])
+    kkt = kkt_residuals(H, g, C, d, z, lam)
+    return dict(z=z, lam=lam, iters=iters, converged=done, polished=polished, kkt=kkt)

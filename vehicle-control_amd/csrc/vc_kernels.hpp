@@ -1,0 +1,51 @@
+// vc_kernels.hpp -- kernel argument blocks and launchers shared by the .hip units.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#include "vcmpc.h"
+
+namespace vc {
+
+// Fused kinematic LTV-MPC step (kin_ltv.hip).
+struct KinLtvArgs {
+  const double* x0;     // [B][6]
+  const double* kappa;  // [B][N]
+  const double* ds;     // [B][N]
+  const double* ubar;   // [B][N][2]  warm start (may alias u_out)
+  double* u_out;        // [B][N][2]  u*
+  double* x_out;        // [B][N+1][6] x*
+  double* u0;           // [B][2]
+  int32_t* status;      // [B]
+  int32_t* iters;       // [B]
+  double* H_out;        // [B][2N][2N]  (mode 1 only)
+  double* g_out;        // [B][2N]      (mode 1 only)
+  int mode;             // 0 = full solve, 1 = stop after condensing and write H, g
+  int B;
+  double L;             // wheelbase
+  vc_kin_mpc w;
+  vc_qp qp;
+};
+
+// Elementwise model kernels (models.hip).
+struct ModelArgs {
+  int model;  // vc_model
+  int B, N;
+  double L;   // kinematic wheelbase
+  vc_dyn_car dyn;
+};
+
+hipError_t launch_kin_ltv(const KinLtvArgs& a, int N, hipStream_t stream);
+size_t kin_ltv_smem_bytes(int N);
+hipError_t launch_plant_step(const ModelArgs& m, int dtype, const void* x, const void* u, const void* kappa, double dt,
+                             void* xn, hipStream_t st);
+hipError_t launch_spatial_step(const ModelArgs& m, int dtype, const void* x, const void* u, const void* kappa,
+                               const void* ds, void* xn, hipStream_t st);
+hipError_t launch_rollout(const ModelArgs& m, int dtype, const void* x0, const void* ubar, const void* kappa,
+                          const void* ds, void* xbar, hipStream_t st);
+hipError_t launch_kin_linearize(const ModelArgs& m, const void* xbar, const void* ubar, const void* kappa,
+                                const void* ds, void* A, void* Bm, hipStream_t st);
+
+}  // namespace vc

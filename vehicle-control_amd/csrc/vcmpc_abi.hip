@@ -1,0 +1,362 @@
+// vcmpc_abi.hip -- the C ABI of libvcmpc.so (declared in include/vcmpc.h).
+//
+// Context management, argument validation, host<->device staging for
+// VC_HOST_PTRS calls, and dispatch to the HIP kernels.  No compute happens on
+// the host: every numeric result comes from a gfx950 kernel.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "vc_kernels.hpp"
+#include "vcmpc.h"
+
+
+struct vc_ctx {
+  int device = 0, model = 0, N = 0, max_batch = 0, dtype = 0;
+  vc_params p{};
+  hipStream_t own = nullptr;
+  hipStream_t stream = nullptr;
+  void* arena = nullptr;
+  size_t arena_bytes = 0;
+  std::string err;
+};
+
+namespace {
+thread_local std::string g_create_err;
+
+int fail(vc_ctx* c, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  else g_create_err = buf;
+  return code;
+}
+
+#define VC_HIP(ctx, call)                                                                         \
+  do {                                                                                            \
+    hipError_t e_ = (call);                                                                       \
+    if (e_ != hipSuccess) return fail((ctx), VC_E_HIP, "%s: %s", #call, hipGetErrorString(e_)); \
+  } while (0)
+
+size_t esize(const vc_ctx* c) { return c->dtype == VC_F32 ? 4 : 8; }
+int nx_of(const vc_ctx* c) { return c->model == VC_MODEL_KINEMATIC ? 6 : 8; }
+
+int ensure_arena(vc_ctx* c, size_t bytes) {
+  if (bytes <= c->arena_bytes) return 0;
+  VC_HIP(c, hipSetDevice(c->device));
+  if (c->arena) VC_HIP(c, hipFree(c->arena));
+  c->arena = nullptr;
+  c->arena_bytes = 0;
+  VC_HIP(c, hipMalloc(&c->arena, bytes));
+  c->arena_bytes = bytes;
+  return 0;
+}
+
+// Staging plan for a host-pointer call: each buffer gets an aligned arena slice.
+struct Slot {
+  const void* host_in;  // copied H2D before the launch (may be null)
+  void* host_out;       // copied D2H after the launch (may be null)
+  size_t bytes;
+  void* dev;
+};
+
+int stage(vc_ctx* c, std::vector<Slot>& slots) {
+  size_t total = 0;
+  for (auto& s : slots) total += (s.bytes + 255) & ~size_t(255);
+  if (int r = ensure_arena(c, total ? total : 256)) return r;
+  size_t off = 0;
+  for (auto& s : slots) {
+    s.dev = static_cast<char*>(c->arena) + off;
+    off += (s.bytes + 255) & ~size_t(255);
+    if (s.host_in && s.bytes) VC_HIP(c, hipMemcpyAsync(s.dev, s.host_in, s.bytes, hipMemcpyHostToDevice, c->stream));
+  }
+  return 0;
+}
+
+int unstage(vc_ctx* c, const std::vector<Slot>& slots) {
+  for (auto& s : slots)
+    if (s.host_out && s.bytes) VC_HIP(c, hipMemcpyAsync(s.host_out, s.dev, s.bytes, hipMemcpyDeviceToHost, c->stream));
+  VC_HIP(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int check_common(vc_ctx* c, int B, int flags) {
+  if (!c) return VC_E_ARG;
+  if (B < 0 || B > c->max_batch) return fail(c, VC_E_ARG, "batch %d outside [0, max_batch=%d]", B, c->max_batch);
+  if (flags != VC_HOST_PTRS && flags != VC_DEVICE_PTRS) return fail(c, VC_E_ARG, "bad flags %d", flags);
+  hipError_t e = hipSetDevice(c->device);
+  if (e != hipSuccess) return fail(c, VC_E_HIP, "hipSetDevice: %s", hipGetErrorString(e));
+  return 0;
+}
+
+vc::ModelArgs model_args(const vc_ctx* c, int B) {
+  vc::ModelArgs m{};
+  m.model = c->model;
+  m.B = B;
+  m.N = c->N;
+  m.L = c->p.kin_car.l;
+  m.dyn = c->p.dyn_car;
+  return m;
+}
+
+bool kin_solve_built(const vc_ctx* c) {
+  return c->model == VC_MODEL_KINEMATIC && c->dtype == VC_F64 && vc::kin_ltv_smem_bytes(c->N) > 0;
+}
+}  // namespace
+
+extern "C" {
+
+int vc_abi_version(void) { return VCMPC_ABI_VERSION; }
+int vc_params_sizeof(void) { return (int)sizeof(vc_params); }
+
+vc_ctx* vc_create(int device, int model, int N, int max_batch, int dtype, const vc_params* params) {
+  g_create_err.clear();
+  if (!params) { fail(nullptr, VC_E_ARG, "params is NULL"); return nullptr; }
+  if (model != VC_MODEL_KINEMATIC && model != VC_MODEL_DYNAMIC) { fail(nullptr, VC_E_ARG, "bad model %d", model); return nullptr; }
+  if (dtype != VC_F64 && dtype != VC_F32) { fail(nullptr, VC_E_ARG, "bad dtype %d", dtype); return nullptr; }
+  if (N < 1 || N > 4096) { fail(nullptr, VC_E_ARG, "bad horizon N=%d", N); return nullptr; }
+  if (max_batch < 1) { fail(nullptr, VC_E_ARG, "bad max_batch %d", max_batch); return nullptr; }
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev == 0) {
+    fail(nullptr, VC_E_HIP, "no HIP device available (%s)", hipGetErrorString(e));
+    return nullptr;
+  }
+  if (device < 0 || device >= ndev) { fail(nullptr, VC_E_ARG, "device %d not in [0,%d)", device, ndev); return nullptr; }
+  e = hipSetDevice(device);
+  if (e != hipSuccess) { fail(nullptr, VC_E_HIP, "hipSetDevice: %s", hipGetErrorString(e)); return nullptr; }
+  vc_ctx* c = new vc_ctx();
+  c->device = device;
+  c->model = model;
+  c->N = N;
+  c->max_batch = max_batch;
+  c->dtype = dtype;
+  c->p = *params;
+  e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    fail(nullptr, VC_E_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
+    delete c;
+    return nullptr;
+  }
+  c->stream = c->own;
+  return c;
+}
+
+void vc_destroy(vc_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->arena) (void)hipFree(c->arena);
+  if (c->own) (void)hipStreamDestroy(c->own);
+  delete c;
+}
+
+const char* vc_last_error(const vc_ctx* c) { return c ? c->err.c_str() : g_create_err.c_str(); }
+
+int vc_set_stream(vc_ctx* c, void* stream) {
+  if (!c) return VC_E_ARG;
+  c->stream = stream ? static_cast<hipStream_t>(stream) : c->own;
+  return 0;
+}
+
+int vc_synchronize(vc_ctx* c) {
+  if (!c) return VC_E_ARG;
+  VC_HIP(c, hipSetDevice(c->device));
+  VC_HIP(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int vc_solve(vc_ctx* c, int B, const void* x0, const void* kappa, const void* ds, void* xbar, void* ubar, void* u0,
+             int32_t* status, int32_t* iters, int flags) {
+  if (int r = check_common(c, B, flags)) return r;
+  if (!kin_solve_built(c))
+    return fail(c, VC_E_UNSUPPORTED, "vc_solve: model=%d dtype=%d N=%d not built (kinematic fp64 N=20 is)", c->model,
+                c->dtype, c->N);
+  if (!x0 || !kappa || !ds || !xbar || !ubar || !u0 || !status || !iters) return fail(c, VC_E_ARG, "null pointer");
+  if (B == 0) return 0;
+  const int N = c->N, nx = 6, nu = 2;
+  vc::KinLtvArgs a{};
+  a.mode = 0;
+  a.B = B;
+  a.L = c->p.kin_car.l;
+  a.w = c->p.kin_mpc;
+  a.qp = c->p.qp;
+  std::vector<Slot> slots;
+  if (flags == VC_HOST_PTRS) {
+    slots = {{x0, nullptr, (size_t)B * nx * 8, nullptr},
+             {kappa, nullptr, (size_t)B * N * 8, nullptr},
+             {ds, nullptr, (size_t)B * N * 8, nullptr},
+             {ubar, ubar, (size_t)B * N * nu * 8, nullptr},
+             {nullptr, xbar, (size_t)B * (N + 1) * nx * 8, nullptr},
+             {nullptr, u0, (size_t)B * nu * 8, nullptr},
+             {nullptr, status, (size_t)B * 4, nullptr},
+             {nullptr, iters, (size_t)B * 4, nullptr}};
+    if (int r = stage(c, slots)) return r;
+    a.x0 = (const double*)slots[0].dev;
+    a.kappa = (const double*)slots[1].dev;
+    a.ds = (const double*)slots[2].dev;
+    a.ubar = (const double*)slots[3].dev;
+    a.u_out = (double*)slots[3].dev;
+    a.x_out = (double*)slots[4].dev;
+    a.u0 = (double*)slots[5].dev;
+    a.status = (int32_t*)slots[6].dev;
+    a.iters = (int32_t*)slots[7].dev;
+  } else {
+    a.x0 = (const double*)x0;
+    a.kappa = (const double*)kappa;
+    a.ds = (const double*)ds;
+    a.ubar = (const double*)ubar;
+    a.u_out = (double*)ubar;
+    a.x_out = (double*)xbar;
+    a.u0 = (double*)u0;
+    a.status = status;
+    a.iters = iters;
+  }
+  VC_HIP(c, vc::launch_kin_ltv(a, N, c->stream));
+  if (flags == VC_HOST_PTRS) return unstage(c, slots);
+  return 0;
+}
+
+int vc_condense(vc_ctx* c, int B, const void* x0, const void* ubar, const void* kappa, const void* ds, void* H,
+                void* g, int flags) {
+  if (int r = check_common(c, B, flags)) return r;
+  if (!kin_solve_built(c))
+    return fail(c, VC_E_UNSUPPORTED, "vc_condense: model=%d dtype=%d N=%d not built", c->model, c->dtype, c->N);
+  if (!x0 || !kappa || !ds || !ubar || !H || !g) return fail(c, VC_E_ARG, "null pointer");
+  if (B == 0) return 0;
+  const int N = c->N, n = 2 * N;
+  vc::KinLtvArgs a{};
+  a.mode = 1;
+  a.B = B;
+  a.L = c->p.kin_car.l;
+  a.w = c->p.kin_mpc;
+  a.qp = c->p.qp;
+  std::vector<Slot> slots;
+  if (flags == VC_HOST_PTRS) {
+    slots = {{x0, nullptr, (size_t)B * 6 * 8, nullptr},
+             {kappa, nullptr, (size_t)B * N * 8, nullptr},
+             {ds, nullptr, (size_t)B * N * 8, nullptr},
+             {ubar, nullptr, (size_t)B * n * 8, nullptr},
+             {nullptr, H, (size_t)B * n * n * 8, nullptr},
+             {nullptr, g, (size_t)B * n * 8, nullptr}};
+    if (int r = stage(c, slots)) return r;
+    a.x0 = (const double*)slots[0].dev;
+    a.kappa = (const double*)slots[1].dev;
+    a.ds = (const double*)slots[2].dev;
+    a.ubar = (const double*)slots[3].dev;
+    a.H_out = (double*)slots[4].dev;
+    a.g_out = (double*)slots[5].dev;
+  } else {
+    a.x0 = (const double*)x0;
+    a.kappa = (const double*)kappa;
+    a.ds = (const double*)ds;
+    a.ubar = (const double*)ubar;
+    a.H_out = (double*)H;
+    a.g_out = (double*)g;
+  }
+  VC_HIP(c, vc::launch_kin_ltv(a, N, c->stream));
+  if (flags == VC_HOST_PTRS) return unstage(c, slots);
+  return 0;
+}
+
+int vc_rollout(vc_ctx* c, int B, const void* x0, const void* ubar, const void* kappa, const void* ds, void* xbar,
+               int flags) {
+  if (int r = check_common(c, B, flags)) return r;
+  if (!x0 || !ubar || !kappa || !ds || !xbar) return fail(c, VC_E_ARG, "null pointer");
+  if (B == 0) return 0;
+  const int N = c->N, nx = nx_of(c);
+  const size_t es = esize(c);
+  vc::ModelArgs m = model_args(c, B);
+  if (flags == VC_HOST_PTRS) {
+    std::vector<Slot> slots = {{x0, nullptr, (size_t)B * nx * es, nullptr},
+                               {ubar, nullptr, (size_t)B * N * 2 * es, nullptr},
+                               {kappa, nullptr, (size_t)B * N * es, nullptr},
+                               {ds, nullptr, (size_t)B * N * es, nullptr},
+                               {nullptr, xbar, (size_t)B * (N + 1) * nx * es, nullptr}};
+    if (int r = stage(c, slots)) return r;
+    VC_HIP(c, vc::launch_rollout(m, c->dtype, slots[0].dev, slots[1].dev, slots[2].dev, slots[3].dev, slots[4].dev,
+                                 c->stream));
+    return unstage(c, slots);
+  }
+  VC_HIP(c, vc::launch_rollout(m, c->dtype, x0, ubar, kappa, ds, xbar, c->stream));
+  return 0;
+}
+
+int vc_linearize(vc_ctx* c, int B, const void* xbar, const void* ubar, const void* kappa, const void* ds, void* A,
+                 void* Bm, int flags) {
+  if (int r = check_common(c, B, flags)) return r;
+  if (c->model != VC_MODEL_KINEMATIC || c->dtype != VC_F64)
+    return fail(c, VC_E_UNSUPPORTED, "vc_linearize: only the kinematic fp64 model is built");
+  if (!xbar || !ubar || !kappa || !ds || !A || !Bm) return fail(c, VC_E_ARG, "null pointer");
+  if (B == 0) return 0;
+  const int N = c->N;
+  vc::ModelArgs m = model_args(c, B);
+  if (flags == VC_HOST_PTRS) {
+    std::vector<Slot> slots = {{xbar, nullptr, (size_t)B * (N + 1) * 6 * 8, nullptr},
+                               {ubar, nullptr, (size_t)B * N * 2 * 8, nullptr},
+                               {kappa, nullptr, (size_t)B * N * 8, nullptr},
+                               {ds, nullptr, (size_t)B * N * 8, nullptr},
+                               {nullptr, A, (size_t)B * N * 36 * 8, nullptr},
+                               {nullptr, Bm, (size_t)B * N * 12 * 8, nullptr}};
+    if (int r = stage(c, slots)) return r;
+    VC_HIP(c, vc::launch_kin_linearize(m, slots[0].dev, slots[1].dev, slots[2].dev, slots[3].dev, slots[4].dev,
+                                       slots[5].dev, c->stream));
+    return unstage(c, slots);
+  }
+  VC_HIP(c, vc::launch_kin_linearize(m, xbar, ubar, kappa, ds, A, Bm, c->stream));
+  return 0;
+}
+
+int vc_plant_step(vc_ctx* c, int B, const void* x, const void* u, const void* kappa, double dt, void* x_next,
+                  int flags) {
+  if (int r = check_common(c, B, flags)) return r;
+  if (!x || !u || !kappa || !x_next) return fail(c, VC_E_ARG, "null pointer");
+  if (B == 0) return 0;
+  const int nx = nx_of(c);
+  const size_t es = esize(c);
+  vc::ModelArgs m = model_args(c, B);
+  if (flags == VC_HOST_PTRS) {
+    std::vector<Slot> slots = {{x, nullptr, (size_t)B * nx * es, nullptr},
+                               {u, nullptr, (size_t)B * 2 * es, nullptr},
+                               {kappa, nullptr, (size_t)B * es, nullptr},
+                               {nullptr, x_next, (size_t)B * nx * es, nullptr}};
+    if (int r = stage(c, slots)) return r;
+    VC_HIP(c, vc::launch_plant_step(m, c->dtype, slots[0].dev, slots[1].dev, slots[2].dev, dt, slots[3].dev,
+                                    c->stream));
+    return unstage(c, slots);
+  }
+  VC_HIP(c, vc::launch_plant_step(m, c->dtype, x, u, kappa, dt, x_next, c->stream));
+  return 0;
+}
+
+int vc_spatial_step(vc_ctx* c, int B, const void* x, const void* u, const void* kappa, const void* ds, void* x_next,
+                    int flags) {
+  if (int r = check_common(c, B, flags)) return r;
+  if (!x || !u || !kappa || !ds || !x_next) return fail(c, VC_E_ARG, "null pointer");
+  if (B == 0) return 0;
+  const int nx = nx_of(c);
+  const size_t es = esize(c);
+  vc::ModelArgs m = model_args(c, B);
+  if (flags == VC_HOST_PTRS) {
+    std::vector<Slot> slots = {{x, nullptr, (size_t)B * nx * es, nullptr},
+                               {u, nullptr, (size_t)B * 2 * es, nullptr},
+                               {kappa, nullptr, (size_t)B * es, nullptr},
+                               {ds, nullptr, (size_t)B * es, nullptr},
+                               {nullptr, x_next, (size_t)B * nx * es, nullptr}};
+    if (int r = stage(c, slots)) return r;
+    VC_HIP(c, vc::launch_spatial_step(m, c->dtype, slots[0].dev, slots[1].dev, slots[2].dev, slots[3].dev,
+                                      slots[4].dev, c->stream));
+    return unstage(c, slots);
+  }
+  VC_HIP(c, vc::launch_spatial_step(m, c->dtype, x, u, kappa, ds, x_next, c->stream));
+  return 0;
+}
+
+}  // extern "C"

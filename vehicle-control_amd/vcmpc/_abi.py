@@ -1,0 +1,111 @@
+"""ctypes binding of ``libvcmpc.so`` (the C ABI declared in ``include/vcmpc.h``).
+
+This is the "thin ctypes C-ABI shim" of the north star: struct mirrors of
+``vc_params`` and typed prototypes of every ``vc_*`` entry point.  There is no
+CPU fallback anywhere in the package -- if the shared library is missing or was
+built for a different ABI, importing the solver raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+LIB_NAME = "libvcmpc.so"
+LIB_PATH = os.environ.get("VCMPC_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME))
+ABI_VERSION = 1
+
+VC_MODEL_KINEMATIC, VC_MODEL_DYNAMIC = 0, 1
+VC_F64, VC_F32 = 0, 1
+VC_HOST_PTRS, VC_DEVICE_PTRS = 0, 1
+VC_TYRE_FIALA, VC_TYRE_LINEAR = 0, 1
+VC_SOLVED, VC_MAX_ITER, VC_NONFINITE = 0, 1, 2
+VC_OK, VC_E_ARG, VC_E_HIP, VC_E_UNSUPPORTED = 0, -1, -2, -3
+
+STATUS_NAMES = {VC_SOLVED: "solved", VC_MAX_ITER: "max_iter", VC_NONFINITE: "nonfinite"}
+
+
+class vc_kin_car(C.Structure):
+    _fields_ = [("l", C.c_double)]
+
+
+class vc_dyn_car(C.Structure):
+    _fields_ = [(k, C.c_double) for k in (
+        "l", "m", "Izz", "a", "b", "h", "eps", "Peng",
+        "Xdf", "Xdr", "Xbf", "Xbr", "Caf", "Car",
+        "Cd", "muf", "mur", "theta", "phi", "Av2", "Frr")] + [("tyre", C.c_int32), ("pad_", C.c_int32)]
+
+
+class vc_kin_mpc(C.Structure):
+    _fields_ = [(k, C.c_double) for k in (
+        "w_time", "w_ey", "w_epsi", "w_v", "w_w", "w_a", "w_dev", "w_b",
+        "a_min", "a_max", "w_min", "w_max",
+        "v_min", "v_max", "delta_min", "delta_max", "ey_min", "ey_max")]
+
+
+class vc_qp(C.Structure):
+    _fields_ = [("prox", C.c_double), ("tol", C.c_double), ("max_iter", C.c_int32), ("polish", C.c_int32)]
+
+
+class vc_params(C.Structure):
+    _fields_ = [("kin_car", vc_kin_car), ("dyn_car", vc_dyn_car), ("kin_mpc", vc_kin_mpc), ("qp", vc_qp)]
+
+
+class VcError(RuntimeError):
+    """Raised for a negative ``vc_*`` return code (API or HIP error)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"vcmpc error {code}: {msg}")
+        self.code = code
+
+
+_vp = C.c_void_p
+_i32p = C.POINTER(C.c_int32)
+
+# name -> (restype, argtypes); every symbol include/vcmpc.h declares
+PROTOTYPES = {
+    "vc_abi_version": (C.c_int, []),
+    "vc_params_sizeof": (C.c_int, []),
+    "vc_create": (_vp, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(vc_params)]),
+    "vc_destroy": (None, [_vp]),
+    "vc_last_error": (C.c_char_p, [_vp]),
+    "vc_set_stream": (C.c_int, [_vp, _vp]),
+    "vc_synchronize": (C.c_int, [_vp]),
+    "vc_solve": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int]),
+    "vc_rollout": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, C.c_int]),
+    "vc_linearize": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int]),
+    "vc_condense": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int]),
+    "vc_plant_step": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, C.c_double, _vp, C.c_int]),
+    "vc_spatial_step": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, C.c_int]),
+}
+
+_LIB = None
+
+
+def load_library(path: str | None = None) -> C.CDLL:
+    """Load ``libvcmpc.so`` once, bind every prototype and check the ABI."""
+    global _LIB
+    if _LIB is not None and path is None:
+        return _LIB
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise ImportError(
+            f"{p} not found: build it with `make -C vehicle-control_amd/csrc` "
+            "(or __graft_entry__.build()); vcmpc has no CPU fallback")
+    lib = C.CDLL(p)
+    for name, (res, args) in PROTOTYPES.items():
+        fn = getattr(lib, name)  # AttributeError = missing export
+        fn.restype = res
+        fn.argtypes = args
+    if lib.vc_abi_version() != ABI_VERSION:
+        raise ImportError(f"{p}: ABI version {lib.vc_abi_version()} != {ABI_VERSION}")
+    if lib.vc_params_sizeof() != C.sizeof(vc_params):
+        raise ImportError(f"{p}: sizeof(vc_params) {lib.vc_params_sizeof()} != ctypes {C.sizeof(vc_params)}")
+    if path is None:
+        _LIB = lib
+    return lib
+
+
+def check(lib, ctx, code: int) -> None:
+    if code != VC_OK:
+        msg = lib.vc_last_error(ctx)
+        raise VcError(code, msg.decode() if msg else "")

@@ -1,0 +1,100 @@
+"""Configuration: YAML loading and packing of ``vc_params``.
+
+The reference reads its YAML with ``yaml.safe_load`` (utils/common_utils.py:16-19)
+and wraps it in OmegaConf for dot access (scripts/kinmain.py:6-11).  OmegaConf is
+not available here, so :class:`AttrDict` provides the same dot access.
+"""
+from __future__ import annotations
+
+import os
+
+import yaml
+
+from . import _abi
+
+CONFIG_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "config")
+
+# The build's LTV-QP contract defaults (no reference counterpart).
+QP_DEFAULTS = {"prox": 1e-4, "tol": 1e-10, "max_iter": 40, "polish": 6}
+
+
+class AttrDict(dict):
+    """dict with attribute access, recursively (a stand-in for OmegaConf.create)."""
+
+    def __init__(self, *args, **kwargs):
+        super().__init__(*args, **kwargs)
+        for k, v in list(self.items()):
+            self[k] = _wrap(v)
+
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError as e:
+            raise AttributeError(k) from e
+
+    def __setattr__(self, k, v):
+        self[k] = _wrap(v)
+
+
+def _wrap(v):
+    if isinstance(v, dict) and not isinstance(v, AttrDict):
+        return AttrDict(v)
+    if isinstance(v, list):
+        return [_wrap(x) for x in v]
+    return v
+
+
+def load_config(path: str) -> AttrDict:
+    """``load_config`` of utils/common_utils.py:16-19, returning dot-accessible dicts.
+    A bare name (``"kinematic_mpc"``) resolves to ``vehicle-control_amd/config/<name>.yaml``."""
+    if not os.path.sep in path and not path.endswith(".yaml"):
+        path = os.path.join(CONFIG_DIR, path + ".yaml")
+    with open(path, "r") as f:
+        return AttrDict(yaml.safe_load(f))
+
+
+def kin_mpc_struct(cfg) -> _abi.vc_kin_mpc:
+    """Weights and bounds of a kinematic controller config (reference schema
+    config/controllers/kinematic.yaml:7-32)."""
+    cw, ic, sc = cfg["cost_weights"], cfg["input_constraints"], cfg["state_constraints"]
+    return _abi.vc_kin_mpc(
+        w_time=float(cw["time"]), w_ey=float(cw["ey"]), w_epsi=float(cw["epsi"]), w_v=float(cw["v"]),
+        w_w=float(cw["w"]), w_a=float(cw["a"]), w_dev=float(cw["deviation"]), w_b=float(cw["boundary"]),
+        a_min=float(ic["a_min"]), a_max=float(ic["a_max"]), w_min=float(ic["w_min"]), w_max=float(ic["w_max"]),
+        v_min=float(sc["v_min"]), v_max=float(sc["v_max"]), delta_min=float(sc["delta_min"]),
+        delta_max=float(sc["delta_max"]), ey_min=float(sc["ey_min"]), ey_max=float(sc["ey_max"]))
+
+
+def qp_struct(cfg=None) -> _abi.vc_qp:
+    q = dict(QP_DEFAULTS)
+    if cfg is not None and cfg.get("qp") is not None:
+        q.update(cfg["qp"])
+    return _abi.vc_qp(prox=float(q["prox"]), tol=float(q["tol"]), max_iter=int(q["max_iter"]),
+                      polish=int(q["polish"]))
+
+
+def dyn_car_struct(cfg, tyre: str = "fiala") -> _abi.vc_dyn_car:
+    """Dynamic-car parameters (reference schema config/models/dynamic_car.yaml:4-32,
+    consumed at models/dynamic_car.py:62-151)."""
+    car, env = cfg["car"], cfg["env"]
+    return _abi.vc_dyn_car(
+        l=float(car["l"]), m=float(car["m"]), Izz=float(car["Izz"]), a=float(car["a"]), b=float(car["b"]),
+        h=float(car["h"]), eps=float(car["eps"]), Peng=float(car["Peng"]),
+        Xdf=float(car["Xd"]["f"]), Xdr=float(car["Xd"]["r"]), Xbf=float(car["Xb"]["f"]), Xbr=float(car["Xb"]["r"]),
+        Caf=float(car["C_alpha"]["f"]), Car=float(car["C_alpha"]["r"]),
+        Cd=float(env["Cd"]), muf=float(env["mu"]["f"]), mur=float(env["mu"]["r"]), theta=float(env["theta"]),
+        phi=float(env["phi"]), Av2=float(env["Av2"]), Frr=float(env["Frr"]),
+        tyre=_abi.VC_TYRE_LINEAR if tyre == "linear" else _abi.VC_TYRE_FIALA)
+
+
+def make_params(kin_car=None, dyn_car=None, kin_mpc=None, tyre: str = "fiala") -> _abi.vc_params:
+    """Pack whichever configs are given into one ``vc_params`` (others zeroed)."""
+    p = _abi.vc_params()
+    if kin_car is not None:
+        p.kin_car = _abi.vc_kin_car(l=float(kin_car["car"]["l"]))
+    if dyn_car is not None:
+        p.dyn_car = dyn_car_struct(dyn_car, tyre)
+    if kin_mpc is not None:
+        p.kin_mpc = kin_mpc_struct(kin_mpc)
+    p.qp = qp_struct(kin_mpc)
+    return p

@@ -1,0 +1,2 @@
+from .controller import Controller  # noqa: F401
+from .kinematic_mpc import KinematicMPC, BatchedKinematicMPC  # noqa: F401

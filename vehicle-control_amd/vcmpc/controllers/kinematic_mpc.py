@@ -1,0 +1,100 @@
+"""Kinematic-bicycle MPC on the GPU -- drop-in for controllers/mpc/kinematic_mpc.py.
+
+``KinematicMPC(car, config).command(state) -> KinematicCarAction`` keeps the
+reference's surface (kinematic_mpc.py:14-193): the same config schema, the same
+``state_prediction`` (ns, N+1) / ``action_prediction`` (na, N) warm-start
+attributes with the same initial values (kinematic_mpc.py:64-68, seed 31 at
+:11), the same horizon-parameter construction ``_init_horizon``
+(kinematic_mpc.py:170-187, quirks included) and ``get_state_prediction``.
+
+What changes is the solve (kinematic_mpc.py:162, IPOPT + HSL MA27 on the NLP):
+one LTV-QP step (predict -> linearize -> condense -> interior point) in one
+fused gfx950 kernel (csrc/kin_ltv.hip).  ``BatchedKinematicMPC`` is the same
+controller for B vehicles at once -- the data-parallel hot path.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .. import _abi
+from ..config import make_params
+from ..solver import Context
+from .controller import Controller
+
+IV, IS = 0, 2
+
+
+def horizon_params(s0, v_pred, mpc_dt, k_of_s):
+    """``_init_horizon`` parameter construction (kinematic_mpc.py:177-187), batched.
+
+    s0[B], v_pred[B, N+1] (the *unshifted* previous speed prediction) ->
+    ds[B, N] = mpc_dt * v_pred[:, :N] + 0.5 and kappa[B, N] = k(s) at
+    s = s0 + cumsum(ds_traj with ds_traj[0] = 0)[:N] (the reference's off-by-one)."""
+    ds_traj = mpc_dt * np.asarray(v_pred, np.float64) + 0.5
+    ds = ds_traj[:, :-1].copy()
+    ds_traj[:, 0] = 0.0
+    s_traj = (np.cumsum(ds_traj, axis=1) + np.asarray(s0, np.float64)[:, None])[:, :-1]
+    kappa = np.ascontiguousarray(np.asarray(k_of_s(s_traj), np.float64).reshape(s_traj.shape))
+    return ds, kappa
+
+
+class BatchedKinematicMPC(Controller):
+    """B independent kinematic MPCs solved in one launch."""
+
+    def __init__(self, car, config, batch: int, device: int = 0, seed: int | None = 31):
+        super().__init__()
+        self.config = config
+        self.car = car
+        self.N = int(config["horizon"])
+        self.dt = float(config["mpc_dt"])
+        self.ns, self.na = len(car.state), len(car.input)
+        self.B = int(batch)
+        if config.get("obstacles", False):
+            raise NotImplementedError("obstacle barrier terms (kinematic_mpc.py:130-133) are SURVEY 8(f) row 4")
+        self.ctx = Context(model=_abi.VC_MODEL_KINEMATIC, N=self.N, max_batch=self.B, dtype=_abi.VC_F64,
+                           device=device, params=make_params(kin_car=car.config, kin_mpc=config))
+        # warm starts: kinematic_mpc.py:64-68 (zeros, v = 0.1; actions 1 + U[0,1) seeded)
+        rng = np.random.RandomState(seed) if seed is not None else np.random
+        self.state_prediction = np.zeros((self.B, self.ns, self.N + 1))
+        self.state_prediction[:, IV, :] += 0.1
+        self.action_prediction = np.ones((self.B, self.na, self.N)) + rng.random_sample((self.B, self.na, self.N))
+        self.status = np.zeros(self.B, np.int32)
+        self.iters = np.zeros(self.B, np.int32)
+
+    def command(self, states):
+        """states[B, ns] -> actions[B, na] (u*_0 of every problem)."""
+        x0 = np.ascontiguousarray(np.asarray(states, np.float64).reshape(self.B, self.ns))
+        ds, kappa = horizon_params(x0[:, IS], self.state_prediction[:, IV, :], self.dt, self.car.track.k)
+        ubar = np.ascontiguousarray(np.swapaxes(self.action_prediction, 1, 2))
+        u0, xbar, ustar, status, iters = self.ctx.solve(x0, kappa, ds, ubar)
+        self.action_prediction = np.swapaxes(ustar, 1, 2).copy()
+        self.state_prediction = np.swapaxes(xbar, 1, 2).copy()
+        self.status, self.iters = status, iters
+        return u0
+
+
+class KinematicMPC(BatchedKinematicMPC):
+    """Single-vehicle drop-in for ``KinematicMPC(car, config)`` (kinematic_mpc.py:14)."""
+
+    def __init__(self, car, config, device: int = 0):
+        super().__init__(car, config, batch=1, device=device, seed=None)
+        # kinematic_mpc.py:65-67 draws from the global numpy RNG seeded at import
+        self.state_prediction = self.state_prediction[0]
+        self.action_prediction = np.ones((self.na, self.N)) + np.random.random((self.na, self.N))
+
+    def command(self, state):
+        sp, ap = self.state_prediction, self.action_prediction
+        self.state_prediction, self.action_prediction = sp[None], ap[None]
+        try:
+            u0 = super().command(state.values.reshape(1, -1))
+        except Exception:
+            self.state_prediction, self.action_prediction = sp, ap
+            raise
+        self.state_prediction = self.state_prediction[0]
+        self.action_prediction = self.action_prediction[0]
+        return self.car.create_action(*u0[0])
+
+    def get_state_prediction(self):
+        """Global (x, y, psi) of the first N predicted states -- kinematic_mpc.py:189-193."""
+        preds = [self.car.rel2glob(self.state_prediction[:, i]) for i in range(self.N)]
+        return np.array(preds).squeeze()

@@ -1,0 +1,174 @@
+"""Batched solve context: the Python face of ``vc_ctx`` (include/vcmpc.h).
+
+Every method takes either host numpy arrays (the call stages them through the
+context's device arena and returns when results are back in the caller's arrays)
+or device-resident ``torch`` tensors on the context's GPU (the call only enqueues
+work on the context stream -- the fast path, used by ``bench.py``).
+
+Shapes (batch-outermost, C-contiguous, state/action orders of the reference
+FancyVector keys, see include/vcmpc.h):
+
+    x0[B, nx]  kappa[B, N]  ds[B, N]  ubar[B, N, nu]  xbar[B, N+1, nx]  u0[B, nu]
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _abi
+from .config import make_params
+
+NX = {_abi.VC_MODEL_KINEMATIC: 6, _abi.VC_MODEL_DYNAMIC: 8}
+NU = 2
+_NP_DT = {_abi.VC_F64: np.float64, _abi.VC_F32: np.float32}
+
+
+def _is_torch(a) -> bool:
+    return type(a).__module__.startswith("torch")
+
+
+class Context:
+    """One solve context (one device, one model, one horizon, one stream)."""
+
+    def __init__(self, model: int = _abi.VC_MODEL_KINEMATIC, N: int = 20, max_batch: int = 1024,
+                 dtype: int = _abi.VC_F64, device: int = 0, params: _abi.vc_params | None = None, **cfgs):
+        self.lib = _abi.load_library()
+        self.model, self.N, self.max_batch, self.dtype, self.device = model, int(N), int(max_batch), dtype, device
+        self.nx = NX[model]
+        self.params = params if params is not None else make_params(**cfgs)
+        h = self.lib.vc_create(device, model, self.N, self.max_batch, dtype, C.byref(self.params))
+        if not h:
+            raise _abi.VcError(_abi.VC_E_HIP, self.lib.vc_last_error(None).decode())
+        self._h = C.c_void_p(h)
+
+    # -- lifetime ---------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.vc_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, code):
+        _abi.check(self.lib, self._h, code)
+
+    def set_stream(self, stream_handle: int | None):
+        """Run on an external HIP stream (e.g. ``torch.cuda.current_stream().cuda_stream``)."""
+        self._check(self.lib.vc_set_stream(self._h, C.c_void_p(stream_handle or 0)))
+
+    def synchronize(self):
+        self._check(self.lib.vc_synchronize(self._h))
+
+    # -- argument marshalling -----------------------------------------------------
+    def _marshal(self, arrays, shapes, dtypes):
+        """Validate a set of buffers; all host numpy or all device torch.
+        Returns (pointers, flags)."""
+        dev = [_is_torch(a) for a in arrays]
+        if any(dev) and not all(dev):
+            raise TypeError("mix of host and device buffers in one call")
+        ptrs = []
+        for a, shp, dt in zip(arrays, shapes, dtypes):
+            if dev[0]:
+                import torch
+                tdt = {np.float64: torch.float64, np.float32: torch.float32, np.int32: torch.int32}[dt]
+                if a.dtype != tdt or not a.is_contiguous() or tuple(a.shape) != tuple(shp):
+                    raise ValueError(f"device buffer must be contiguous {tdt}{tuple(shp)}, got {a.dtype}{tuple(a.shape)}")
+                if not a.is_cuda or a.device.index != self.device:
+                    raise ValueError(f"device buffer must live on cuda:{self.device}")
+                ptrs.append(C.c_void_p(a.data_ptr()))
+            else:
+                if not isinstance(a, np.ndarray) or a.dtype != dt or not a.flags.c_contiguous or a.shape != tuple(shp):
+                    got = f"{getattr(a, 'dtype', type(a))}{getattr(a, 'shape', '')}"
+                    raise ValueError(f"host buffer must be C-contiguous {np.dtype(dt)}{tuple(shp)}, got {got}")
+                ptrs.append(C.c_void_p(a.ctypes.data))
+        return ptrs, (_abi.VC_DEVICE_PTRS if dev[0] else _abi.VC_HOST_PTRS)
+
+    def _batch(self, x):
+        B = int(x.shape[0])
+        if B > self.max_batch:
+            raise ValueError(f"batch {B} > max_batch {self.max_batch}")
+        return B
+
+    # -- entry points -------------------------------------------------------------
+    def solve(self, x0, kappa, ds, ubar, xbar=None, u0=None, status=None, iters=None):
+        """One LTV-MPC step (``vc_solve``).  ``ubar`` is the warm start and is
+        overwritten with u*; returns (u0, xbar, ubar, status, iters)."""
+        B, N, nx, f = self._batch(x0), self.N, self.nx, _NP_DT[self.dtype]
+        if _is_torch(x0):
+            import torch
+            kw = dict(device=x0.device)
+            xbar = torch.empty((B, N + 1, nx), dtype=x0.dtype, **kw) if xbar is None else xbar
+            u0 = torch.empty((B, NU), dtype=x0.dtype, **kw) if u0 is None else u0
+            status = torch.empty((B,), dtype=torch.int32, **kw) if status is None else status
+            iters = torch.empty((B,), dtype=torch.int32, **kw) if iters is None else iters
+        else:
+            xbar = np.empty((B, N + 1, nx), f) if xbar is None else xbar
+            u0 = np.empty((B, NU), f) if u0 is None else u0
+            status = np.empty((B,), np.int32) if status is None else status
+            iters = np.empty((B,), np.int32) if iters is None else iters
+        (px0, pk, pds, pxb, pub, pu0, pst, pit), flags = self._marshal(
+            [x0, kappa, ds, xbar, ubar, u0, status, iters],
+            [(B, nx), (B, N), (B, N), (B, N + 1, nx), (B, N, NU), (B, NU), (B,), (B,)],
+            [f, f, f, f, f, f, np.int32, np.int32])
+        self._check(self.lib.vc_solve(self._h, B, px0, pk, pds, pxb, pub, pu0, pst, pit, flags))
+        return u0, xbar, ubar, status, iters
+
+    def rollout(self, x0, ubar, kappa, ds):
+        B, N, nx, f = self._batch(x0), self.N, self.nx, _NP_DT[self.dtype]
+        xbar = self._like(x0, (B, N + 1, nx))
+        ptrs, flags = self._marshal([x0, ubar, kappa, ds, xbar],
+                                    [(B, nx), (B, N, NU), (B, N), (B, N), (B, N + 1, nx)], [f] * 5)
+        self._check(self.lib.vc_rollout(self._h, B, *ptrs, flags))
+        return xbar
+
+    def linearize(self, xbar, ubar, kappa, ds):
+        B, N, nx, f = self._batch(xbar), self.N, self.nx, _NP_DT[self.dtype]
+        A = self._like(xbar, (B, N, nx, nx))
+        Bm = self._like(xbar, (B, N, nx, NU))
+        ptrs, flags = self._marshal([xbar, ubar, kappa, ds, A, Bm],
+                                    [(B, N + 1, nx), (B, N, NU), (B, N), (B, N), (B, N, nx, nx), (B, N, nx, NU)],
+                                    [f] * 6)
+        self._check(self.lib.vc_linearize(self._h, B, *ptrs, flags))
+        return A, Bm
+
+    def condense(self, x0, ubar, kappa, ds):
+        B, N, nx, f = self._batch(x0), self.N, self.nx, _NP_DT[self.dtype]
+        n = NU * N
+        H = self._like(x0, (B, n, n))
+        g = self._like(x0, (B, n))
+        ptrs, flags = self._marshal([x0, ubar, kappa, ds, H, g],
+                                    [(B, nx), (B, N, NU), (B, N), (B, N), (B, n, n), (B, n)], [f] * 6)
+        self._check(self.lib.vc_condense(self._h, B, *ptrs, flags))
+        return H, g
+
+    def plant_step(self, x, u, kappa, dt):
+        B, nx, f = self._batch(x), self.nx, _NP_DT[self.dtype]
+        xn = self._like(x, (B, nx))
+        px, pu, pk, pxn = self._marshal([x, u, kappa, xn], [(B, nx), (B, NU), (B,), (B, nx)], [f] * 4)[0]
+        flags = _abi.VC_DEVICE_PTRS if _is_torch(x) else _abi.VC_HOST_PTRS
+        self._check(self.lib.vc_plant_step(self._h, B, px, pu, pk, float(dt), pxn, flags))
+        return xn
+
+    def spatial_step(self, x, u, kappa, ds):
+        B, nx, f = self._batch(x), self.nx, _NP_DT[self.dtype]
+        xn = self._like(x, (B, nx))
+        ptrs, flags = self._marshal([x, u, kappa, ds, xn], [(B, nx), (B, NU), (B,), (B,), (B, nx)], [f] * 5)
+        self._check(self.lib.vc_spatial_step(self._h, B, *ptrs, flags))
+        return xn
+
+    def _like(self, ref, shape):
+        if _is_torch(ref):
+            import torch
+            return torch.empty(shape, dtype=ref.dtype, device=ref.device)
+        return np.empty(shape, _NP_DT[self.dtype])
