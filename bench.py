@@ -89,7 +89,10 @@ def main():
     ubar0 = t["ubar"].clone()
     ctx = Context(model=_abi.VC_MODEL_KINEMATIC, N=N_HORIZON, max_batch=B, device=local,
                   kin_car=load_config("kinematic_car"), kin_mpc=load_config("kinematic_mpc"))
-    stream = torch.cuda.current_stream(dev)
+    # a dedicated stream: the default torch stream is the null stream (handle 0),
+    # which vc_set_stream would read as "the context's own stream"
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
     xbar = torch.empty((B, N_HORIZON + 1, NX), dtype=torch.float64, device=dev)
     u0 = torch.empty((B, NU), dtype=torch.float64, device=dev)

@@ -125,6 +125,15 @@ int vc_synchronize(vc_ctx* ctx);
 int vc_solve(vc_ctx* ctx, int B, const void* x0, const void* kappa, const void* ds,
              void* xbar, void* ubar, void* u0, int32_t* status, int32_t* iters, int flags);
 
+/* vc_solve plus per-problem solver diagnostics diag[B][4]:
+ *   [0] final scaled KKT residual, [1] final scaled complementarity mu,
+ *   [2] flags: 1 = interior-point factorisation failed, 2 = interior point
+ *       converged, 4 = active-set polish certified, 8 = polish factorisation failed,
+ *   [3] polish rounds used.  diag follows the pointer convention of `flags`. */
+int vc_solve_diag(vc_ctx* ctx, int B, const void* x0, const void* kappa, const void* ds,
+                  void* xbar, void* ubar, void* u0, int32_t* status, int32_t* iters, void* diag,
+                  int flags);
+
 /* Predict: xbar[B][N+1][nx] from x0[B][nx] and ubar[B][N][nu] (spatial step). */
 int vc_rollout(vc_ctx* ctx, int B, const void* x0, const void* ubar, const void* kappa,
                const void* ds, void* xbar, int flags);

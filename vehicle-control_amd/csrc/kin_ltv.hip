@@ -9,14 +9,24 @@
 //
 // Lane roles (n = 2N decision variables, NC = 2(N-1) state-constraint rows):
 //   lane j < n   owns decision variable dz_j: column j of the condensed
-//                sensitivity G, row j of the Hessian H (registers), row j of the
-//                KKT matrix and of its Cholesky factor (registers), and the two
+//                sensitivity G during the forward sweep, row j of the normal
+//                matrix and of its Cholesky factor (registers Mr), and the two
 //                box inequalities of u_j.
 //   lane r < NC  owns state-constraint row r: r < N-1 -> v_{r+1} >= v_min,
 //                else delta_{r-N+2} in [delta_min, delta_max].
-// LDS holds the constraint rows of G (read as broadcasts), the Cholesky factor
-// for the transposed solve, and small broadcast vectors.  HBM traffic is only
-// the compulsory per-problem inputs and outputs (roofline).
+// LDS holds the Hessian H, the constraint rows of G (broadcast reads), the
+// packed columns of the Cholesky factor (pivot-column broadcast during the
+// factorisation and the transposed solve), and small broadcast vectors:
+// 37.8 KB at N = 20, so four problems fit a CU (B = 1024 fills 256 CUs once).  HBM traffic is only the
+// compulsory per-problem inputs and outputs (roofline).
+//
+// Register discipline (checked with `make resources`: no scratch): Mr[n] is the
+// only register array in the solver loops and is indexed with compile-time
+// indices only (fully unrolled loops); lane-dependent stores are branch-free
+// (dummy LDS slots) because divergent ifs inside the unrolled factorisation make
+// the register allocator spill; sched_barrier fences bound how far the
+// scheduler hoists LDS broadcast reads; LDS is static so every address folds
+// into the ds instruction's offset field.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -26,116 +36,74 @@
 #include "vcmpc.h"
 
 namespace vc {
-
+namespace {
 
 // ---- wave-level helpers ----------------------------------------------------
-__device__ inline double wave_sum(double v) {
+__device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
-__device__ inline double wave_max(double v) {
+__device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
   return v;
 }
-__device__ inline double wave_min(double v) {
+__device__ __forceinline__ double wave_min(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
   return v;
 }
-// value of `v` in lane `src` (src a compile-time constant in the unrolled loops)
-__device__ inline double lane_bcast(double v, int src) {
+// value of `v` in lane `src` (src wave-uniform)
+__device__ __forceinline__ double lane_bcast(double v, int src) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), src);
   const int hi = __builtin_amdgcn_readlane(__double2hiint(v), src);
   return __hiloint2double(hi, lo);
 }
-__device__ inline void wave_sync() { __syncthreads(); }  // one-wave workgroup: cheap
+// one-wave workgroup: LDS ordering point (s_waitcnt + a trivial s_barrier)
+__device__ __forceinline__ void wave_sync() { __syncthreads(); }
+__device__ __forceinline__ void fence() { __builtin_amdgcn_sched_barrier(0); }
+// compiler-only memory barrier: stops LICM from hoisting the (loop-invariant) LDS
+// reads of G / the factor out of the solver loops into thousands of live registers
+__device__ __forceinline__ void no_hoist() { asm volatile("" ::: "memory"); }
+
+// LDS pointer the compiler cannot see through: re-derived from an opaque
+// register at the point of use, it stops the address arithmetic of the
+// (thousands of) constant-address broadcast reads in the unrolled matrix build
+// from being hoisted out of the solver loop into live registers, which spills.
+using lds_cdouble = const __attribute__((address_space(3))) double;
+__device__ __forceinline__ lds_cdouble* lds_opaque(const double* p) {
+  uint32_t a = (uint32_t)(uintptr_t)(lds_cdouble*)p;
+  asm volatile("" : "+v"(a));
+  return (lds_cdouble*)(uintptr_t)a;
+}
 
 // largest a in (0,1] keeping v + a dv >= 0
-__device__ inline double step_bound(double v, double dv) { return dv < 0.0 ? -v / dv : 1.0; }
+__device__ __forceinline__ double step_bound(double v, double dv) { return dv < 0.0 ? -v / dv : 1.0; }
 
 template <int N>
-struct KinDims {
-  static constexpr int n = 2 * N;        // decision variables
-  static constexpr int NC = 2 * (N - 1); // state-constraint rows
-  static constexpr int LD = n + 1;       // padded LDS row stride (conflict-free column reads)
-  static_assert(n <= 64, "one wavefront per problem needs 2N <= 64");
+struct Dims {
+  static constexpr int n = 2 * N;         // decision variables
+  static constexpr int NC = 2 * (N - 1);  // state-constraint rows
+  static constexpr int LD = n + 1;        // odd LDS row stride: lane-varying-row reads are conflict-free
+  static_assert(n <= 64 && N >= 2, "one wavefront per problem needs 2 <= N <= 32");
 };
 
 template <int N>
-struct __align__(16) KinShared {
-  using D = KinDims<N>;
-  double G[D::NC][D::LD];     // constraint rows of the condensed sensitivity
-  double Lm[D::n][D::LD];     // Cholesky factor rows (for the transposed solve)
-  double xb[N + 1][KIN_NX];   // predicted trajectory
-  double jac[N][9];           // Jacobian data per stage (KinJac)
-  double ub[D::n];            // warm-start inputs
+struct Smem {
+  using D = Dims<N>;
+  double G[D::NC][D::LD];   // constraint rows of the condensed sensitivity (row r: stage crow_stage(r))
+  double H[D::n + 1][D::LD];  // condensed Hessian (constant over the solve); row n: dummy
+  double Lc[D::n * (D::n + 1) / 2 + 1];  // packed columns of the Cholesky factor (+1 dummy slot)
+  double xb[N + 1][KIN_NX]; // predicted trajectory
+  double jac[N][9];         // Jacobian data per stage (KinJac)
+  double ub[D::n];          // warm-start inputs, interleaved (a_0, w_0, a_1, ...)
   double kap[N], ds[N];
-  double vz[64];              // broadcast: a length-n vector (z, dz, fixed values, ...)
-  double vc[64];              // broadcast: a length-NC vector (weights, residual terms)
-  double col[2][64];          // broadcast: one Cholesky column / one G row
-  double dinv[64];            // 1 / L_kk
+  double dinv[64];          // 1 / L_kk
+  double vz[64];            // broadcast: a length-n vector (z, dz, ...)
+  double vc[64];            // broadcast: a length-NC vector (weights, residual terms)
+  double col[2][64];        // broadcast: one sensitivity column during the forward sweep
 };
-
-// ---- dense kernels on register-resident rows -------------------------------
-
-// In-place Cholesky of the SPD matrix whose row `lane` is Mr[0..n).  On return
-// Mr holds row `lane` of L (lower part), s.Lm the same rows, s.dinv = 1/diag.
-// Returns false if a pivot is not positive (uniform).
-template <int N>
-__device__ bool chol_rows(double (&Mr)[KinDims<N>::n], KinShared<N>& s, int lane) {
-  constexpr int n = KinDims<N>::n;
-  bool ok = true;
-  double mydiag = 1.0;
-#pragma unroll
-  for (int k = 0; k < n; ++k) {
-    const double dkk = lane_bcast(Mr[k], k);
-    ok = ok && (dkk > 0.0);
-    const double d = sqrt(dkk);
-    const double inv = 1.0 / d;
-    const double lik = (lane == k) ? d : Mr[k] * inv;
-    if (lane == k) mydiag = d;
-    Mr[k] = lik;
-    double* cb = s.col[k & 1];
-    cb[lane] = lik;
-    wave_sync();
-#pragma unroll
-    for (int j = k + 1; j < n; ++j) Mr[j] -= lik * cb[j];
-  }
-  if (lane < n) {
-#pragma unroll
-    for (int j = 0; j < n; ++j) s.Lm[lane][j] = Mr[j];
-    s.dinv[lane] = 1.0 / mydiag;
-  }
-  wave_sync();
-  return ok;
-}
-
-// Solve (L L') x = b, lane j holding b_j; returns x_j.  Runtime loops over the
-// factor in LDS (s.Lm rows, s.dinv): the substitution chain is inherently serial,
-// so unrolling it only inflates register pressure.
-template <int N>
-__device__ double chol_solve(const KinShared<N>& s, double b, int lane) {
-  constexpr int n = KinDims<N>::n;
-  const int row = lane < n ? lane : 0;
-  double acc = b, y = 0.0;
-#pragma unroll 2
-  for (int k = 0; k < n; ++k) {  // forward: L y = b  (lane i reads L[i][k])
-    const double yk = lane_bcast(acc, k) * s.dinv[k];
-    if (lane == k) y = yk;
-    acc -= s.Lm[row][k] * yk;
-  }
-  acc = y;
-  double x = 0.0;
-#pragma unroll 2
-  for (int k = n - 1; k >= 0; --k) {  // backward: L' x = y  (lane i reads L[k][i])
-    const double xk = lane_bcast(acc, k) * s.dinv[k];
-    if (lane == k) x = xk;
-    acc -= s.Lm[k][row] * xk;
-  }
-  return x;
-}
 
 // stage index (1..N-1) of constraint row r
 template <int N>
@@ -143,50 +111,170 @@ __host__ __device__ constexpr int crow_stage(int r) {
   return r < N - 1 ? r + 1 : r - (N - 1) + 1;
 }
 
-// y_r = G_r . v for lane r (v broadcast in s.vz)
+// packed-column offset of column k of the factor (rows k..n-1)
+template <int n>
+__host__ __device__ constexpr int lc_off(int k) {
+  return k * n - k * (k - 1) / 2;
+}
+
+// y_r = G_r . v for lane r (v broadcast in s.vz); rows have <= 2(N-1) nonzeros
 template <int N>
-__device__ double grow_dot(const KinShared<N>& s, int lane) {
-  constexpr int n = KinDims<N>::n, NC = KinDims<N>::NC;
-  if (lane >= NC) return 0.0;
-  double acc = 0.0;
-#pragma unroll
-  for (int i = 0; i < n - 2; ++i) acc += s.G[lane][i] * s.vz[i];  // rows have <= 2(N-1) nonzeros
-  return acc;
+__device__ double grow_dot(const Smem<N>& s, int lane) {
+  constexpr int NC = Dims<N>::NC;
+  const int r = lane < NC ? lane : 0;
+  lds_cdouble* g = lds_opaque(&s.G[r][0]);
+  lds_cdouble* v = lds_opaque(&s.vz[0]);
+  double a0 = 0.0, a1 = 0.0;
+#pragma unroll 2
+  for (int i = 0; i < 2 * (N - 1); i += 2) {
+    a0 += g[i] * v[i];
+    a1 += g[i + 1] * v[i + 1];
+  }
+  return lane < NC ? a0 + a1 : 0.0;
 }
 
 // (G' v)_j for lane j (v broadcast in s.vc)
 template <int N>
-__device__ double gt_dot(const KinShared<N>& s, int lane) {
-  constexpr int n = KinDims<N>::n, NC = KinDims<N>::NC;
-  if (lane >= n) return 0.0;
-  double acc = 0.0;
-#pragma unroll
-  for (int r = 0; r < NC; ++r) acc += s.G[r][lane] * s.vc[r];
-  return acc;
+__device__ double gt_dot(const Smem<N>& s, int lane) {
+  constexpr int n = Dims<N>::n, NC = Dims<N>::NC;
+  constexpr int LD = Dims<N>::LD;
+  const int j = lane < n ? lane : 0;
+  lds_cdouble* g = lds_opaque(&s.G[0][j]);
+  lds_cdouble* v = lds_opaque(&s.vc[0]);
+  double a0 = 0.0, a1 = 0.0;
+#pragma unroll 2
+  for (int r = 0; r < NC; r += 2) {
+    a0 += g[r * LD] * v[r];
+    a1 += g[(r + 1) * LD] * v[r + 1];
+  }
+  return lane < n ? a0 + a1 : 0.0;
 }
 
-// (H v)_j with H row j in registers (v broadcast in s.vz)
+// (H v)_j for lane j (v broadcast in s.vz)
 template <int N>
-__device__ double h_dot(const double (&Hr)[KinDims<N>::n], const KinShared<N>& s) {
-  constexpr int n = KinDims<N>::n;
-  double acc = 0.0;
-#pragma unroll
-  for (int i = 0; i < n; ++i) acc += Hr[i] * s.vz[i];
-  return acc;
+__device__ double h_dot(const Smem<N>& s, int lane) {
+  constexpr int n = Dims<N>::n;
+  const int j = lane < n ? lane : 0;
+  lds_cdouble* h = lds_opaque(&s.H[j][0]);
+  lds_cdouble* v = lds_opaque(&s.vz[0]);
+  double a0 = 0.0, a1 = 0.0;
+#pragma unroll 4
+  for (int i = 0; i < n; i += 2) {
+    a0 += h[i] * v[i];
+    a1 += h[i + 1] * v[i + 1];
+  }
+  return a0 + a1;
 }
 
-// inequality side data of one lane role (box or state row)
+// In-place right-looking Cholesky of the SPD matrix whose row `lane` is Mr.
+// On return Mr holds row `lane` of L (lower part), s.Lc its columns, s.dinv the
+// inverse pivots.  Returns false (uniform) if a pivot is not positive.
+template <int N>
+__device__ bool cholesky(double (&Mr)[Dims<N>::n], Smem<N>& s, int lane) {
+  constexpr int n = Dims<N>::n;
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < n; ++k) {
+    const double dkk = lane_bcast(Mr[k], k);
+    ok = ok && (dkk > 0.0);
+    const double d = sqrt(dkk);
+    const double inv = 1.0 / d;
+    const double lik = (lane == k) ? d : Mr[k] * inv;
+    Mr[k] = lik;
+    // branch-free stores (dummy slots): lane-divergent ifs in this fully unrolled
+    // loop make the register allocator spill hundreds of VGPRs
+    s.Lc[lane >= k && lane < n ? lc_off<n>(k) + lane - k : n * (n + 1) / 2] = lik;
+    s.dinv[lane == k ? k : 63] = inv;
+    wave_sync();
+    fence();
+#pragma unroll
+    for (int j = k + 1; j < n; ++j) {
+      Mr[j] -= lik * s.Lc[lc_off<n>(k) + j - k];
+      if (((j - k) & 7) == 0) fence();
+    }
+    fence();
+  }
+  return ok;
+}
+
+// Solve (L L') x = b, lane j holding b_j; returns x_j.  The forward sweep reads
+// L[i][k] from the row registers, the backward sweep L[k][i] (column i of the
+// packed factor) from LDS.
+template <int N>
+__device__ double chol_solve(const double (&Lr)[Dims<N>::n], const Smem<N>& s, double b, int lane) {
+  constexpr int n = Dims<N>::n;
+  const int row = lane < n ? lane : 0;
+  const int off = lc_off<n>(row) - row;
+  double acc = b, y = 0.0;
+#pragma unroll
+  for (int k = 0; k < n; ++k) {  // L y = b
+    const double yk = lane_bcast(acc, k) * s.dinv[k];
+    y = (lane == k) ? yk : y;
+    acc -= Lr[k] * yk;
+    if ((k & 3) == 3) fence();
+  }
+  acc = y;
+  double x = 0.0;
+#pragma unroll 4
+  for (int k = n - 1; k >= 0; --k) {  // L' x = y: lane i < k needs L[k][i]
+    const double xk = lane_bcast(acc, k) * s.dinv[k];
+    x = (lane == k) ? xk : x;
+    acc -= s.Lc[k >= row ? off + k : 0] * xk;
+  }
+  return x;
+}
+
+// Mr = row `lane` of H + diag(wb) + sum_r wc_r g_r g_r'  (wc broadcast in s.vc;
+// row r of G has 2 crow_stage(r) nonzero columns)
+template <int N>
+__device__ __forceinline__ void build_normal(double (&Mr)[Dims<N>::n], const Smem<N>& s, double wb, int lane) {
+  constexpr int n = Dims<N>::n, NC = Dims<N>::NC;
+  constexpr int LD = Dims<N>::LD;
+  const int j = lane < n ? lane : 0;
+  lds_cdouble* Hrow = lds_opaque(&s.H[j][0]);
+#pragma unroll
+  for (int i = 0; i < n; ++i) {
+    Mr[i] = Hrow[i] + (i == lane ? wb : 0.0);
+    if ((i & 7) == 7) fence();
+  }
+  lds_cdouble* G = lds_opaque(&s.G[0][0]);
+  lds_cdouble* Gcol = lds_opaque(&s.G[0][j]);
+  lds_cdouble* vc = lds_opaque(&s.vc[0]);
+#pragma unroll
+  for (int r = 0; r < NC; ++r) {
+    // unconditional (clamped-index) load: a `lane < n ? load : 0` select becomes a
+    // divergent branch, and branches inside this unrolled block make the
+    // register allocator spill; rows of lanes >= n are discarded below
+    const double t = vc[r] * Gcol[r * LD];
+    fence();
+#pragma unroll
+    for (int i = 0; i < 2 * crow_stage<N>(r); ++i) {
+      Mr[i] += t * G[r * LD + i];
+      if ((i & 7) == 7) fence();
+    }
+    fence();
+  }
+#pragma unroll
+  for (int i = 0; i < n; ++i) Mr[i] = (lane < n) ? Mr[i] : 0.0;
+}
+
+// inequality data of one lane role (box or state row): bounds lo <= y <= hi,
+// slacks slo = y - lo, shi = hi - y, multipliers llo, lhi.
 struct Side {
   double lo, hi, slo, shi, llo, lhi;
   bool hasLo, hasHi;
 };
 
+}  // namespace
+
 template <int N>
 __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
-  using D = KinDims<N>;
+  using D = Dims<N>;
   constexpr int n = D::n, NC = D::NC;
-  extern __shared__ __align__(16) unsigned char smem_raw[];
-  KinShared<N>& s = *reinterpret_cast<KinShared<N>*>(smem_raw);
+  // static LDS: every address is a compile-time constant folded into the ds
+  // instruction's offset field (a dynamic extern buffer makes the compiler
+  // materialise each address in an SGPR and spill them)
+  __shared__ Smem<N> s;
   const int lane = threadIdx.x;
   const int b = blockIdx.x;
   if (b >= A.B) return;
@@ -201,9 +289,9 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
   if (lane < KIN_NX) s.xb[0][lane] = A.x0[(size_t)b * KIN_NX + lane];
   wave_sync();
 
-  // ---- predict + linearize + condense (fused, one pass over the horizon) ---
-  // Trajectory values are uniform across lanes; lane j also carries column j of
-  // the sensitivity (dv, ddelta, dey, depsi, dt) w.r.t. dz_j.
+  // ---- predict + linearize + condense (one fused pass over the horizon) -----
+  // The trajectory is uniform across lanes; lane j also carries column j of the
+  // sensitivity (dv, ddelta, dey, depsi, dt) with respect to dz_j.
   double x[KIN_NX];
 #pragma unroll
   for (int i = 0; i < KIN_NX; ++i) x[i] = s.xb[0][i];
@@ -214,6 +302,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
   double gj = 0.0;
   bool finite = true;
 
+#pragma unroll 1
   for (int k = 0; k < N; ++k) {
     const double a = s.ub[2 * k], w = s.ub[2 * k + 1], kk = s.kap[k], h = s.ds[k];
     const KinJac J = kin_spatial_jac(x, kk, A.L);
@@ -262,27 +351,31 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
     cb[lane] = (lane < n) ? cey : 0.0;
     wave_sync();
     const double t2 = 2.0 * cw * cey;
+    fence();
 #pragma unroll
-    for (int i = 0; i < n; ++i) Hr[i] += t2 * cb[i];
+    for (int i = 0; i < n; ++i) {
+      Hr[i] += t2 * cb[i];
+      if ((i & 7) == 7) fence();
+    }
     gj += 2.0 * lin * cey;
   }
   // terminal rows on v_N (kinematic_mpc.py:144-148), epsi_N (:155-157), t_N (:149-151)
   {
     const double vN = x[0];
-    const double cw = (vN >= W.v_max) ? W.w_v : 0.0;
-    double* cb = s.col[0];
-    cb[lane] = (lane < n) ? cv : 0.0;
+    const double cwv = (vN >= W.v_max) ? W.w_v : 0.0;
     wave_sync();
-    const double t2 = 2.0 * cw * cv;
-#pragma unroll
-    for (int i = 0; i < n; ++i) Hr[i] += t2 * cb[i];
-    gj += 2.0 * cw * (vN - W.v_max) * cv;
-    double* cb1 = s.col[1];
-    cb1[lane] = (lane < n) ? cep : 0.0;
+    s.col[0][lane] = (lane < n) ? cv : 0.0;
+    s.col[1][lane] = (lane < n) ? cep : 0.0;
     wave_sync();
+    const double t2 = 2.0 * cwv * cv;
     const double t3 = 2.0 * W.w_epsi * cep;
+    fence();
 #pragma unroll
-    for (int i = 0; i < n; ++i) Hr[i] += t3 * cb1[i];
+    for (int i = 0; i < n; ++i) {
+      Hr[i] += t2 * s.col[0][i] + t3 * s.col[1][i];
+      if ((i & 7) == 7) fence();
+    }
+    gj += 2.0 * cwv * (vN - W.v_max) * cv;
     gj += 2.0 * W.w_epsi * x[4] * cep;
     gj += W.w_time * ct;
   }
@@ -312,8 +405,15 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
       if (i == lane + 2) Hr[i] += dp2;
     }
   }
-  if (lane >= n) gj = 0.0;
+  gj = (lane < n) ? gj : 0.0;
+#pragma unroll
+  for (int i = 0; i < n; ++i) Hr[i] = (lane < n) ? Hr[i] : 0.0;
   wave_sync();
+  {
+    const int j = lane < n ? lane : n;  // lanes >= n write the dummy row
+#pragma unroll
+    for (int i = 0; i < n; ++i) s.H[j][i] = Hr[i];
+  }
   if (A.mode == 1) {  // vc_condense: expose the QP data of the fused kernel
     if (lane < n) {
 #pragma unroll
@@ -371,160 +471,61 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
   cs.llo = cs.hasLo ? 1.0 : 0.0;
   cs.lhi = cs.hasHi ? 1.0 : 0.0;
 
-  // ---- solver state machine ---------------------------------------------------
-  // Phase PDIP: Mehrotra predictor-corrector on the normal equations
-  //   (H + C'WC) dz = -rd - C'e.
-  // Phase POLISH: crossover to the active set the interior point identified:
-  //   box-active inputs are fixed (identity rows), active state rows are imposed
-  //   with an augmented Lagrangian (P + rho C_A'C_A), whose multiplier update
-  //   converges in a few solves with one factorisation; the set is repaired
-  //   until primal and dual feasible (oracle/qp.py:polish does the same with a
-  //   direct KKT solve).  Every phase shares one matrix build, one Cholesky and
-  //   one solve site, keeping the unrolled code and register footprint small.
-  enum { PH_PDIP = 0, PH_POLISH = 1, PH_DONE = 2 };
-  constexpr double AL_RHO = 100.0;
-  constexpr int AL_MAX = 8;
+  // ---- Phase 1: Mehrotra predictor-corrector interior point ------------------
+  // Normal equations (H + diag(wb) + G'diag(wc)G) dz = rhs, one factorisation and
+  // two solves (predictor, corrector) per iteration.
   const int max_iter = A.qp.max_iter;
   const double tol = A.qp.tol * scale;
-  const double ptol = 1e-11 * scale;
-  int phase = finite ? PH_PDIP : PH_DONE;
-  int it = 0, rounds = 0;
-  bool converged = false, polished = false;
+  int it = 0;
+  bool converged = false, chol_fail = false, near = false;
+  double last_res = 0.0, last_mu = 0.0;
   double Mr[n];
-  // polish state
-  bool alo_b = false, ahi_b = false, alo_c = false, ahi_c = false;
-  bool fixed = false;
-  double zfix = 0.0, rho_c = 0.0, nu_c = 0.0, bnd_c = 0.0, base = 0.0;
-  uint64_t fmask = 0ull;
-  // PDIP per-iteration quantities
-  double rd = 0, rlo_b = 0, rhi_b = 0, rlo_c = 0, rhi_c = 0, mu = 0;
-  double wlo_b = 0, whi_b = 0, wlo_c = 0, whi_c = 0;
-  double pa1 = 0, pa2 = 0, pa3 = 0, pa4 = 0, pc1 = 0, pc2 = 0, pc3 = 0, pc4 = 0;  // predictor directions
-
-  while (phase != PH_DONE) {
-    double wb = 0.0, wc = 0.0;
-    if (phase == PH_PDIP) {
+  if (finite) {
+#pragma unroll 1
+    for (;;) {
+      no_hoist();
       wave_sync();
-      if (lane < n) s.vz[lane] = z;
+      s.vz[lane] = (lane < n) ? z : 0.0;
       s.vc[lane] = (lane < NC) ? (cs.lhi - cs.llo) : 0.0;
       wave_sync();
       const double yc = grow_dot<N>(s, lane);
-      rd = (lane < n) ? (h_dot<N>(Hr, s) + gj + (bx.lhi - bx.llo) + gt_dot<N>(s, lane)) : 0.0;
-      rlo_b = bx.hasLo ? (z - bx.lo - bx.slo) : 0.0;
-      rhi_b = bx.hasHi ? (bx.hi - z - bx.shi) : 0.0;
-      rlo_c = cs.hasLo ? (yc - cs.lo - cs.slo) : 0.0;
-      rhi_c = cs.hasHi ? (cs.hi - yc - cs.shi) : 0.0;
-      mu = wave_sum(bx.slo * bx.llo + bx.shi * bx.lhi + cs.slo * cs.llo + cs.shi * cs.lhi) / mtot;
+      const double rd = (lane < n) ? (h_dot<N>(s, lane) + gj + (bx.lhi - bx.llo) + gt_dot<N>(s, lane)) : 0.0;
+      const double rlo_b = bx.hasLo ? (z - bx.lo - bx.slo) : 0.0;
+      const double rhi_b = bx.hasHi ? (bx.hi - z - bx.shi) : 0.0;
+      const double rlo_c = cs.hasLo ? (yc - cs.lo - cs.slo) : 0.0;
+      const double rhi_c = cs.hasHi ? (cs.hi - yc - cs.shi) : 0.0;
+      const double mu = wave_sum(bx.slo * bx.llo + bx.shi * bx.lhi + cs.slo * cs.llo + cs.shi * cs.lhi) / mtot;
       const double res =
           wave_max(fmax(fmax(fabs(rd), fmax(fabs(rlo_b), fabs(rhi_b))), fmax(fabs(rlo_c), fabs(rhi_c))));
-      const bool stop = (res <= tol && mu <= tol) || it >= max_iter || !isfinite(res) || !isfinite(mu);
-      if (stop) {
-        converged = (res <= tol && mu <= tol);
-        if (A.qp.polish > 0 && isfinite(res) && isfinite(mu)) {
-          phase = PH_POLISH;
-          alo_b = bx.hasLo && bx.llo > bx.slo;
-          ahi_b = bx.hasHi && bx.lhi > bx.shi;
-          alo_c = cs.hasLo && cs.llo > cs.slo;
-          ahi_c = cs.hasHi && cs.lhi > cs.shi;
-        } else {
-          phase = PH_DONE;
-        }
-        continue;
-      }
+      converged = res <= tol && mu <= tol;
+      last_res = res;
+      last_mu = mu;
+      if (converged || it >= max_iter || !isfinite(res) || !isfinite(mu)) break;
       ++it;
-      wlo_b = bx.hasLo ? bx.llo / bx.slo : 0.0;
-      whi_b = bx.hasHi ? bx.lhi / bx.shi : 0.0;
-      wlo_c = cs.hasLo ? cs.llo / cs.slo : 0.0;
-      whi_c = cs.hasHi ? cs.lhi / cs.shi : 0.0;
-      wb = wlo_b + whi_b;
-      wc = wlo_c + whi_c;
-      fmask = 0ull;
-      fixed = false;
-    } else {  // PH_POLISH: set up the reduced problem of this round
-      if (rounds >= A.qp.polish) { phase = PH_DONE; continue; }
-      ++rounds;
-      fixed = (lane < n) && (alo_b || ahi_b);
-      zfix = alo_b ? bx.lo : (ahi_b ? bx.hi : 0.0);
-      if (!fixed) zfix = 0.0;
-      fmask = __ballot(fixed);
-      const bool act = (lane < NC) && (alo_c || ahi_c);
-      bnd_c = alo_c ? cs.lo : cs.hi;
+      const double wlo_b = bx.hasLo ? bx.llo / bx.slo : 0.0;
+      const double whi_b = bx.hasHi ? bx.lhi / bx.shi : 0.0;
+      const double wlo_c = cs.hasLo ? cs.llo / cs.slo : 0.0;
+      const double whi_c = cs.hasHi ? cs.lhi / cs.shi : 0.0;
       wave_sync();
-      if (lane < n) s.vz[lane] = zfix;
+      s.vc[lane] = (lane < NC) ? wlo_c + whi_c : 0.0;
       wave_sync();
-      // fixed-variable part of each active row, and its free-part norm for rho
-      const double gfix = grow_dot<N>(s, lane);
-      double gn2 = 0.0;
-      if (lane < NC) {
-#pragma unroll
-        for (int i = 0; i < n - 2; ++i) {
-          const double gi = ((fmask >> i) & 1ull) ? 0.0 : s.G[lane][i];
-          gn2 += gi * gi;
-        }
+      build_normal<N>(Mr, s, wlo_b + whi_b, lane);
+      if (!cholesky<N>(Mr, s, lane)) {
+        // The barrier weights lambda/s of the active set (~1/mu) have made the
+        // normal matrix numerically indefinite.  This happens only at the very
+        // end (mu ~ 1e-14); the iterate is then accurate enough for the
+        // active-set polish to identify and solve the exact optimum.
+        chol_fail = true;
+        near = res <= 1e-6 * scale && mu <= tol;
+        break;
       }
-      rho_c = act ? AL_RHO * hdiag_max / fmax(gn2, 1e-300) : 0.0;
-      if (act && gn2 <= 1e-28) { rho_c = 0.0; }  // row fully determined by fixed inputs
-      nu_c = 0.0;
-      bnd_c = act ? (bnd_c - gfix) : 0.0;  // b' = b - G_X zfix
-      base = (lane < n) ? -(gj + h_dot<N>(Hr, s)) : 0.0;
-      wb = 0.0;
-      wc = rho_c;
-    }
-
-    // ---- matrix build: Mr = row `lane` of H + diag(wb) + sum_r wc_r g_r g_r' ----
-    wave_sync();
-    s.vc[lane] = wc;
-    wave_sync();
-#pragma unroll
-    for (int i = 0; i < n; ++i) Mr[i] = Hr[i] + (i == lane ? wb : 0.0);
-#pragma unroll
-    for (int r = 0; r < NC; ++r) {
-      const double t = s.vc[r] * ((lane < n) ? s.G[r][lane] : 0.0);
-      const int nz = 2 * crow_stage<N>(r);
-#pragma unroll
-      for (int i = 0; i < nz; ++i) Mr[i] += t * s.G[r][i];
-    }
-    if (fmask) {  // reduced matrix: fixed rows/cols -> identity
-#pragma unroll
-      for (int i = 0; i < n; ++i) {
-        const bool fi = (fmask >> i) & 1ull;
-        Mr[i] = fixed ? (i == lane ? 1.0 : 0.0) : (fi ? 0.0 : Mr[i]);
-      }
-    }
-    if (lane >= n) {
-#pragma unroll
-      for (int i = 0; i < n; ++i) Mr[i] = 0.0;
-    }
-    if (!chol_rows<N>(Mr, s, lane)) { phase = PH_DONE; continue; }
-
-    // ---- solve passes ----------------------------------------------------------
-    const int npass = (phase == PH_PDIP) ? 2 : AL_MAX;
-    double zp = 0.0;
+      double sm = 0.0, pp1 = 0.0, pp2 = 0.0, pp3 = 0.0, pp4 = 0.0;
 #pragma unroll 1
-    for (int pass = 0; pass < npass; ++pass) {
-      double rhs;
-      double rclo_b = 0, rchi_b = 0, rclo_c = 0, rchi_c = 0;
-      if (phase == PH_PDIP) {
-        if (pass == 0) {  // predictor (affine scaling)
-          rclo_b = bx.slo * bx.llo; rchi_b = bx.shi * bx.lhi;
-          rclo_c = cs.slo * cs.llo; rchi_c = cs.shi * cs.lhi;
-        } else {          // Mehrotra corrector
-          const double aa = wave_min(fmin(
-              fmin(fmin(step_bound(bx.slo, pa1), step_bound(bx.llo, pa2)),
-                   fmin(step_bound(bx.shi, pa3), step_bound(bx.lhi, pa4))),
-              fmin(fmin(step_bound(cs.slo, pc1), step_bound(cs.llo, pc2)),
-                   fmin(step_bound(cs.shi, pc3), step_bound(cs.lhi, pc4)))));
-          const double mua =
-              wave_sum((bx.slo + aa * pa1) * (bx.llo + aa * pa2) + (bx.shi + aa * pa3) * (bx.lhi + aa * pa4) +
-                       (cs.slo + aa * pc1) * (cs.llo + aa * pc2) + (cs.shi + aa * pc3) * (cs.lhi + aa * pc4)) /
-              mtot;
-          const double sr = mua / mu;
-          const double sm = sr * sr * sr * mu;  // sigma * mu with sigma = (mu_aff / mu)^3
-          rclo_b = bx.slo * bx.llo + pa1 * pa2 - sm;
-          rchi_b = bx.shi * bx.lhi + pa3 * pa4 - sm;
-          rclo_c = cs.slo * cs.llo + pc1 * pc2 - sm;
-          rchi_c = cs.shi * cs.lhi + pc3 * pc4 - sm;
-        }
+      for (int pass = 0; pass < 2; ++pass) {
+        no_hoist();
+        // complementarity residuals: affine (pass 0), Mehrotra corrector (pass 1)
+        const double rclo_b = bx.slo * bx.llo + pp1 - sm, rchi_b = bx.shi * bx.lhi + pp2 - sm;
+        const double rclo_c = cs.slo * cs.llo + pp3 - sm, rchi_c = cs.shi * cs.lhi + pp4 - sm;
         const double eb = (bx.hasHi ? (-rchi_b / bx.shi - whi_b * rhi_b) : 0.0) +
                           (bx.hasLo ? (rclo_b / bx.slo + wlo_b * rlo_b) : 0.0);
         const double ec = (cs.hasHi ? (-rchi_c / cs.shi - whi_c * rhi_c) : 0.0) +
@@ -532,95 +533,169 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
         wave_sync();
         s.vc[lane] = (lane < NC) ? ec : 0.0;
         wave_sync();
-        rhs = (lane < n) ? (-rd - eb - gt_dot<N>(s, lane)) : 0.0;
-      } else {  // augmented-Lagrangian pass on the active set
+        const double rhs = (lane < n) ? (-rd - eb - gt_dot<N>(s, lane)) : 0.0;
+        const double dz = chol_solve<N>(Mr, s, rhs, lane);
         wave_sync();
-        s.vc[lane] = (lane < NC) ? (nu_c - rho_c * bnd_c) : 0.0;
+        s.vz[lane] = (lane < n) ? dz : 0.0;
         wave_sync();
-        rhs = (lane < n) ? (fixed ? zfix : (base - gt_dot<N>(s, lane))) : 0.0;
-      }
-
-      const double dz = chol_solve<N>(s, rhs, lane);  // the one solve site
-
-      wave_sync();
-      if (lane < n) s.vz[lane] = dz;
-      wave_sync();
-      const double dyc = grow_dot<N>(s, lane);
-      if (phase == PH_PDIP) {
-        const double dyb = dz;
-        const double d1 = bx.hasLo ? dyb + rlo_b : 0.0;
-        const double d2 = bx.hasLo ? (-rclo_b / bx.slo - wlo_b * (dyb + rlo_b)) : 0.0;
-        const double d3 = bx.hasHi ? rhi_b - dyb : 0.0;
-        const double d4 = bx.hasHi ? (-rchi_b / bx.shi - whi_b * (rhi_b - dyb)) : 0.0;
+        const double dyc = grow_dot<N>(s, lane);
+        const double d1 = bx.hasLo ? dz + rlo_b : 0.0;
+        const double d2 = bx.hasLo ? (-rclo_b / bx.slo - wlo_b * (dz + rlo_b)) : 0.0;
+        const double d3 = bx.hasHi ? rhi_b - dz : 0.0;
+        const double d4 = bx.hasHi ? (-rchi_b / bx.shi - whi_b * (rhi_b - dz)) : 0.0;
         const double e1 = cs.hasLo ? dyc + rlo_c : 0.0;
         const double e2 = cs.hasLo ? (-rclo_c / cs.slo - wlo_c * (dyc + rlo_c)) : 0.0;
         const double e3 = cs.hasHi ? rhi_c - dyc : 0.0;
         const double e4 = cs.hasHi ? (-rchi_c / cs.shi - whi_c * (rhi_c - dyc)) : 0.0;
+        const double amax = fmin(1.0, wave_min(fmin(fmin(fmin(step_bound(bx.slo, d1), step_bound(bx.llo, d2)),
+                                                         fmin(step_bound(bx.shi, d3), step_bound(bx.lhi, d4))),
+                                                    fmin(fmin(step_bound(cs.slo, e1), step_bound(cs.llo, e2)),
+                                                         fmin(step_bound(cs.shi, e3), step_bound(cs.lhi, e4))))));
         if (pass == 0) {
-          pa1 = d1; pa2 = d2; pa3 = d3; pa4 = d4;
-          pc1 = e1; pc2 = e2; pc3 = e3; pc4 = e4;
+          const double mua = wave_sum((bx.slo + amax * d1) * (bx.llo + amax * d2) +
+                                      (bx.shi + amax * d3) * (bx.lhi + amax * d4) +
+                                      (cs.slo + amax * e1) * (cs.llo + amax * e2) +
+                                      (cs.shi + amax * e3) * (cs.lhi + amax * e4)) / mtot;
+          const double sr = mua / mu;
+          sm = sr * sr * sr * mu;  // sigma * mu with sigma = (mu_aff / mu)^3
+          pp1 = d1 * d2; pp2 = d3 * d4; pp3 = e1 * e2; pp4 = e3 * e4;
         } else {
-          const double al = 0.99 * wave_min(fmin(
-                                       fmin(fmin(step_bound(bx.slo, d1), step_bound(bx.llo, d2)),
-                                            fmin(step_bound(bx.shi, d3), step_bound(bx.lhi, d4))),
-                                       fmin(fmin(step_bound(cs.slo, e1), step_bound(cs.llo, e2)),
-                                            fmin(step_bound(cs.shi, e3), step_bound(cs.lhi, e4)))));
-          if (lane < n) z += al * dz;
+          const double al = 0.99 * amax;
+          z = (lane < n) ? z + al * dz : z;
           bx.slo += al * d1; bx.llo += al * d2; bx.shi += al * d3; bx.lhi += al * d4;
           cs.slo += al * e1; cs.llo += al * e2; cs.shi += al * e3; cs.lhi += al * e4;
         }
-      } else {
-        zp = dz;
-        // dyc = G_r . zp (zp carries zfix on fixed lanes): multiplier update
-        const bool act = (lane < NC) && (alo_c || ahi_c) && rho_c > 0.0;
-        const double e = act ? (dyc - (alo_c ? cs.lo : cs.hi)) : 0.0;
-        nu_c += rho_c * e;
-        if (wave_max(fabs(e)) <= 1e-14 * scale) break;
       }
     }
-    if (phase == PH_PDIP) continue;
+  }
 
-    // ---- polish: KKT check of zp and active-set repair --------------------------
-    wave_sync();
-    if (lane < n) s.vz[lane] = zp;
-    s.vc[lane] = (lane < NC) ? nu_c : 0.0;
-    wave_sync();
-    const double grad = (lane < n) ? (h_dot<N>(Hr, s) + gj + gt_dot<N>(s, lane)) : 0.0;
-    const double ypc = grow_dot<N>(s, lane);
-    bool ok = true;
-    bool n_alo_b = alo_b, n_ahi_b = ahi_b, n_alo_c = alo_c, n_ahi_c = ahi_c;
-    if (lane < n) {
-      if (ahi_b && -grad < -ptol) { ok = false; n_ahi_b = false; }
-      if (alo_b && grad < -ptol) { ok = false; n_alo_b = false; }
-      if (!fixed) {
-        if (zp < bx.lo - ptol) { ok = false; n_alo_b = true; }
-        if (zp > bx.hi + ptol) { ok = false; n_ahi_b = true; }
+  // ---- Phase 2: active-set polish --------------------------------------------
+  // Crossover to the active set the interior point identified (lambda > s):
+  // box-active inputs are fixed (identity rows), active state rows are imposed
+  // with an augmented Lagrangian (P + rho C_A'C_A) whose multiplier update
+  // converges in a few solves with one factorisation.  The candidate is accepted
+  // when it is primal and dual feasible to ptol; otherwise ONE constraint is
+  // changed per round -- the most negative multiplier dropped, else the most
+  // violated constraint added (oracle/qp.py:polish uses the same rule with a
+  // direct KKT solve).  If no candidate certifies within qp.polish rounds, the
+  // converged interior-point iterate is kept.
+  bool polished = false, pchol_fail = false;
+  int rounds = 0;
+  if ((converged || near) && A.qp.polish > 0) {
+    constexpr double AL_RHO = 1e4;
+    constexpr int AL_MAX = 16;
+    const double ptol = 1e-9 * scale;
+    bool alo_b = bx.hasLo && bx.llo > bx.slo;
+    bool ahi_b = bx.hasHi && bx.lhi > bx.shi;
+    bool alo_c = cs.hasLo && cs.llo > cs.slo;
+    bool ahi_c = cs.hasHi && cs.lhi > cs.shi;
+#pragma unroll 1
+    for (int round = 0; round < A.qp.polish; ++round) {
+      no_hoist();
+      rounds = round + 1;
+      const bool fixed = (lane < n) && (alo_b || ahi_b);
+      const double zfix = fixed ? (alo_b ? bx.lo : bx.hi) : 0.0;
+      const uint64_t fmask = __ballot(fixed);
+      const bool act = (lane < NC) && (alo_c || ahi_c);
+      wave_sync();
+      s.vz[lane] = (lane < n) ? zfix : 0.0;
+      wave_sync();
+      // fixed-variable part of each active row, and its free-part norm for rho
+      const double gfix = grow_dot<N>(s, lane);
+      double gn2 = 0.0;
+      {
+        const int r = lane < NC ? lane : 0;
+#pragma unroll 2
+        for (int i = 0; i < 2 * (N - 1); ++i) {
+          const double gi = ((fmask >> i) & 1ull) ? 0.0 : s.G[r][i];
+          gn2 += gi * gi;
+        }
       }
-    }
-    if (lane < NC) {
-      if (ahi_c && nu_c < -ptol) { ok = false; n_ahi_c = false; }
-      if (alo_c && -nu_c < -ptol) { ok = false; n_alo_c = false; }
-      if (!(alo_c || ahi_c)) {
-        if (cs.hasLo && ypc < cs.lo - ptol) { ok = false; n_alo_c = true; }
-        if (cs.hasHi && ypc > cs.hi + ptol) { ok = false; n_ahi_c = true; }
-      } else if (fabs(ypc - (alo_c ? cs.lo : cs.hi)) > ptol) {
-        ok = false;  // equality not met (e.g. a row left fully fixed by the inputs)
-        n_alo_c = n_ahi_c = false;
+      const double rho_c = (act && gn2 > 1e-28) ? AL_RHO * hdiag_max / gn2 : 0.0;
+      const double bnd_c = act ? ((alo_c ? cs.lo : cs.hi) - gfix) : 0.0;  // b' = b - G_X zfix
+      const double base = (lane < n) ? -(gj + h_dot<N>(s, lane)) : 0.0;
+      wave_sync();
+      s.vc[lane] = rho_c;
+      wave_sync();
+      build_normal<N>(Mr, s, 0.0, lane);
+#pragma unroll
+      for (int i = 0; i < n; ++i) {  // reduced matrix: fixed rows/cols -> identity
+        const bool fi = (fmask >> i) & 1ull;
+        Mr[i] = fixed ? (i == lane ? 1.0 : 0.0) : (fi ? 0.0 : Mr[i]);
       }
-    }
-    if (__ballot(!ok) == 0ull) {
-      z = zp;
-      polished = true;
-      phase = PH_DONE;
-    } else {
-      alo_b = n_alo_b; ahi_b = n_ahi_b; alo_c = n_alo_c; ahi_c = n_ahi_c;
+      if (!cholesky<N>(Mr, s, lane)) {
+        pchol_fail = true;
+        break;
+      }
+      double nu_c = 0.0, zp = 0.0, emax = 0.0;
+#pragma unroll 1
+      for (int pass = 0; pass < AL_MAX; ++pass) {
+        no_hoist();
+        wave_sync();
+        s.vc[lane] = (lane < NC) ? (nu_c - rho_c * bnd_c) : 0.0;
+        wave_sync();
+        const double rhs = (lane < n) ? (fixed ? zfix : (base - gt_dot<N>(s, lane))) : 0.0;
+        zp = chol_solve<N>(Mr, s, rhs, lane);
+        wave_sync();
+        s.vz[lane] = (lane < n) ? zp : 0.0;
+        wave_sync();
+        // G_r . zp (zp carries zfix on fixed lanes): multiplier update
+        const double yr = grow_dot<N>(s, lane);
+        const bool al_act = act && rho_c > 0.0;
+        const double e = al_act ? (yr - (alo_c ? cs.lo : cs.hi)) : 0.0;
+        nu_c += rho_c * e;
+        emax = wave_max(fabs(e));
+        if (emax <= 1e-14 * scale) break;
+      }
+      // KKT check of zp
+      wave_sync();
+      s.vz[lane] = (lane < n) ? zp : 0.0;
+      s.vc[lane] = (lane < NC) ? nu_c : 0.0;
+      wave_sync();
+      const double grad = (lane < n) ? (h_dot<N>(s, lane) + gj + gt_dot<N>(s, lane)) : 0.0;
+      const double ypc = grow_dot<N>(s, lane);
+      // dual violations (> 0 is wrong-signed): box multiplier of an active bound is
+      // -grad (upper) / grad (lower); state-row multiplier is nu (upper) / -nu (lower)
+      const double dv_b = (lane < n) ? (ahi_b ? grad : (alo_b ? -grad : -1.0)) : -1.0;
+      const double dv_c = (lane < NC) ? (ahi_c ? -nu_c : (alo_c ? nu_c : -1.0)) : -1.0;
+      // primal violations of the inactive constraints
+      const double pv_b = (lane < n && !fixed) ? fmax(bx.lo - zp, zp - bx.hi) : -1.0;
+      const double pv_c = (lane < NC && !(alo_c || ahi_c))
+                              ? fmax(cs.hasLo ? cs.lo - ypc : -1.0, cs.hasHi ? ypc - cs.hi : -1.0)
+                              : -1.0;
+      const double dmax = wave_max(fmax(dv_b, dv_c));
+      const double pmax = wave_max(fmax(pv_b, pv_c));
+      if (dmax <= ptol && pmax <= ptol) {
+        if (emax <= ptol) {
+          z = (lane < n) ? zp : z;
+          polished = true;
+        }
+        break;  // certified, or the equality solve did not converge: keep the IPM iterate
+      }
+      // change one constraint: the lowest lane holding the worst violation
+      const bool dual = dmax > ptol;
+      const double worst = dual ? dmax : pmax;
+      const double vb = dual ? dv_b : pv_b, vcr = dual ? dv_c : pv_c;
+      const uint64_t who = __ballot(fmax(vb, vcr) == worst);
+      const int sel = __builtin_ffsll((long long)who) - 1;
+      if (lane == sel) {
+        if (vb >= vcr) {  // box constraint of input `lane`
+          if (dual) { alo_b = false; ahi_b = false; }
+          else if (zp < bx.lo) alo_b = true;
+          else ahi_b = true;
+        } else {          // state row `lane`
+          if (dual) { alo_c = false; ahi_c = false; }
+          else if (ypc < cs.lo) alo_c = true;
+          else ahi_c = true;
+        }
+      }
     }
   }
 
   // ---- outputs -------------------------------------------------------------------
   int32_t st;
   if (!finite) st = VC_NONFINITE;
-  else if (polished || (converged && A.qp.polish <= 0)) st = VC_SOLVED;
+  else if (polished || converged) st = VC_SOLVED;
   else st = VC_MAX_ITER;
   if (!finite) z = 0.0;
   wave_sync();
@@ -633,11 +708,19 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
   if (lane == 0) {
     A.status[b] = st;
     A.iters[b] = it;
+    if (A.diag) {
+      A.diag[(size_t)b * 4 + 0] = last_res / scale;
+      A.diag[(size_t)b * 4 + 1] = last_mu / scale;
+      A.diag[(size_t)b * 4 + 2] = double((chol_fail ? 1 : 0) | (converged ? 2 : 0) | (polished ? 4 : 0) |
+                                         (pchol_fail ? 8 : 0));
+      A.diag[(size_t)b * 4 + 3] = double(rounds);
+    }
   }
   // x* = xbar + G dz via the linearised recursion, lanes 0..5 own components
   double dx[KIN_NX] = {0, 0, 0, 0, 0, 0};
   double* xo = A.x_out + (size_t)b * (N + 1) * KIN_NX;
   if (lane < KIN_NX) xo[lane] = s.xb[0][lane];
+#pragma unroll 1
   for (int k = 0; k < N; ++k) {
     const double q = s.jac[k][0], qv = s.jac[k][1], qey = s.jac[k][2], qep = s.jac[k][3];
     const double h = s.ds[k], a = s.ub[2 * k], w = s.ub[2 * k + 1];
@@ -660,13 +743,10 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
   }
 }
 
-}  // namespace vc
-
 // ---- host launcher ---------------------------------------------------------------
-namespace vc {
 size_t kin_ltv_smem_bytes(int N) {
   switch (N) {
-    case 20: return sizeof(KinShared<20>);
+    case 20: return sizeof(Smem<20>);
     default: return 0;
   }
 }
@@ -675,10 +755,11 @@ hipError_t launch_kin_ltv(const KinLtvArgs& a, int N, hipStream_t stream) {
   if (a.B <= 0) return hipSuccess;
   switch (N) {
     case 20:
-      hipLaunchKernelGGL(kin_ltv_kernel<20>, dim3(a.B), dim3(64), sizeof(KinShared<20>), stream, a);
+      hipLaunchKernelGGL(kin_ltv_kernel<20>, dim3(a.B), dim3(64), 0, stream, a);
       return hipGetLastError();
     default:
       return hipErrorInvalidValue;
   }
 }
+
 }  // namespace vc

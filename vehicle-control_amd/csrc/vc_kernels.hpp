@@ -20,6 +20,7 @@ struct KinLtvArgs {
   double* u0;           // [B][2]
   int32_t* status;      // [B]
   int32_t* iters;       // [B]
+  double* diag;         // [B][4] optional solver diagnostics (vc_solve_diag), may be null
   double* H_out;        // [B][2N][2N]  (mode 1 only)
   double* g_out;        // [B][2N]      (mode 1 only)
   int mode;             // 0 = full solve, 1 = stop after condensing and write H, g

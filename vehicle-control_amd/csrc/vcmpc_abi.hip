@@ -175,6 +175,11 @@ int vc_synchronize(vc_ctx* c) {
 
 int vc_solve(vc_ctx* c, int B, const void* x0, const void* kappa, const void* ds, void* xbar, void* ubar, void* u0,
              int32_t* status, int32_t* iters, int flags) {
+  return vc_solve_diag(c, B, x0, kappa, ds, xbar, ubar, u0, status, iters, nullptr, flags);
+}
+
+int vc_solve_diag(vc_ctx* c, int B, const void* x0, const void* kappa, const void* ds, void* xbar, void* ubar,
+                  void* u0, int32_t* status, int32_t* iters, void* diag, int flags) {
   if (int r = check_common(c, B, flags)) return r;
   if (!kin_solve_built(c))
     return fail(c, VC_E_UNSUPPORTED, "vc_solve: model=%d dtype=%d N=%d not built (kinematic fp64 N=20 is)", c->model,
@@ -197,7 +202,8 @@ int vc_solve(vc_ctx* c, int B, const void* x0, const void* kappa, const void* ds
              {nullptr, xbar, (size_t)B * (N + 1) * nx * 8, nullptr},
              {nullptr, u0, (size_t)B * nu * 8, nullptr},
              {nullptr, status, (size_t)B * 4, nullptr},
-             {nullptr, iters, (size_t)B * 4, nullptr}};
+             {nullptr, iters, (size_t)B * 4, nullptr},
+             {nullptr, diag, diag ? (size_t)B * 4 * 8 : 0, nullptr}};
     if (int r = stage(c, slots)) return r;
     a.x0 = (const double*)slots[0].dev;
     a.kappa = (const double*)slots[1].dev;
@@ -208,6 +214,7 @@ int vc_solve(vc_ctx* c, int B, const void* x0, const void* kappa, const void* ds
     a.u0 = (double*)slots[5].dev;
     a.status = (int32_t*)slots[6].dev;
     a.iters = (int32_t*)slots[7].dev;
+    a.diag = diag ? (double*)slots[8].dev : nullptr;
   } else {
     a.x0 = (const double*)x0;
     a.kappa = (const double*)kappa;
@@ -218,6 +225,7 @@ int vc_solve(vc_ctx* c, int B, const void* x0, const void* kappa, const void* ds
     a.u0 = (double*)u0;
     a.status = status;
     a.iters = iters;
+    a.diag = (double*)diag;
   }
   VC_HIP(c, vc::launch_kin_ltv(a, N, c->stream));
   if (flags == VC_HOST_PTRS) return unstage(c, slots);

@@ -71,6 +71,7 @@ PROTOTYPES = {
     "vc_set_stream": (C.c_int, [_vp, _vp]),
     "vc_synchronize": (C.c_int, [_vp]),
     "vc_solve": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int]),
+    "vc_solve_diag": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int]),
     "vc_rollout": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, C.c_int]),
     "vc_linearize": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int]),
     "vc_condense": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int]),
@@ -87,6 +88,14 @@ def load_library(path: str | None = None) -> C.CDLL:
     if _LIB is not None and path is None:
         return _LIB
     p = path or LIB_PATH
+    # One HIP runtime per process: torch ships its own libamdhip64.so.7 (same
+    # SONAME as /opt/rocm's).  Loading torch first makes the dynamic loader bind
+    # libvcmpc.so to that copy; loaded the other way round, two runtimes coexist
+    # and torch's device discovery fails.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(p):
         raise ImportError(
             f"{p} not found: build it with `make -C vehicle-control_amd/csrc` "

@@ -15,7 +15,7 @@ from . import _abi
 CONFIG_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "config")
 
 # The build's LTV-QP contract defaults (no reference counterpart).
-QP_DEFAULTS = {"prox": 1e-4, "tol": 1e-10, "max_iter": 40, "polish": 6}
+QP_DEFAULTS = {"prox": 1e-4, "tol": 1e-10, "max_iter": 40, "polish": 10}
 
 
 class AttrDict(dict):

@@ -62,11 +62,30 @@ class BatchedKinematicMPC(Controller):
         self.iters = np.zeros(self.B, np.int32)
 
     def command(self, states):
-        """states[B, ns] -> actions[B, na] (u*_0 of every problem)."""
+        """states[B, ns] -> actions[B, na] (u*_0 of every problem).
+
+        The warm start is the previous solution, unshifted, as in the reference
+        (kinematic_mpc.py:175-176), projected onto the input box first: the LTV-QP
+        linearises around the warm-start rollout, and the reference's initial guess
+        1 + U[0, 1) (kinematic_mpc.py:65-67) is far outside w_max = 0.4 (IPOPT
+        recovers from that by globalisation; one QP step cannot).  A problem that
+        does not come back VC_SOLVED (e.g. linearised state rows infeasible) keeps
+        its projected warm start as prediction and applies its first action --
+        the reference's simulator instead swallows the solver exception
+        (racing.py:416-423)."""
         x0 = np.ascontiguousarray(np.asarray(states, np.float64).reshape(self.B, self.ns))
         ds, kappa = horizon_params(x0[:, IS], self.state_prediction[:, IV, :], self.dt, self.car.track.k)
         ubar = np.ascontiguousarray(np.swapaxes(self.action_prediction, 1, 2))
+        ic = self.config["input_constraints"]
+        np.clip(ubar[..., 0], ic["a_min"], ic["a_max"], out=ubar[..., 0])
+        np.clip(ubar[..., 1], ic["w_min"], ic["w_max"], out=ubar[..., 1])
+        warm = ubar.copy()
         u0, xbar, ustar, status, iters = self.ctx.solve(x0, kappa, ds, ubar)
+        bad = status != 0
+        if bad.any():
+            ustar[bad] = warm[bad]
+            u0[bad] = warm[bad, 0]
+            xbar[bad] = self.ctx.rollout(x0[bad], np.ascontiguousarray(warm[bad]), kappa[bad], ds[bad])
         self.action_prediction = np.swapaxes(ustar, 1, 2).copy()
         self.state_prediction = np.swapaxes(xbar, 1, 2).copy()
         self.status, self.iters = status, iters

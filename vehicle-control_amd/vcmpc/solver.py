@@ -101,9 +101,11 @@ class Context:
         return B
 
     # -- entry points -------------------------------------------------------------
-    def solve(self, x0, kappa, ds, ubar, xbar=None, u0=None, status=None, iters=None):
+    def solve(self, x0, kappa, ds, ubar, xbar=None, u0=None, status=None, iters=None, diag=None):
         """One LTV-MPC step (``vc_solve``).  ``ubar`` is the warm start and is
-        overwritten with u*; returns (u0, xbar, ubar, status, iters)."""
+        overwritten with u*; returns (u0, xbar, ubar, status, iters).  With
+        ``diag=True`` (or a [B, 4] buffer) it calls ``vc_solve_diag`` and returns
+        the per-problem solver diagnostics as a sixth element."""
         B, N, nx, f = self._batch(x0), self.N, self.nx, _NP_DT[self.dtype]
         if _is_torch(x0):
             import torch
@@ -117,11 +119,17 @@ class Context:
             u0 = np.empty((B, NU), f) if u0 is None else u0
             status = np.empty((B,), np.int32) if status is None else status
             iters = np.empty((B,), np.int32) if iters is None else iters
-        (px0, pk, pds, pxb, pub, pu0, pst, pit), flags = self._marshal(
-            [x0, kappa, ds, xbar, ubar, u0, status, iters],
-            [(B, nx), (B, N), (B, N), (B, N + 1, nx), (B, N, NU), (B, NU), (B,), (B,)],
-            [f, f, f, f, f, f, np.int32, np.int32])
-        self._check(self.lib.vc_solve(self._h, B, px0, pk, pds, pxb, pub, pu0, pst, pit, flags))
+        bufs = [x0, kappa, ds, xbar, ubar, u0, status, iters]
+        shapes = [(B, nx), (B, N), (B, N), (B, N + 1, nx), (B, N, NU), (B, NU), (B,), (B,)]
+        dts = [f, f, f, f, f, f, np.int32, np.int32]
+        if diag is not None and diag is not False:
+            if diag is True:
+                diag = self._like(x0, (B, 4))
+            ptrs, flags = self._marshal(bufs + [diag], shapes + [(B, 4)], dts + [f])
+            self._check(self.lib.vc_solve_diag(self._h, B, *ptrs, flags))
+            return u0, xbar, ubar, status, iters, diag
+        ptrs, flags = self._marshal(bufs, shapes, dts)
+        self._check(self.lib.vc_solve(self._h, B, *ptrs, flags))
         return u0, xbar, ubar, status, iters
 
     def rollout(self, x0, ubar, kappa, ds):
