@@ -88,6 +88,8 @@ typedef struct vc_kin_mpc {
 typedef struct vc_qp {
   double prox;      /* proximal weight: + prox * ||u - ubar||^2 */
   double tol;       /* interior-point stopping tolerance (scaled) */
+  double trust_a;   /* trust region |u_a - ubar_a| <= trust_a (0 = off) */
+  double trust_w;   /* trust region |u_w - ubar_w| <= trust_w (0 = off) */
   int32_t max_iter; /* interior-point iteration cap */
   int32_t polish;   /* active-set polish rounds after the interior point (0 = off) */
 } vc_qp;

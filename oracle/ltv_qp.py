@@ -29,6 +29,8 @@ Constraints:
   a_min <= a_n <= a_max, w_min <= w_n <= w_max, n = 0..N-1  kinematic_mpc.py:88-93
   v_n >= v_min, delta_min <= delta_n <= delta_max, n = 1..N-1  kinematic_mpc.py:80-85
   (n = 0 is the fixed initial state, kinematic_mpc.py:23-25: a constant, dropped.)
+  optional trust region |du_n| <= (trust_a, trust_w) tightening the input boxes
+  (SQP globalisation used by the closed-loop controller; 0 = off, the default).
 """
 from __future__ import annotations
 
@@ -55,6 +57,7 @@ def kin_weights(cfg: dict) -> dict:
         delta_min=float(sc["delta_min"]), delta_max=float(sc["delta_max"]),
         ey_min=float(sc["ey_min"]), ey_max=float(sc["ey_max"]),
         prox=float(qp.get("prox", 1e-4)),
+        trust_a=float(qp.get("trust_a", 0.0)), trust_w=float(qp.get("trust_w", 0.0)),
     )
 
 
@@ -134,11 +137,15 @@ def kin_qp(x0, ubar, kappa, ds, L, W):
     # inequalities C dz <= d
     rows, rhs = [], []
     I = np.eye(n)
+    tr = {IA: W.get("trust_a", 0.0), IW: W.get("trust_w", 0.0)}
     for k in range(N):
         for j, (lo, hi) in ((IA, (W["a_min"], W["a_max"])), (IW, (W["w_min"], W["w_max"]))):
             e = np.broadcast_to(I[2 * k + j], (B, n))
-            rows.append(e); rhs.append(hi - ubar[:, k, j])
-            rows.append(-e); rhs.append(ubar[:, k, j] - lo)
+            up, dn = hi - ubar[:, k, j], ubar[:, k, j] - lo
+            if tr[j] > 0:  # trust region |du| <= tr (SQP globalisation; 0 = off)
+                up, dn = np.minimum(up, tr[j]), np.minimum(dn, tr[j])
+            rows.append(e); rhs.append(up)
+            rows.append(-e); rhs.append(dn)
     for k in range(1, N):
         rows.append(-G[:, k, IV]); rhs.append(xbar[:, k, IV] - W["v_min"])
         rows.append(G[:, k, ID]); rhs.append(W["delta_max"] - xbar[:, k, ID])

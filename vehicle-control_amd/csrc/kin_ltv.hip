@@ -430,6 +430,11 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
     const double u = (lane < n) ? s.ub[lane] : 0.0;
     bx.lo = (isw ? W.w_min : W.a_min) - u;
     bx.hi = (isw ? W.w_max : W.a_max) - u;
+    const double tr = isw ? A.qp.trust_w : A.qp.trust_a;  // trust region (SQP globalisation), 0 = off
+    if (tr > 0.0) {
+      bx.lo = fmax(bx.lo, -tr);
+      bx.hi = fmin(bx.hi, tr);
+    }
     bx.hasLo = bx.hasHi = (lane < n);
     const int st = crow_stage<N>(lane < NC ? lane : 0);
     if (lane < N - 1) {

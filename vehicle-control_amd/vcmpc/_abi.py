@@ -43,7 +43,8 @@ class vc_kin_mpc(C.Structure):
 
 
 class vc_qp(C.Structure):
-    _fields_ = [("prox", C.c_double), ("tol", C.c_double), ("max_iter", C.c_int32), ("polish", C.c_int32)]
+    _fields_ = [("prox", C.c_double), ("tol", C.c_double), ("trust_a", C.c_double), ("trust_w", C.c_double),
+                ("max_iter", C.c_int32), ("polish", C.c_int32)]
 
 
 class vc_params(C.Structure):

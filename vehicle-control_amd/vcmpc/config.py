@@ -15,7 +15,7 @@ from . import _abi
 CONFIG_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "config")
 
 # The build's LTV-QP contract defaults (no reference counterpart).
-QP_DEFAULTS = {"prox": 1e-4, "tol": 1e-10, "max_iter": 40, "polish": 10}
+QP_DEFAULTS = {"prox": 1e-4, "tol": 1e-10, "max_iter": 40, "polish": 10, "trust_a": 0.0, "trust_w": 0.0}
 
 
 class AttrDict(dict):
@@ -69,8 +69,8 @@ def qp_struct(cfg=None) -> _abi.vc_qp:
     q = dict(QP_DEFAULTS)
     if cfg is not None and cfg.get("qp") is not None:
         q.update(cfg["qp"])
-    return _abi.vc_qp(prox=float(q["prox"]), tol=float(q["tol"]), max_iter=int(q["max_iter"]),
-                      polish=int(q["polish"]))
+    return _abi.vc_qp(prox=float(q["prox"]), tol=float(q["tol"]), trust_a=float(q["trust_a"]),
+                      trust_w=float(q["trust_w"]), max_iter=int(q["max_iter"]), polish=int(q["polish"]))
 
 
 def dyn_car_struct(cfg, tyre: str = "fiala") -> _abi.vc_dyn_car:

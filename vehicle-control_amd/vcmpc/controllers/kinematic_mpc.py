@@ -22,6 +22,12 @@ from ..solver import Context
 from .controller import Controller
 
 IV, IS = 0, 2
+# Real-time-iteration globalisation of the closed-loop controller: a trust region
+# on the per-step input change (vc_qp.trust_a / trust_w).  The reference solves
+# each NLP to convergence with IPOPT's line search; one LTV-QP step per control
+# step linearised around a far-off warm start can otherwise overshoot into a
+# region where the linearisation is meaningless (cos(epsi) -> 0).
+RTI_TRUST = {"trust_a": 1.0, "trust_w": 0.1}
 
 
 def horizon_params(s0, v_pred, mpc_dt, k_of_s):
@@ -51,8 +57,12 @@ class BatchedKinematicMPC(Controller):
         self.B = int(batch)
         if config.get("obstacles", False):
             raise NotImplementedError("obstacle barrier terms (kinematic_mpc.py:130-133) are SURVEY 8(f) row 4")
+        qp = dict(RTI_TRUST)
+        qp.update(config.get("qp") or {})
+        cfg = dict(config)
+        cfg["qp"] = qp
         self.ctx = Context(model=_abi.VC_MODEL_KINEMATIC, N=self.N, max_batch=self.B, dtype=_abi.VC_F64,
-                           device=device, params=make_params(kin_car=car.config, kin_mpc=config))
+                           device=device, params=make_params(kin_car=car.config, kin_mpc=cfg))
         # warm starts: kinematic_mpc.py:64-68 (zeros, v = 0.1; actions 1 + U[0,1) seeded)
         rng = np.random.RandomState(seed) if seed is not None else np.random
         self.state_prediction = np.zeros((self.B, self.ns, self.N + 1))
@@ -79,13 +89,14 @@ class BatchedKinematicMPC(Controller):
         ic = self.config["input_constraints"]
         np.clip(ubar[..., 0], ic["a_min"], ic["a_max"], out=ubar[..., 0])
         np.clip(ubar[..., 1], ic["w_min"], ic["w_max"], out=ubar[..., 1])
-        warm = ubar.copy()
         u0, xbar, ustar, status, iters = self.ctx.solve(x0, kappa, ds, ubar)
         bad = status != 0
         if bad.any():
-            ustar[bad] = warm[bad]
-            u0[bad] = warm[bad, 0]
-            xbar[bad] = self.ctx.rollout(x0[bad], np.ascontiguousarray(warm[bad]), kappa[bad], ds[bad])
+            # retry from the neutral warm start u = 0 (steering held, speed held):
+            # its linearised state rows are feasible at dz = 0 whenever x0 is
+            idx = np.nonzero(bad)[0]
+            r = self.ctx.solve(x0[idx], kappa[idx], ds[idx], np.zeros((len(idx), self.N, self.na)))
+            u0[idx], xbar[idx], ustar[idx], status[idx], iters[idx] = r
         self.action_prediction = np.swapaxes(ustar, 1, 2).copy()
         self.state_prediction = np.swapaxes(xbar, 1, 2).copy()
         self.status, self.iters = status, iters
