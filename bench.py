@@ -28,6 +28,32 @@ N_HORIZON, NX, NU = 20, 6, 2
 # u* + x* + u0 (fp64) + status + iters.
 BYTES_PER_SOLVE = (NX + N_HORIZON + N_HORIZON + N_HORIZON * NU) * 8 + \
                   (N_HORIZON * NU + (N_HORIZON + 1) * NX + NU) * 8 + 8
+# Algorithmic fp64 FLOPs of the fused kernel (DESIGN.md "Arithmetic"): forward
+# sweep (rollout, Jacobians, rank-1 Hessian build) once, then per interior-point
+# iteration the normal-matrix build sum_r w_r g_r g_r' over the lower-triangular
+# constraint rows, an n^3/3 Cholesky, two triangular-solve pairs and the
+# mat-vecs; the polish costs about one iteration per round.
+N_DEC = NU * N_HORIZON
+NC_ROWS = 2 * (N_HORIZON - 1)
+FLOP_SWEEP = N_HORIZON * (2 * N_DEC * N_DEC + 200) + 3 * 2 * N_DEC * N_DEC
+FLOP_ITER = (2 * N_DEC * sum(2 * (1 + r % (N_HORIZON - 1)) for r in range(NC_ROWS))  # build
+             + N_DEC ** 3 // 3 + 2 * 2 * N_DEC * N_DEC                                  # Cholesky, 2 solves
+             + 4 * (2 * NC_ROWS * N_DEC) + 2 * 2 * N_DEC * N_DEC)                       # mat-vecs
+FP64_VALU_PEAK = 78.6  # TFLOP/s
+PMC_PROFILE = os.path.join(ROOT, "profiles", "r01", "pmc_b1024.json")
+
+
+def pmc_traffic(batch):
+    """HBM bytes per launch from the committed rocprofv3 PMC passes (FETCH_SIZE +
+    WRITE_SIZE, scripts/pmc_profile.sh) when they were taken at this batch."""
+    try:
+        with open(PMC_PROFILE) as f:
+            p = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if p.get("batch") != batch:
+        return None
+    return p["derived"]["traffic_bytes_per_launch"]
 
 
 def parse():
@@ -123,11 +149,22 @@ def main():
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
     st = status.cpu().numpy()
     it = iters.cpu().numpy()
+    # PCIe-inclusive rate of the host-pointer path (VC_HOST_PTRS: H2D, solve, D2H)
+    # -- reported beside `value`, never as it (DESIGN.md "Measurement")
+    ctx.set_stream(None)
+    host = {k: v.copy() for k, v in data.items()}
+    ctx.solve(host["x0"], host["kappa"], host["ds"], host["ubar"].copy())
+    reps = max(3, min(args.steps, 10))
+    th = time.perf_counter()
+    for _ in range(reps):
+        ctx.solve(host["x0"], host["kappa"], host["ds"], host["ubar"].copy())
+    host_rate = B * reps / (time.perf_counter() - th)
     solves, elapsed_max, kern_ms_max = dist.aggregate(float(B * args.steps), elapsed, kern_ms, dev)
 
     if rank == 0:
         value = solves / elapsed_max
         achieved = BYTES_PER_SOLVE * B / (kern_ms / 1e3) / 1e9
+        flops = FLOP_SWEEP + (float(it.mean()) + 1.0) * FLOP_ITER  # +1: the polish round(s)
         out = {
             "metric": "MPC solves/sec (batched, N=20)",
             "value": value,
@@ -145,9 +182,15 @@ def main():
                        "batch_per_gpu": B, "global_batch": B * world, "horizon": N_HORIZON,
                        "parallelism": f"dp{world} (independent shards)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(B),
+                         "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE+WRITE_SIZE, profiles/r01)",
+                         "algorithmic_bytes": BYTES_PER_SOLVE * B,
                          "kernel": "kin_ltv_kernel<20>", "kernel_ms": kern_ms,
-                         "bytes_per_solve": BYTES_PER_SOLVE},
+                         "bytes_per_solve": BYTES_PER_SOLVE,
+                         "valu_fp64": {"flops_per_solve": flops, "achieved": flops * B / (kern_ms / 1e3) / 1e12,
+                                       "peak": FP64_VALU_PEAK, "unit": "TFLOP/s",
+                                       "frac": flops * B / (kern_ms / 1e3) / 1e12 / FP64_VALU_PEAK}},
+            "host_ptr_solves_per_s": host_rate,
             "solver": {"solved_frac": float((st == 0).mean()), "iters_mean": float(it.mean()),
                        "iters_max": int(it.max())},
         }

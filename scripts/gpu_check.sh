@@ -24,6 +24,6 @@ run pytest_gpu_$TAG.log 600 python -m pytest tests -m gpu -x -q
 run smoke_$TAG.log 300 python -c "import __graft_entry__ as g; g.smoke()"
 run bench_$TAG.log 600 python bench.py --steps "$STEPS" --warmup 3
 cd /tmp
-run rocprof_$TAG.log 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run -- \
+run rocprof_$TAG.log 600 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof_$TAG" -o run -- \
     python3 "$ROOT/bench.py" --steps "$STEPS" --warmup 3 --no-cpu-baseline
 find "$OUT/prof_$TAG" -name "*stats*" | head
