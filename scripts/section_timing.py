@@ -1,0 +1,51 @@
+"""Per-section cycle counts of the fused kernel (timing build: make -C
+vehicle-control_amd/csrc timing).  Run with VCMPC_LIB pointing at
+libvcmpc_timing.so.  Prints mean s_memtime cycles per problem for each section,
+and per interior-point iteration."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "vehicle-control_amd"))
+os.environ.setdefault("VCMPC_LIB", os.path.join(ROOT, "vehicle-control_amd", "vcmpc", "libvcmpc_timing.so"))
+from vcmpc import Context, _abi, make_params  # noqa: E402
+from vcmpc.config import load_config  # noqa: E402
+from vcmpc.workload import kinematic_batch  # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+tol = float(sys.argv[2]) if len(sys.argv) > 2 else 1e-10
+names = ["sweep", "setup", "resid", "build", "chol", "solve", "update", "polish", "out"]
+dev = torch.device("cuda:0")
+d = kinematic_batch(B, seed=31)
+t = {k: torch.from_numpy(v).to(dev) for k, v in d.items()}
+p = make_params(kin_car=load_config("kinematic_car"), kin_mpc=load_config("kinematic_mpc"))
+p.qp.tol = tol
+with Context(N=20, max_batch=B, params=p) as c:
+    B_, N = B, 20
+    xbar = torch.empty((B, N + 1, 6), dtype=torch.float64, device=dev)
+    u0 = torch.empty((B, 2), dtype=torch.float64, device=dev)
+    st = torch.empty((B,), dtype=torch.int32, device=dev)
+    it = torch.empty((B,), dtype=torch.int32, device=dev)
+    diag = torch.zeros((B, 13), dtype=torch.float64, device=dev)
+    ptrs = [C for C in (t["x0"], t["kappa"], t["ds"], xbar, t["ubar"].clone(), u0, st, it, diag)]
+    import ctypes as C
+    for _ in range(2):
+        ub = t["ubar"].clone()
+        rc = c.lib.vc_solve_diag(c._h, B, *[C.c_void_p(x.data_ptr()) for x in
+                                            (t["x0"], t["kappa"], t["ds"], xbar, ub, u0, st, it, diag)],
+                                 _abi.VC_DEVICE_PTRS)
+        assert rc == 0
+        c.synchronize()
+    dg = diag.cpu().numpy()
+    its = it.cpu().numpy().astype(float)
+    cyc = dg[:, 4:]
+    tot = cyc.sum(1)
+    print(f"B={B} tol={tol:g}: solved {(st.cpu().numpy() == 0).mean():.4f} iters mean {its.mean():.2f} max {its.max():.0f} "
+          f"polish rounds mean {dg[:, 3].mean():.2f}")
+    print(f"  total stamped cycles/problem: mean {tot.mean():.0f}  max {tot.max():.0f}")
+    for i, nm in enumerate(names):
+        per_it = cyc[:, i].sum() / max(its.sum(), 1) if nm in ("resid", "build", "chol", "solve") else float("nan")
+        print(f"  {nm:7s} mean {cyc[:, i].mean():10.0f}  ({100 * cyc[:, i].mean() / tot.mean():5.1f} %)  per IPM iter {per_it:9.0f}")

@@ -39,26 +39,37 @@ namespace vc {
 namespace {
 
 // ---- wave-level helpers ----------------------------------------------------
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-  return v;
-}
-__device__ __forceinline__ double wave_min(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
-  return v;
-}
 // value of `v` in lane `src` (src wave-uniform)
 __device__ __forceinline__ double lane_bcast(double v, int src) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), src);
   const int hi = __builtin_amdgcn_readlane(__double2hiint(v), src);
   return __hiloint2double(hi, lo);
+}
+// v of lane (i - K) within each 16-lane DPP row, `ident` where that leaves the row
+template <int K>
+__device__ __forceinline__ double dpp_row_shr(double v, double ident) {
+  const int lo = __builtin_amdgcn_update_dpp(__double2loint(ident), __double2loint(v), 0x110 + K, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(__double2hiint(ident), __double2hiint(v), 0x110 + K, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+// Wave-wide reductions: a DPP prefix within each 16-lane row (VALU latency, no
+// LDS round trip), then the four row totals combined from SGPR readlanes.
+template <typename Op>
+__device__ __forceinline__ double wave_reduce(double v, double ident, Op op) {
+  v = op(v, dpp_row_shr<1>(v, ident));
+  v = op(v, dpp_row_shr<2>(v, ident));
+  v = op(v, dpp_row_shr<4>(v, ident));
+  v = op(v, dpp_row_shr<8>(v, ident));
+  return op(op(lane_bcast(v, 15), lane_bcast(v, 31)), op(lane_bcast(v, 47), lane_bcast(v, 63)));
+}
+__device__ __forceinline__ double wave_sum(double v) {
+  return wave_reduce(v, 0.0, [](double a, double b) { return a + b; });
+}
+__device__ __forceinline__ double wave_max(double v) {
+  return wave_reduce(v, -__builtin_inf(), [](double a, double b) { return fmax(a, b); });
+}
+__device__ __forceinline__ double wave_min(double v) {
+  return wave_reduce(v, __builtin_inf(), [](double a, double b) { return fmin(a, b); });
 }
 // one-wave workgroup: LDS ordering point (s_waitcnt + a trivial s_barrier)
 __device__ __forceinline__ void wave_sync() { __syncthreads(); }
@@ -78,6 +89,25 @@ __device__ __forceinline__ lds_cdouble* lds_opaque(const double* p) {
   return (lds_cdouble*)(uintptr_t)a;
 }
 
+// Section timing (debug builds only, -DVC_TIMING, `make timing`): wave-uniform
+// s_memtime stamps accumulated per section and written to diag[b][4..].
+#ifdef VC_TIMING
+#define VC_TSTAMP(var) \
+  fence();              \
+  const uint64_t var = __builtin_amdgcn_s_memtime(); \
+  fence();
+#define VC_TACC(slot, t0) \
+  {                      \
+    fence();             \
+    tacc[slot] += __builtin_amdgcn_s_memtime() - (t0); \
+    fence();             \
+  }
+#else
+#define VC_TSTAMP(var)
+#define VC_TACC(slot, t0)
+#endif
+enum { T_SWEEP = 0, T_SETUP, T_RESID, T_BUILD, T_CHOL, T_SOLVE, T_UPDATE, T_POLISH, T_OUT, T_NSLOT };
+
 // largest a in (0,1] keeping v + a dv >= 0
 __device__ __forceinline__ double step_bound(double v, double dv) { return dv < 0.0 ? -v / dv : 1.0; }
 
@@ -95,14 +125,12 @@ struct Smem {
   double G[D::NC][D::LD];   // constraint rows of the condensed sensitivity (row r: stage crow_stage(r))
   double H[D::n + 1][D::LD];  // condensed Hessian (constant over the solve); row n: dummy
   double Lc[D::n * (D::n + 1) / 2 + 1];  // packed columns of the Cholesky factor (+1 dummy slot)
-  double xb[N + 1][KIN_NX]; // predicted trajectory
-  double jac[N][9];         // Jacobian data per stage (KinJac)
+  double xb[N + 1][KIN_NX + 1];  // predicted trajectory (+1: dummy column for branch-free stores)
+  double jac[N + 1][9];     // Jacobian data per stage (KinJac); row N: dummy
   double ub[D::n];          // warm-start inputs, interleaved (a_0, w_0, a_1, ...)
   double kap[N], ds[N];
-  double dinv[64];          // 1 / L_kk
   double vz[64];            // broadcast: a length-n vector (z, dz, ...)
   double vc[64];            // broadcast: a length-NC vector (weights, residual terms)
-  double col[2][64];        // broadcast: one sensitivity column during the forward sweep
 };
 
 // stage index (1..N-1) of constraint row r
@@ -117,6 +145,36 @@ __host__ __device__ constexpr int lc_off(int k) {
   return k * n - k * (k - 1) / 2;
 }
 
+// sum_{i<LEN} a[i*SA] b[i*SB] over LDS operands, loaded one CH-chunk ahead of
+// their FMAs so the LDS latency is paid about once per call
+template <int LEN, int SA, int SB>
+__device__ __forceinline__ double lds_dot(lds_cdouble* a, lds_cdouble* b) {
+  constexpr int CH = 4, NCH = (LEN + CH - 1) / CH;
+  double ca[2][CH], cb[2][CH];
+  auto fetch = [&](int c, int buf) {
+#pragma unroll
+    for (int q = 0; q < CH; ++q) {
+      const int i = c * CH + q;
+      ca[buf][q] = (i < LEN) ? a[i * SA] : 0.0;
+      cb[buf][q] = (i < LEN) ? b[i * SB] : 0.0;
+    }
+  };
+  double a0 = 0.0, a1 = 0.0;
+  fetch(0, 0);
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    if (c + 1 < NCH) fetch(c + 1, (c + 1) & 1);
+    fence();
+#pragma unroll
+    for (int q = 0; q < CH; q += 2) {
+      a0 += ca[c & 1][q] * cb[c & 1][q];
+      a1 += ca[c & 1][q + 1] * cb[c & 1][q + 1];
+    }
+    fence();
+  }
+  return a0 + a1;
+}
+
 // y_r = G_r . v for lane r (v broadcast in s.vz); rows have <= 2(N-1) nonzeros
 template <int N>
 __device__ double grow_dot(const Smem<N>& s, int lane) {
@@ -125,7 +183,7 @@ __device__ double grow_dot(const Smem<N>& s, int lane) {
   lds_cdouble* g = lds_opaque(&s.G[r][0]);
   lds_cdouble* v = lds_opaque(&s.vz[0]);
   double a0 = 0.0, a1 = 0.0;
-#pragma unroll 2
+#pragma unroll 4
   for (int i = 0; i < 2 * (N - 1); i += 2) {
     a0 += g[i] * v[i];
     a1 += g[i + 1] * v[i + 1];
@@ -142,7 +200,7 @@ __device__ double gt_dot(const Smem<N>& s, int lane) {
   lds_cdouble* g = lds_opaque(&s.G[0][j]);
   lds_cdouble* v = lds_opaque(&s.vc[0]);
   double a0 = 0.0, a1 = 0.0;
-#pragma unroll 2
+#pragma unroll 4
   for (int r = 0; r < NC; r += 2) {
     a0 += g[r * LD] * v[r];
     a1 += g[(r + 1) * LD] * v[r + 1];
@@ -155,71 +213,105 @@ template <int N>
 __device__ double h_dot(const Smem<N>& s, int lane) {
   constexpr int n = Dims<N>::n;
   const int j = lane < n ? lane : 0;
-  lds_cdouble* h = lds_opaque(&s.H[j][0]);
-  lds_cdouble* v = lds_opaque(&s.vz[0]);
-  double a0 = 0.0, a1 = 0.0;
-#pragma unroll 4
-  for (int i = 0; i < n; i += 2) {
-    a0 += h[i] * v[i];
-    a1 += h[i + 1] * v[i + 1];
-  }
-  return a0 + a1;
+  return lds_dot<n, 1, 1>(lds_opaque(&s.H[j][0]), lds_opaque(&s.vz[0]));
 }
 
 // In-place right-looking Cholesky of the SPD matrix whose row `lane` is Mr.
 // On return Mr holds row `lane` of L (lower part), s.Lc its columns, s.dinv the
 // inverse pivots.  Returns false (uniform) if a pivot is not positive.
+//
+// One-column lookahead: in step k, as soon as column k is visible in LDS, column
+// k+1 is updated first, its pivot taken and column k+1 published to LDS; only
+// then does the rest of step k's trailing update run, so the LDS round trip of
+// column k+1 overlaps those FMAs instead of sitting on the critical path.
 template <int N>
-__device__ bool cholesky(double (&Mr)[Dims<N>::n], Smem<N>& s, int lane) {
+__device__ __forceinline__ double chol_pivot(double (&Mr)[Dims<N>::n], Smem<N>& s, int lane, int k, bool& ok,
+                                             double& dj) {
+  constexpr int n = Dims<N>::n;
+  const double dkk = lane_bcast(Mr[k], k);
+  ok = ok && (dkk > 0.0);
+  // 1/sqrt(dkk): hardware v_rsq_f64 + two Newton steps (full fp64 accuracy, a
+  // much shorter dependent chain than IEEE sqrt followed by IEEE divide)
+  double inv = __builtin_amdgcn_rsq(dkk);
+  inv = inv * (1.5 - 0.5 * dkk * inv * inv);
+  inv = inv * (1.5 - 0.5 * dkk * inv * inv);
+  const double lik = (lane == k) ? dkk * inv : Mr[k] * inv;
+  Mr[k] = lik;
+  // branch-free stores (dummy slots): lane-divergent ifs in this fully unrolled
+  // code make the register allocator spill hundreds of VGPRs
+  s.Lc[lane >= k && lane < n ? lc_off<n>(k) + lane - k : n * (n + 1) / 2] = lik;
+  dj = (lane == k) ? inv : dj;  // lane k keeps 1/L_kk
+  return lik;
+}
+
+template <int N>
+__device__ bool cholesky(double (&Mr)[Dims<N>::n], Smem<N>& s, int lane, double& dj) {
   constexpr int n = Dims<N>::n;
   bool ok = true;
+  double lik = chol_pivot<N>(Mr, s, lane, 0, ok, dj);
 #pragma unroll
-  for (int k = 0; k < n; ++k) {
-    const double dkk = lane_bcast(Mr[k], k);
-    ok = ok && (dkk > 0.0);
-    const double d = sqrt(dkk);
-    const double inv = 1.0 / d;
-    const double lik = (lane == k) ? d : Mr[k] * inv;
-    Mr[k] = lik;
-    // branch-free stores (dummy slots): lane-divergent ifs in this fully unrolled
-    // loop make the register allocator spill hundreds of VGPRs
-    s.Lc[lane >= k && lane < n ? lc_off<n>(k) + lane - k : n * (n + 1) / 2] = lik;
-    s.dinv[lane == k ? k : 63] = inv;
-    wave_sync();
+  for (int k = 0; k < n - 1; ++k) {
+    wave_sync();  // column k visible
     fence();
+    const double* col = &s.Lc[lc_off<n>(k) - k];  // col[j] = L[j][k]
+    double cv[n];  // column k, issued at once so the loads overlap the pivot chain
 #pragma unroll
-    for (int j = k + 1; j < n; ++j) {
-      Mr[j] -= lik * s.Lc[lc_off<n>(k) + j - k];
-      if (((j - k) & 7) == 0) fence();
-    }
+    for (int j = k + 1; j < n; ++j) cv[j] = col[j];
+    // lookahead: column k+1 and its pivot
+    Mr[k + 1] -= lik * cv[k + 1];
+    const double lik_next = chol_pivot<N>(Mr, s, lane, k + 1, ok, dj);
     fence();
+    // rest of step k's trailing update
+#pragma unroll
+    for (int j = k + 2; j < n; ++j) Mr[j] -= lik * cv[j];
+    fence();
+    lik = lik_next;
   }
   return ok;
 }
 
-// Solve (L L') x = b, lane j holding b_j; returns x_j.  The forward sweep reads
-// L[i][k] from the row registers, the backward sweep L[k][i] (column i of the
-// packed factor) from LDS.
+// Solve (L L') x = b, lane j holding b_j and its inverse pivot dj = 1/L_jj;
+// returns x_j.  The forward sweep reads L[i][k] from the row registers and
+// broadcasts y_k = acc_k d_k from lane k (no LDS on the chain); the backward
+// sweep reads L[k][i] (column i of the packed factor) from LDS, prefetched one
+// 8-step chunk ahead so the LDS latency stays off the dependent chain.
 template <int N>
-__device__ double chol_solve(const double (&Lr)[Dims<N>::n], const Smem<N>& s, double b, int lane) {
+__device__ double chol_solve(const double (&Lr)[Dims<N>::n], const Smem<N>& s, double dj, double b, int lane) {
   constexpr int n = Dims<N>::n;
+  constexpr int CH = 8;
+  static_assert(n % CH == 0, "backward prefetch chunks");
   const int row = lane < n ? lane : 0;
   const int off = lc_off<n>(row) - row;
   double acc = b, y = 0.0;
 #pragma unroll
   for (int k = 0; k < n; ++k) {  // L y = b
-    const double yk = lane_bcast(acc, k) * s.dinv[k];
+    const double yk = lane_bcast(acc * dj, k);
     y = (lane == k) ? yk : y;
     acc -= Lr[k] * yk;
-    if ((k & 3) == 3) fence();
   }
   acc = y;
   double x = 0.0;
-#pragma unroll 4
-  for (int k = n - 1; k >= 0; --k) {  // L' x = y: lane i < k needs L[k][i]
-    const double xk = lane_bcast(acc, k) * s.dinv[k];
-    x = (lane == k) ? xk : x;
-    acc -= s.Lc[k >= row ? off + k : 0] * xk;
+  double lk[2][CH];
+  auto fetch = [&](int c, int buf) {  // L[k][row] for k = n-1-c*CH ... n-CH-c*CH
+#pragma unroll
+    for (int q = 0; q < CH; ++q) {
+      const int k = n - 1 - c * CH - q;
+      lk[buf][q] = s.Lc[k >= row ? off + k : 0];
+    }
+  };
+  fetch(0, 0);
+#pragma unroll
+  for (int c = 0; c < n / CH; ++c) {  // L' x = y: lane i < k needs L[k][i]
+    if (c + 1 < n / CH) fetch(c + 1, (c + 1) & 1);
+    fence();
+#pragma unroll
+    for (int q = 0; q < CH; ++q) {
+      const int k = n - 1 - c * CH - q;
+      const double xk = lane_bcast(acc * dj, k);
+      x = (lane == k) ? xk : x;
+      acc -= lk[c & 1][q] * xk;
+    }
+    fence();
   }
   return x;
 }
@@ -242,18 +334,100 @@ __device__ __forceinline__ void build_normal(double (&Mr)[Dims<N>::n], const Sme
   lds_cdouble* vc = lds_opaque(&s.vc[0]);
 #pragma unroll
   for (int r = 0; r < NC; ++r) {
-    // unconditional (clamped-index) load: a `lane < n ? load : 0` select becomes a
-    // divergent branch, and branches inside this unrolled block make the
+    // each row's broadcast operands are loaded into registers at once, so their
+    // LDS latency is paid once per row rather than once per few FMAs.
+    // unconditional (clamped-index) loads: a `lane < n ? load : 0` select becomes
+    // a divergent branch, and branches inside this unrolled block make the
     // register allocator spill; rows of lanes >= n are discarded below
+    constexpr int dummy = 0;
+    (void)dummy;
+    double gr[2 * (N - 1)];
+#pragma unroll
+    for (int i = 0; i < 2 * crow_stage<N>(r); ++i) gr[i] = G[r * LD + i];
     const double t = vc[r] * Gcol[r * LD];
     fence();
 #pragma unroll
-    for (int i = 0; i < 2 * crow_stage<N>(r); ++i) {
-      Mr[i] += t * G[r * LD + i];
-      if ((i & 7) == 7) fence();
-    }
+    for (int i = 0; i < 2 * crow_stage<N>(r); ++i) Mr[i] += t * gr[i];
     fence();
   }
+#pragma unroll
+  for (int i = 0; i < n; ++i) Mr[i] = (lane < n) ? Mr[i] : 0.0;
+}
+
+// The same normal matrix with the constraint part C'WC on the matrix cores:
+// M_c = (W G)' G as 16x16 tiles of v_mfma_f64_16x16x4_f64 (K = the NC rows of G,
+// 4 per step; only the lower block triangle), then moved from the MFMA
+// accumulator layout to the row-per-lane layout one 16-row block at a time
+// through a 16 x 49 LDS buffer that aliases the (not yet written) factor storage.
+template <int N>
+__device__ __forceinline__ void build_normal_mfma(double (&Mr)[Dims<N>::n], Smem<N>& s, double wb, int lane) {
+  constexpr int n = Dims<N>::n, NC = Dims<N>::NC, LD = Dims<N>::LD;
+  constexpr int NB = (n + 15) / 16, KS = (NC + 3) / 4, NT = NB * (NB + 1) / 2, BLD = 16 * NB + 1;
+  static_assert(16 * BLD <= n * (n + 1) / 2 + 1, "transpose buffer must fit the factor storage");
+  using d4 = __attribute__((ext_vector_type(4))) double;
+  const int lr = lane >> 4, lc = lane & 15;
+  d4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+  lds_cdouble* G = lds_opaque(&s.G[0][0]);
+  lds_cdouble* vc = lds_opaque(&s.vc[0]);
+  // all operands loaded up front (Mr is not live yet, so the registers are free):
+  // the LDS latency is paid once, not once per k-step
+  double gk[KS][NB], wk[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    // operands of k-step ks: lane l holds row r = 4 ks + (l >> 4), column 16 J + (l & 15)
+    const int r = 4 * ks + lr;
+    const int rr = r < NC ? r : 0;
+    wk[ks] = vc[rr];
+#pragma unroll
+    for (int J = 0; J < NB; ++J) {
+      const int c = 16 * J + lc;
+      gk[ks][J] = G[rr * LD + (c < n ? c : 0)];  // clamped, unconditional load
+    }
+  }
+  fence();
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const bool rv = 4 * ks + lr < NC;
+    double g[NB];
+#pragma unroll
+    for (int J = 0; J < NB; ++J) g[J] = (rv && 16 * J + lc < n) ? gk[ks][J] : 0.0;
+#pragma unroll
+    for (int I = 0, t = 0; I < NB; ++I) {
+      const double a = wk[ks] * g[I];
+#pragma unroll
+      for (int J = 0; J <= I; ++J, ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, g[J], acc[t], 0, 0, 0);
+    }
+  }
+  // Mr = H row + diag, then add this lane's row of M_c block-row by block-row
+  const int j0 = lane < n ? lane : 0;
+  lds_cdouble* Hrow = lds_opaque(&s.H[j0][0]);
+#pragma unroll
+  for (int i = 0; i < n; ++i) Mr[i] = Hrow[i] + (i == lane ? wb : 0.0);
+  double* buf = &s.Lc[0];
+  const int myI = lane >> 4;
+#pragma unroll
+  for (int I = 0, t0 = 0; I < NB; t0 += ++I) {
+    wave_sync();  // previous block-row consumed
+#pragma unroll
+    for (int J = 0; J <= I; ++J) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) buf[(lr + 4 * q) * BLD + 16 * J + lc] = acc[t0 + J][q];
+    }
+    wave_sync();
+    lds_cdouble* brow = lds_opaque(&buf[lc * BLD]);
+    constexpr int dummy = 0;
+    (void)dummy;
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+      if (i < 16 * (I + 1)) {
+        const double v = brow[i];
+        Mr[i] += (myI == I) ? v : 0.0;
+      }
+    }
+  }
+  wave_sync();  // buffer reads done before the factorisation overwrites it
 #pragma unroll
   for (int i = 0; i < n; ++i) Mr[i] = (lane < n) ? Mr[i] : 0.0;
 }
@@ -289,95 +463,144 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
   if (lane < KIN_NX) s.xb[0][lane] = A.x0[(size_t)b * KIN_NX + lane];
   wave_sync();
 
-  // ---- predict + linearize + condense (one fused pass over the horizon) -----
-  // The trajectory is uniform across lanes; lane j also carries column j of the
-  // sensitivity (dv, ddelta, dey, depsi, dt) with respect to dz_j.
-  double x[KIN_NX];
-#pragma unroll
-  for (int i = 0; i < KIN_NX; ++i) x[i] = s.xb[0][i];
-  double cv = 0, cd = 0, cey = 0, cep = 0, ct = 0;
-  double Hr[n];
-#pragma unroll
-  for (int i = 0; i < n; ++i) Hr[i] = 0.0;
-  double gj = 0.0;
+#ifdef VC_TIMING
+  uint64_t tacc[T_NSLOT] = {};
+#endif
+  VC_TSTAMP(t_sweep0)
+  // ---- predict + linearize + condense ------------------------------------------
+  // S1 serial rollout (uniform across lanes; the only serial transcendental
+  // chain), S2 Jacobians of all stages in parallel (lane k: stage k), S3 the
+  // sensitivity sweep (lane j carries column j of G: dv, ddelta, dey, depsi, dt
+  // w.r.t. dz_j) writing the v / delta constraint rows and the ey cost rows to
+  // LDS, S4 the Hessian from the ey rows (rank-1 updates, each row's broadcast
+  // operands preloaded at once).  No LDS round trip sits inside S1/S3's chains
+  // except the one-stage-ahead Jacobian prefetch.
+  constexpr int LD = Dims<N>::LD;
+  double* E = &s.H[0][0];  // ey rows E[k][j] (k < N) + 2 terminal rows, scratch until H is written
   bool finite = true;
-
+  {  // S1
+    double x[KIN_NX];
+#pragma unroll
+    for (int i = 0; i < KIN_NX; ++i) x[i] = s.xb[0][i];
 #pragma unroll 1
-  for (int k = 0; k < N; ++k) {
-    const double a = s.ub[2 * k], w = s.ub[2 * k + 1], kk = s.kap[k], h = s.ds[k];
-    const KinJac J = kin_spatial_jac(x, kk, A.L);
-    double u2[2] = {a, w}, f[KIN_NX], xn[KIN_NX];
-    kin_spatial_ode(x, u2, kk, A.L, f);
-    euler_apply<double, KIN_NX>(x, f, h, xn);
-    // column update: c_{k+1} = A_k c_k + B_k e_j
-    const double dq = J.qv * cv + J.qey * cey + J.qep * cep;
-    const double ncv = cv + h * a * dq + (lane == 2 * k ? h * J.q : 0.0);
-    const double ncd = cd + h * w * dq + (lane == 2 * k + 1 ? h * J.q : 0.0);
-    const double ncey = cey + h * (J.J33 * cey + J.J34 * cep);
-    const double ncep = cep + h * (J.J41 * cd + J.J43 * cey + J.J44 * cep);
-    ct += h * dq;
-    cv = ncv; cd = ncd; cey = ncey; cep = ncep;
+    for (int k = 0; k < N; ++k) {
+      const double u2[2] = {s.ub[2 * k], s.ub[2 * k + 1]};
+      const double h = s.ds[k];
+      double f[KIN_NX];
+      kin_spatial_ode(x, u2, s.kap[k], A.L, f);
+      double mine = 0.0;
 #pragma unroll
-    for (int i = 0; i < KIN_NX; ++i) {
-      x[i] = xn[i];
-      finite = finite && isfinite(xn[i]);
+      for (int i = 0; i < KIN_NX; ++i) {
+        x[i] += h * f[i];
+        finite = finite && isfinite(x[i]);
+        mine = (i == lane) ? x[i] : mine;
+      }
+      s.xb[k + 1][lane < KIN_NX ? lane : KIN_NX] = mine;  // xb rows padded: col KIN_NX is a dummy
+      // ey_{k+1} cost weight and linear term: stage (deviation + boundary,
+      // kinematic_mpc.py:110-122) or terminal (:152-154)
+      const double ey = x[3];
+      double cw, lin;
+      if (k + 1 < N) {
+        const double hs = s.ds[k + 1];
+        cw = W.w_dev * hs;
+        lin = W.w_dev * hs * ey;
+        if (ey < W.ey_min) { cw += W.w_b * hs; lin += W.w_b * hs * (ey - W.ey_min); }
+        if (ey > W.ey_max) { cw += W.w_b * hs; lin += W.w_b * hs * (ey - W.ey_max); }
+      } else {
+        cw = W.w_ey;
+        lin = W.w_ey * ey;
+      }
+      s.vc[k] = 2.0 * cw;
+      s.vz[k] = 2.0 * lin;
     }
-    if (lane == 0) {
-#pragma unroll
-      for (int i = 0; i < KIN_NX; ++i) s.xb[k + 1][i] = xn[i];
-      s.jac[k][0] = J.q; s.jac[k][1] = J.qv; s.jac[k][2] = J.qey; s.jac[k][3] = J.qep;
-      s.jac[k][4] = J.J33; s.jac[k][5] = J.J34; s.jac[k][6] = J.J41; s.jac[k][7] = J.J43;
-      s.jac[k][8] = J.J44;
-    }
-    const int st = k + 1;  // stage of the updated column
-    if (st <= N - 1 && lane < n) {
-      s.G[st - 1][lane] = cv;            // row v_st
-      s.G[(N - 1) + st - 1][lane] = cd;  // row delta_st
-    }
-    // ey_st cost: stage (deviation + boundary, kinematic_mpc.py:110-122) or terminal (:152-154)
-    double cw, lin;
-    const double ey = x[3];
-    if (st < N) {
-      const double hs = s.ds[st];
-      cw = W.w_dev * hs;
-      lin = W.w_dev * hs * ey;
-      if (ey < W.ey_min) { cw += W.w_b * hs; lin += W.w_b * hs * (ey - W.ey_min); }
-      if (ey > W.ey_max) { cw += W.w_b * hs; lin += W.w_b * hs * (ey - W.ey_max); }
-    } else {
-      cw = W.w_ey;
-      lin = W.w_ey * ey;
-    }
-    double* cb = s.col[k & 1];
-    cb[lane] = (lane < n) ? cey : 0.0;
-    wave_sync();
-    const double t2 = 2.0 * cw * cey;
-    fence();
-#pragma unroll
-    for (int i = 0; i < n; ++i) {
-      Hr[i] += t2 * cb[i];
-      if ((i & 7) == 7) fence();
-    }
-    gj += 2.0 * lin * cey;
   }
-  // terminal rows on v_N (kinematic_mpc.py:144-148), epsi_N (:155-157), t_N (:149-151)
-  {
-    const double vN = x[0];
-    const double cwv = (vN >= W.v_max) ? W.w_v : 0.0;
-    wave_sync();
-    s.col[0][lane] = (lane < n) ? cv : 0.0;
-    s.col[1][lane] = (lane < n) ? cep : 0.0;
-    wave_sync();
-    const double t2 = 2.0 * cwv * cv;
-    const double t3 = 2.0 * W.w_epsi * cep;
-    fence();
+  wave_sync();
+  {  // S2: lane k < N linearises stage k
+    const int k = lane < N ? lane : 0;
+    double xk[KIN_NX];
 #pragma unroll
-    for (int i = 0; i < n; ++i) {
-      Hr[i] += t2 * s.col[0][i] + t3 * s.col[1][i];
-      if ((i & 7) == 7) fence();
+    for (int i = 0; i < KIN_NX; ++i) xk[i] = s.xb[k][i];
+    const KinJac J = kin_spatial_jac(xk, s.kap[k], A.L);
+    double* jr = s.jac[lane < N ? lane : N];  // row N: dummy
+    jr[0] = J.q; jr[1] = J.qv; jr[2] = J.qey; jr[3] = J.qep;
+    jr[4] = J.J33; jr[5] = J.J34; jr[6] = J.J41; jr[7] = J.J43; jr[8] = J.J44;
+  }
+  wave_sync();
+  double gj = 0.0;
+  double cv = 0, cd = 0, cey = 0, cep = 0, ct = 0;
+  {  // S3
+    const int jcol = lane < n ? lane : n;  // lanes >= n write the padding column
+    double jn[9], hn, an, wn;
+    auto fetch = [&](int k) {
+#pragma unroll
+      for (int q = 0; q < 9; ++q) jn[q] = s.jac[k][q];
+      hn = s.ds[k]; an = s.ub[2 * k]; wn = s.ub[2 * k + 1];
+    };
+    fetch(0);
+#pragma unroll 1
+    for (int k = 0; k < N; ++k) {
+      double J[9];
+#pragma unroll
+      for (int q = 0; q < 9; ++q) J[q] = jn[q];
+      const double h = hn, a = an, w = wn;
+      const double lin2 = s.vz[k];
+      if (k + 1 < N) fetch(k + 1);
+      // c_{k+1} = A_k c_k + B_k e_j
+      const double dq = J[1] * cv + J[2] * cey + J[3] * cep;
+      const double ncv = cv + h * a * dq + (lane == 2 * k ? h * J[0] : 0.0);
+      const double ncd = cd + h * w * dq + (lane == 2 * k + 1 ? h * J[0] : 0.0);
+      const double ncey = cey + h * (J[4] * cey + J[5] * cep);
+      const double ncep = cep + h * (J[6] * cd + J[7] * cey + J[8] * cep);
+      ct += h * dq;
+      cv = ncv; cd = ncd; cey = ncey; cep = ncep;
+      // rows of stage k+1: v and delta constraint rows (k+1 <= N-1), ey cost row
+      const bool has = k + 1 <= N - 1;  // stage N has no constraint rows: padding column
+      s.G[has ? k : 0][has ? jcol : n] = cv;
+      s.G[has ? (N - 1) + k : 0][has ? jcol : n] = cd;
+      E[k * LD + jcol] = cey;
+      gj += lin2 * cey;
     }
+    // terminal rows on v_N (kinematic_mpc.py:144-148) and epsi_N (:155-157)
+    E[N * LD + jcol] = cv;
+    E[(N + 1) * LD + jcol] = cep;
+  }
+  wave_sync();
+  double Hr[n];
+  {  // S4
+    const double vN = s.xb[N][0];
+    const double cwv = (vN >= W.v_max) ? W.w_v : 0.0;
     gj += 2.0 * cwv * (vN - W.v_max) * cv;
-    gj += 2.0 * W.w_epsi * x[4] * cep;
-    gj += W.w_time * ct;
+    gj += 2.0 * W.w_epsi * s.xb[N][4] * cep;
+    gj += W.w_time * ct;  // t_N (:149-151)
+#pragma unroll
+    for (int i = 0; i < n; ++i) Hr[i] = 0.0;
+    // runtime loop over the ey rows (a fully unrolled one lets the scheduler issue
+    // every row's loads at once and spill); inner loops are compile-time
+#pragma unroll 1
+    for (int k = 0; k < N; ++k) {
+      lds_cdouble* Ek = lds_opaque(E + k * LD);
+      double er[n];
+#pragma unroll
+      for (int i = 0; i < n; ++i) er[i] = Ek[i];
+      const double t = s.vc[k] * Ek[lane < n ? lane : n];
+      fence();
+#pragma unroll
+      for (int i = 0; i < n; ++i) Hr[i] += t * er[i];
+    }
+    {  // terminal v_N and epsi_N rows
+      lds_cdouble* Ev = lds_opaque(E + N * LD);
+      lds_cdouble* Ee = lds_opaque(E + (N + 1) * LD);
+      double ev[n], ee[n];
+#pragma unroll
+      for (int i = 0; i < n; ++i) {
+        ev[i] = Ev[i];
+        ee[i] = Ee[i];
+      }
+      const double tv = 2.0 * cwv * cv, te = 2.0 * W.w_epsi * cep;
+      fence();
+#pragma unroll
+      for (int i = 0; i < n; ++i) Hr[i] += tv * ev[i] + te * ee[i];
+    }
   }
   // input costs: w_w w^2 (kinematic_mpc.py:124), slew w_a (a_{n+1}-a_n)^2 (:126-128), prox
   {
@@ -423,6 +646,8 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
     return;
   }
 
+  VC_TACC(T_SWEEP, t_sweep0)
+  VC_TSTAMP(t_setup0)
   // ---- inequality data ------------------------------------------------------
   Side bx, cs;  // box side (lane j < n), state-row side (lane r < NC)
   {
@@ -476,6 +701,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
   cs.llo = cs.hasLo ? 1.0 : 0.0;
   cs.lhi = cs.hasHi ? 1.0 : 0.0;
 
+  VC_TACC(T_SETUP, t_setup0)
   // ---- Phase 1: Mehrotra predictor-corrector interior point ------------------
   // Normal equations (H + diag(wb) + G'diag(wc)G) dz = rhs, one factorisation and
   // two solves (predictor, corrector) per iteration.
@@ -489,6 +715,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
 #pragma unroll 1
     for (;;) {
       no_hoist();
+      VC_TSTAMP(t_res0)
       wave_sync();
       s.vz[lane] = (lane < n) ? z : 0.0;
       s.vc[lane] = (lane < NC) ? (cs.lhi - cs.llo) : 0.0;
@@ -514,8 +741,15 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
       wave_sync();
       s.vc[lane] = (lane < NC) ? wlo_c + whi_c : 0.0;
       wave_sync();
-      build_normal<N>(Mr, s, wlo_b + whi_b, lane);
-      if (!cholesky<N>(Mr, s, lane)) {
+      VC_TACC(T_RESID, t_res0)
+      VC_TSTAMP(t_build0)
+      build_normal_mfma<N>(Mr, s, wlo_b + whi_b, lane);
+      VC_TACC(T_BUILD, t_build0)
+      VC_TSTAMP(t_chol0)
+      double dj = 1.0;
+      const bool chol_ok = cholesky<N>(Mr, s, lane, dj);
+      VC_TACC(T_CHOL, t_chol0)
+      if (!chol_ok) {
         // The barrier weights lambda/s of the active set (~1/mu) have made the
         // normal matrix numerically indefinite.  This happens only at the very
         // end (mu ~ 1e-14); the iterate is then accurate enough for the
@@ -539,7 +773,9 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
         s.vc[lane] = (lane < NC) ? ec : 0.0;
         wave_sync();
         const double rhs = (lane < n) ? (-rd - eb - gt_dot<N>(s, lane)) : 0.0;
-        const double dz = chol_solve<N>(Mr, s, rhs, lane);
+        VC_TSTAMP(t_sol0)
+        const double dz = chol_solve<N>(Mr, s, dj, rhs, lane);
+        VC_TACC(T_SOLVE, t_sol0)
         wave_sync();
         s.vz[lane] = (lane < n) ? dz : 0.0;
         wave_sync();
@@ -574,6 +810,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
     }
   }
 
+  VC_TSTAMP(t_pol0)
   // ---- Phase 2: active-set polish --------------------------------------------
   // Crossover to the active set the interior point identified (lambda > s):
   // box-active inputs are fixed (identity rows), active state rows are imposed
@@ -622,13 +859,14 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
       wave_sync();
       s.vc[lane] = rho_c;
       wave_sync();
-      build_normal<N>(Mr, s, 0.0, lane);
+      build_normal_mfma<N>(Mr, s, 0.0, lane);
 #pragma unroll
       for (int i = 0; i < n; ++i) {  // reduced matrix: fixed rows/cols -> identity
         const bool fi = (fmask >> i) & 1ull;
         Mr[i] = fixed ? (i == lane ? 1.0 : 0.0) : (fi ? 0.0 : Mr[i]);
       }
-      if (!cholesky<N>(Mr, s, lane)) {
+      double dj = 1.0;
+      if (!cholesky<N>(Mr, s, lane, dj)) {
         pchol_fail = true;
         break;
       }
@@ -640,7 +878,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
         s.vc[lane] = (lane < NC) ? (nu_c - rho_c * bnd_c) : 0.0;
         wave_sync();
         const double rhs = (lane < n) ? (fixed ? zfix : (base - gt_dot<N>(s, lane))) : 0.0;
-        zp = chol_solve<N>(Mr, s, rhs, lane);
+        zp = chol_solve<N>(Mr, s, dj, rhs, lane);
         wave_sync();
         s.vz[lane] = (lane < n) ? zp : 0.0;
         wave_sync();
@@ -697,6 +935,8 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
     }
   }
 
+  VC_TACC(T_POLISH, t_pol0)
+  VC_TSTAMP(t_out0)
   // ---- outputs -------------------------------------------------------------------
   int32_t st;
   if (!finite) st = VC_NONFINITE;
@@ -714,11 +954,16 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
     A.status[b] = st;
     A.iters[b] = it;
     if (A.diag) {
-      A.diag[(size_t)b * 4 + 0] = last_res / scale;
-      A.diag[(size_t)b * 4 + 1] = last_mu / scale;
-      A.diag[(size_t)b * 4 + 2] = double((chol_fail ? 1 : 0) | (converged ? 2 : 0) | (polished ? 4 : 0) |
-                                         (pchol_fail ? 8 : 0));
-      A.diag[(size_t)b * 4 + 3] = double(rounds);
+#ifdef VC_TIMING
+      constexpr size_t DS = 4 + T_NSLOT;
+#else
+      constexpr size_t DS = 4;
+#endif
+      A.diag[(size_t)b * DS + 0] = last_res / scale;
+      A.diag[(size_t)b * DS + 1] = last_mu / scale;
+      A.diag[(size_t)b * DS + 2] = double((chol_fail ? 1 : 0) | (converged ? 2 : 0) | (polished ? 4 : 0) |
+                                          (pchol_fail ? 8 : 0));
+      A.diag[(size_t)b * DS + 3] = double(rounds);
     }
   }
   // x* = xbar + G dz via the linearised recursion, lanes 0..5 own components
@@ -746,6 +991,16 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
     }
     if (lane < KIN_NX) xo[(k + 1) * KIN_NX + lane] = s.xb[k + 1][lane] + mine;
   }
+  VC_TACC(T_OUT, t_out0)
+#ifdef VC_TIMING
+  // timing builds: diag is [B][4 + T_NSLOT]; slot T_UPDATE = PDIP total - parts
+  if (A.diag && lane < T_NSLOT) {
+    double v = 0.0;
+#pragma unroll
+    for (int i = 0; i < T_NSLOT; ++i) v = (i == lane) ? double(tacc[i]) : v;
+    A.diag[(size_t)b * (4 + T_NSLOT) + 4 + lane] = v;
+  }
+#endif
 }
 
 // ---- host launcher ---------------------------------------------------------------

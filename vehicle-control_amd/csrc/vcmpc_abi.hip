@@ -15,6 +15,12 @@
 #include "vcmpc.h"
 
 
+#ifdef VC_TIMING
+#define VC_DIAG_COLS 13  // 4 diagnostics + 9 section-cycle counters (kin_ltv.hip T_*)
+#else
+#define VC_DIAG_COLS 4
+#endif
+
 struct vc_ctx {
   int device = 0, model = 0, N = 0, max_batch = 0, dtype = 0;
   vc_params p{};
@@ -203,7 +209,7 @@ int vc_solve_diag(vc_ctx* c, int B, const void* x0, const void* kappa, const voi
              {nullptr, u0, (size_t)B * nu * 8, nullptr},
              {nullptr, status, (size_t)B * 4, nullptr},
              {nullptr, iters, (size_t)B * 4, nullptr},
-             {nullptr, diag, diag ? (size_t)B * 4 * 8 : 0, nullptr}};
+             {nullptr, diag, diag ? (size_t)B * VC_DIAG_COLS * 8 : 0, nullptr}};
     if (int r = stage(c, slots)) return r;
     a.x0 = (const double*)slots[0].dev;
     a.kappa = (const double*)slots[1].dev;
