@@ -859,7 +859,14 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
       wave_sync();
       s.vc[lane] = rho_c;
       wave_sync();
-      build_normal_mfma<N>(Mr, s, 0.0, lane);
+      if (__ballot(rho_c > 0.0)) {
+        build_normal_mfma<N>(Mr, s, 0.0, lane);
+      } else {  // no active state row (most problems): the reduced Hessian only
+        const int j0 = lane < n ? lane : 0;
+        lds_cdouble* Hrow = lds_opaque(&s.H[j0][0]);
+#pragma unroll
+        for (int i = 0; i < n; ++i) Mr[i] = (lane < n) ? Hrow[i] : 0.0;
+      }
 #pragma unroll
       for (int i = 0; i < n; ++i) {  // reduced matrix: fixed rows/cols -> identity
         const bool fi = (fmask >> i) & 1ull;
