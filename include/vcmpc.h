@@ -8,6 +8,9 @@
  *   vc_create        KinematicMPC.__init__            vehicle_control/controllers/mpc/kinematic_mpc.py:15-30
  *                    (the once-only NLP transcription + IPOPT setup, :39-52)
  *   vc_solve         KinematicMPC.command             kinematic_mpc.py:160-168 (opti.solve at :162)
+ *                    CascadedMPC.command (single-track, horizon_pm = 0)
+ *                                                     controllers/mpc/cascaded_mpc.py:306-314 (opti.solve
+ *                                                     at :308; NLP built at :17-39,91-179,279-304)
  *   vc_rollout       KinematicCar.spatial_transition  vehicle_control/models/kinematic_car.py:61-64,70-72,
  *                    applied along the horizon        (the dynamics rows of kinematic_mpc.py:95-99)
  *   vc_linearize     CasADi AD of the dynamics inside IPOPT ("expand": True, kinematic_mpc.py:51)
@@ -46,7 +49,7 @@
 extern "C" {
 #endif
 
-#define VCMPC_ABI_VERSION 1
+#define VCMPC_ABI_VERSION 2
 
 typedef struct vc_ctx vc_ctx;
 
@@ -84,6 +87,18 @@ typedef struct vc_kin_mpc {
   double v_min, v_max, delta_min, delta_max, ey_min, ey_max; /* state_constraints */
 } vc_kin_mpc;
 
+/* Dynamic single-track MPC weights and bounds (config/controllers/singletrack.yaml,
+ * read by cascaded_mpc.py:91-179,279-304) and the build's SQP knobs. */
+typedef struct vc_dyn_mpc {
+  double w_time, w_speed, w_ey, w_epsi, w_w, w_Fx, w_dev, w_b, w_slip; /* cost_weights */
+  double w_min, w_max;                                                /* input_constraints */
+  double Ux_min, max_speed, delta_min, delta_max, ey_min, ey_max;     /* state_constraints */
+  double fx_scale;   /* Fx unit of the scaled decision variable [N] (no reference counterpart) */
+  double trust_Fx;   /* SQP trust region |Fx - Fxbar| <= trust_Fx [N] (0 = off) */
+  int32_t sqp_iters; /* SQP iterations per solve (BASELINE config 3: 3) */
+  int32_t pad_;
+} vc_dyn_mpc;
+
 /* The build's LTV-QP contract knobs (no reference counterpart). */
 typedef struct vc_qp {
   double prox;      /* proximal weight: + prox * ||u - ubar||^2 */
@@ -98,7 +113,8 @@ typedef struct vc_params {
   vc_kin_car kin_car;
   vc_dyn_car dyn_car;
   vc_kin_mpc kin_mpc;
-  vc_qp qp;
+  vc_qp qp;         /* trust_a is the kinematic acceleration trust region; trust_w serves both */
+  vc_dyn_mpc dyn_mpc;
 } vc_params;
 
 int vc_abi_version(void);
@@ -108,8 +124,8 @@ int vc_params_sizeof(void);
 /* Create a solve context on `device` for `model` with horizon N and workspace for
  * up to max_batch problems.  Returns NULL on failure (reason: vc_last_error(NULL)).
  * Built combinations: (VC_MODEL_KINEMATIC, VC_F64, N = 20) for vc_solve /
- * vc_condense; every N >= 1 for vc_rollout / vc_linearize / vc_plant_step /
- * vc_spatial_step. */
+ * vc_condense; (VC_MODEL_DYNAMIC, VC_F32, N = 40) for vc_solve (sequential QP);
+ * every N >= 1 for vc_rollout / vc_linearize / vc_plant_step / vc_spatial_step. */
 vc_ctx* vc_create(int device, int model, int N, int max_batch, int dtype, const vc_params* params);
 void vc_destroy(vc_ctx* ctx);
 const char* vc_last_error(const vc_ctx* ctx);
@@ -119,10 +135,14 @@ const char* vc_last_error(const vc_ctx* ctx);
 int vc_set_stream(vc_ctx* ctx, void* stream);
 int vc_synchronize(vc_ctx* ctx);
 
-/* One LTV-MPC step for B problems (B <= max_batch):
+/* One MPC step for B problems (B <= max_batch):
  *   in:     x0[B][nx], kappa[B][N], ds[B][N], ubar[B][N][nu] (warm start)
- *   out:    ubar <- u*[B][N][nu], xbar <- x*[B][N+1][nx], u0[B][nu] = u*[:,0],
- *           status[B] (enum vc_status), iters[B] (interior-point iterations).
+ *   out:    ubar <- u*[B][N][nu], xbar <- x*[B][NS][nx], u0[B][nu] = u*[:,0],
+ *           status[B] (enum vc_status), iters[B] (interior-point iterations, summed
+ *           over the SQP iterations for the dynamic model).
+ * Kinematic: one LTV-QP step, NS = N + 1 state columns (kinematic_mpc.py:59-64).
+ * Dynamic:   dyn_mpc.sqp_iters QP steps, NS = N columns with dynamics for k < N-1
+ *            (cascaded_mpc.py:70,116-122); x* is the rollout of u*.
  * xbar is output only: the prediction is re-rolled from (x0, ubar). */
 int vc_solve(vc_ctx* ctx, int B, const void* x0, const void* kappa, const void* ds,
              void* xbar, void* ubar, void* u0, int32_t* status, int32_t* iters, int flags);
@@ -135,6 +155,17 @@ int vc_solve(vc_ctx* ctx, int B, const void* x0, const void* kappa, const void* 
 int vc_solve_diag(vc_ctx* ctx, int B, const void* x0, const void* kappa, const void* ds,
                   void* xbar, void* ubar, void* u0, int32_t* status, int32_t* iters, void* diag,
                   int flags);
+
+/* Test diagnostics (dynamic fp32 contexts): vc_solve plus a dump of the first QP
+ * of the first SQP iteration into dbg[B][vc_debug_stride()] floats:
+ * [0,80) gradient g, [80,6480) interior-point normal matrix M at the start point
+ * (row-major, lower tiles + diagonal blocks valid), [6480,12880) the factor storage
+ * after the blocked Cholesky (Y = L^-T in the upper triangle), [12880,12960) the
+ * predictor right-hand side, [12960,13040) the predictor step.  No reference
+ * counterpart: used by tests/test_gpu_parity.py to check each stage of the kernel. */
+int vc_solve_debug(vc_ctx* ctx, int B, const void* x0, const void* kappa, const void* ds, void* xbar, void* ubar,
+                   void* u0, int32_t* status, int32_t* iters, void* dbg, int flags);
+int vc_debug_stride(void);
 
 /* Predict: xbar[B][N+1][nx] from x0[B][nx] and ubar[B][N][nu] (spatial step). */
 int vc_rollout(vc_ctx* ctx, int B, const void* x0, const void* ubar, const void* kappa,

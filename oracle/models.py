@@ -19,6 +19,20 @@ GRAVITY = 9.88  # models/dynamic_car.py:61
 
 
 # ----------------------------------------------------------------------------
+# complex-step-safe |x| and sign(x): identical to np.abs / np.sign on real input;
+# on complex input (x + i h, h ~ 1e-30) they carry the derivative, so the
+# oracle's Jacobians come from complex-step differentiation of these same
+# model functions (dyn_sqp.py), independent of the kernel's dual numbers.
+# ----------------------------------------------------------------------------
+def rabs(x):
+    return np.where(np.real(x) >= 0, x, -x)
+
+
+def rsign(x):
+    return np.sign(np.real(x))
+
+
+# ----------------------------------------------------------------------------
 # integrators  (utils/integrators.py)
 # ----------------------------------------------------------------------------
 def euler_step(f, x, u, kappa, h):
@@ -32,7 +46,7 @@ def rk4_step(f, x, u, kappa, h):
 
     ``x + h*(1/6)*(k1 + 2 k2 + 2 k3 + k4)`` with the stage states
     ``x + 0.5 h k1``, ``x + 0.5 h k2``, ``x + h k3`` (integrators.py:30-34)."""
-    h = np.asarray(h, dtype=np.float64)[..., None]
+    h = np.asarray(h)[..., None]
     k1 = f(x, u, kappa)
     k2 = f(x + 0.5 * h * k1, u, kappa)
     k3 = f(x + 0.5 * h * k2, u, kappa)
@@ -174,11 +188,11 @@ def fiala_lateral_force(alpha, Calpha, Fymax, eps):
     Cubic below alphamod = atan(3 Fymax eps / C_alpha), linear+sign above."""
     ta = np.tan(alpha)
     alphamod = np.arctan((3 * Fymax * eps) / Calpha)
-    inner = (-Calpha * ta + Calpha ** 2 * np.abs(ta) * ta / (3 * Fymax)
+    inner = (-Calpha * ta + Calpha ** 2 * rabs(ta) * ta / (3 * Fymax)
              - (Calpha ** 3 * ta ** 3) / (27 * Fymax ** 2))
     outer = (-Calpha * (1 - 2 * eps + eps ** 2) * ta
-             - Fymax * (3 * eps ** 2 - 2 * eps ** 3) * np.sign(alpha))
-    return np.where(np.abs(alpha) <= alphamod, inner, outer)
+             - Fymax * (3 * eps ** 2 - 2 * eps ** 3) * rsign(alpha))
+    return np.where(np.real(rabs(alpha)) <= np.real(alphamod), inner, outer)
 
 
 def linear_lateral_force(alpha, Calpha):
@@ -193,7 +207,7 @@ def dyn_temporal_ode(x, u, kappa, p, tyre="fiala"):
     """Temporal ODE -- dynamic_car.py:144-163 (Fb = 0, flat track)."""
     Ux, Uy, r, delta, s, ey, epsi, t = np.moveaxis(x, -1, 0)
     w = u[..., 1]
-    kappa = np.asarray(kappa, dtype=np.float64)
+    kappa = np.asarray(kappa)
     F = dyn_forces(x, u, p)
     if tyre == "fiala":
         Fy_f = fiala_lateral_force(F["alpha_f"], p["Caf"], F["Fymax_f"], p["eps"])

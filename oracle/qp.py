@@ -145,8 +145,16 @@ def _eqp(H, g, C, d, act):
     rhs = np.concatenate([-g, d[act]])
     try:
         sol = np.linalg.solve(K, rhs)
+        bad = np.abs(K @ sol - rhs).max() > 1e-10 * (1.0 + np.abs(rhs).max())
     except np.linalg.LinAlgError:
-        return None, None
+        bad = True
+    if bad:
+        # linearly dependent active rows (e.g. the dynamic contract's stage-0 force
+        # bounds, which all act on Fx_0 alone): minimum-norm multipliers; the primal
+        # part is still unique because H is positive definite
+        sol = np.linalg.lstsq(K, rhs, rcond=1e-13)[0]
+        if np.abs(K @ sol - rhs).max() > 1e-9 * (1.0 + np.abs(rhs).max()):
+            return None, None
     lp = np.zeros(len(d))
     lp[act] = sol[n:]
     return sol[:n], lp

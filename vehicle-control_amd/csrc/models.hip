@@ -19,7 +19,7 @@ __device__ inline void temporal_step(const ModelArgs& m, const T* x, const T* u,
     kin_temporal_ode(x, u, kappa, T(m.L), f);   // Euler, kinematic_car.py:42-45
     euler_apply<T, KIN_NX>(x, f, dt, xn);
   } else {
-    rk4_apply<T, DYN_NX>(x, dt, [&](const T* xs, T* f) { dyn_temporal_ode(xs, u, kappa, m.dyn, f); }, xn);
+    rk4_apply<T, DYN_NX>(x, dt, [&](const T* xs, T* f) { dyn_temporal_ode(xs, u, kappa, dyn_coef<T>(m), f); }, xn);
   }
 }
 
@@ -30,7 +30,7 @@ __device__ inline void spatial_step(const ModelArgs& m, const T* x, const T* u, 
     kin_spatial_ode(x, u, kappa, T(m.L), f);    // Euler, kinematic_car.py:61-64
     euler_apply<T, KIN_NX>(x, f, ds, xn);
   } else {
-    rk4_apply<T, DYN_NX>(x, ds, [&](const T* xs, T* f) { dyn_spatial_ode(xs, u, kappa, m.dyn, f); }, xn);
+    rk4_apply<T, DYN_NX>(x, ds, [&](const T* xs, T* f) { dyn_spatial_ode(xs, u, kappa, dyn_coef<T>(m), f); }, xn);
   }
 }
 

@@ -5,6 +5,7 @@
 #include <cstddef>
 #include <cstdint>
 
+#include "vc_models.hpp"
 #include "vcmpc.h"
 
 namespace vc {
@@ -30,15 +31,44 @@ struct KinLtvArgs {
   vc_qp qp;
 };
 
+// Fused dynamic-bicycle SQP step (dyn_sqp.hip), fp32.
+struct DynSqpArgs {
+  const float* x0;     // [B][8]
+  const float* kappa;  // [B][N]
+  const float* ds;     // [B][N]
+  const float* ubar;   // [B][N][2]  warm start (may alias u_out)
+  float* u_out;        // [B][N][2]  u*
+  float* x_out;        // [B][N][8]  x* = rollout(u*)
+  float* u0;           // [B][2]
+  int32_t* status;     // [B]
+  int32_t* iters;      // [B]
+  float* diag;         // [B][4] optional diagnostics, may be null
+  float* dbg;          // [B][dyn_sqp_debug_stride()] first-QP dump (vc_solve_debug), may be null
+  int B;
+  DynCoef<float> car;
+  vc_dyn_mpc w;
+  vc_qp qp;
+};
+
 // Elementwise model kernels (models.hip).
 struct ModelArgs {
   int model;  // vc_model
   int B, N;
   double L;   // kinematic wheelbase
-  vc_dyn_car dyn;
+  DynCoef<double> dyn64;
+  DynCoef<float> dyn32;
 };
+template <typename T>
+__host__ __device__ inline const DynCoef<T>& dyn_coef(const ModelArgs& m);
+template <>
+__host__ __device__ inline const DynCoef<double>& dyn_coef<double>(const ModelArgs& m) { return m.dyn64; }
+template <>
+__host__ __device__ inline const DynCoef<float>& dyn_coef<float>(const ModelArgs& m) { return m.dyn32; }
 
 hipError_t launch_kin_ltv(const KinLtvArgs& a, int N, hipStream_t stream);
+hipError_t launch_dyn_sqp(const DynSqpArgs& a, int N, hipStream_t stream);
+size_t dyn_sqp_smem_bytes(int N);
+int dyn_sqp_debug_stride();
 size_t kin_ltv_smem_bytes(int N);
 hipError_t launch_plant_step(const ModelArgs& m, int dtype, const void* x, const void* u, const void* kappa, double dt,
                              void* xn, hipStream_t st);

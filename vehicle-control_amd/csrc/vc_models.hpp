@@ -86,6 +86,35 @@ __host__ __device__ inline KinJac kin_spatial_jac(const double* x, double kappa,
 // Dynamic bicycle, x = [Ux, Uy, r, delta, s, ey, epsi, t], u = [Fx, w]
 // ---------------------------------------------------------------------------
 
+// Dynamic-bicycle coefficients in the arithmetic type R, precomputed once on the host
+// from vc_dyn_car (double) so the kernels never evaluate parameter expressions (or
+// doubles) in their inner loops.  Every combination keeps the reference's evaluation
+// order (dynamic_car.py:78-151), e.g. (b / l) * m is the left factor of
+// (b / l) * m * (g cos(theta) cos(phi) + Av2 Ux^2) as Python evaluates it.
+template <typename R>
+struct DynCoef {
+  R m, Izz, a, b, h, l, eps, Peng, Caf, Car, Cd, muf, mur, Av2, Frr;
+  R xf_a, xf_b, xr_a, xr_b;  // (Xdf - Xbf)/2, (Xdf + Xbf)/2, (Xbr - Xdr)/2, (Xdr + Xbr)/2
+  R gz0;                     // g cos(theta) cos(phi)
+  R fzf_m, fzr_m;            // (b / l) m, (a / l) m
+  int tyre;
+};
+
+template <typename R>
+__host__ __device__ inline DynCoef<R> make_dyn_coef(const vc_dyn_car& p) {
+  DynCoef<R> c;
+  c.m = R(p.m); c.Izz = R(p.Izz); c.a = R(p.a); c.b = R(p.b); c.h = R(p.h); c.l = R(p.l);
+  c.eps = R(p.eps); c.Peng = R(p.Peng); c.Caf = R(p.Caf); c.Car = R(p.Car); c.Cd = R(p.Cd);
+  c.muf = R(p.muf); c.mur = R(p.mur); c.Av2 = R(p.Av2); c.Frr = R(p.Frr);
+  c.xf_a = R((p.Xdf - p.Xbf) / 2); c.xf_b = R((p.Xdf + p.Xbf) / 2);
+  c.xr_a = R((p.Xbr - p.Xdr) / 2); c.xr_b = R((p.Xdr + p.Xbr) / 2);
+  c.gz0 = R(GRAVITY * cos(p.theta) * cos(p.phi));
+  c.fzf_m = R(p.b / p.l * p.m);
+  c.fzr_m = R(p.a / p.l * p.m);
+  c.tyre = p.tyre;
+  return c;
+}
+
 // Modified Fiala / brush tyre -- models/dynamic_car.py:119-142.
 template <typename T>
 __host__ __device__ inline T fiala_fy(T alpha, T Ca, T Fymax, T eps) {
@@ -99,41 +128,54 @@ __host__ __device__ inline T fiala_fy(T alpha, T Ca, T Fymax, T eps) {
   return -Ca * (T(1) - T(2) * eps + eps * eps) * ta - Fymax * (T(3) * eps * eps - T(2) * eps * eps * eps) * sgn;
 }
 
+// Tyre/load intermediates shared by the ODE and the NLP's stage terms (dynamic_car.py:78-115).
+template <typename T, typename R>
+struct DynForces {
+  T Fx_f, Fx_r, Fz_f, Fz_r, alpha_f, alpha_r;
+  __host__ __device__ DynForces(T Ux, T Uy, T r, T delta, T Fx, const DynCoef<R>& c) {
+    // drive/brake split (dynamic_car.py:78-86)
+    const T Xf = T(c.xf_a) * tanh(T(2) * (Fx / T(1000) + T(0.5))) + T(c.xf_b);
+    Fx_f = Fx * Xf;
+    const T Xr = T(c.xr_a) * tanh(T(-2) * (Fx / T(1000) + T(0.5))) + T(c.xr_b);
+    Fx_r = Fx * Xr;
+    // loads (dynamic_car.py:98-102); l = car.l
+    const T gz = T(c.gz0) + T(c.Av2) * (Ux * Ux);
+    Fz_f = T(c.fzf_m) * gz - T(c.h) * Fx / T(c.l);
+    Fz_r = T(c.fzr_m) * gz + T(c.h) * Fx / T(c.l);
+    // slip angles (dynamic_car.py:111-115)
+    alpha_f = atan((Uy + T(c.a) * r) / Ux) - delta;
+    alpha_r = atan((Uy - T(c.b) * r) / Ux);
+  }
+  // friction-ellipse lateral capacity (dynamic_car.py:107-108)
+  __host__ __device__ T fymax_f(const DynCoef<R>& c) const {
+    return sqrt((T(c.muf) * Fz_f) * (T(c.muf) * Fz_f) - (T(0.99) * Fx_f) * (T(0.99) * Fx_f));
+  }
+  __host__ __device__ T fymax_r(const DynCoef<R>& c) const {
+    return sqrt((T(c.mur) * Fz_r) * (T(c.mur) * Fz_r) - (T(0.99) * Fx_r) * (T(0.99) * Fx_r));
+  }
+};
+
 // Temporal ODE -- models/dynamic_car.py:66-163 (Fb = 0).  tyre: VC_TYRE_FIALA or the
 // build-defined VC_TYRE_LINEAR (Fy = -C_alpha tan alpha, first term of :123).
-template <typename T>
-__host__ __device__ inline void dyn_temporal_ode(const T* x, const T* u, T kappa, const vc_dyn_car& p, T* f) {
+template <typename T, typename R>
+__host__ __device__ inline void dyn_temporal_ode(const T* x, const T* u, T kappa, const DynCoef<R>& c, T* f) {
   const T Ux = x[0], Uy = x[1], r = x[2], delta = x[3], ey = x[5], epsi = x[6];
   const T Fx = u[0], w = u[1];
-  // drive/brake split (dynamic_car.py:78-86)
-  const T Xf = T((p.Xdf - p.Xbf) / 2) * tanh(T(2) * (Fx / T(1000) + T(0.5))) + T((p.Xdf + p.Xbf) / 2);
-  const T Fx_f = Fx * Xf;
-  const T Xr = T((p.Xbr - p.Xdr) / 2) * tanh(T(-2) * (Fx / T(1000) + T(0.5))) + T((p.Xdr + p.Xbr) / 2);
-  const T Fx_r = Fx * Xr;
-  // loads (dynamic_car.py:98-102); l = car.l
-  const T gz = T(GRAVITY) * T(cos(p.theta)) * T(cos(p.phi)) + T(p.Av2) * Ux * Ux;
-  const T Fz_f = T(p.b / p.l) * T(p.m) * gz - T(p.h) * Fx / T(p.l);
-  const T Fz_r = T(p.a / p.l) * T(p.m) * gz + T(p.h) * Fx / T(p.l);
-  // slip angles (dynamic_car.py:111-115)
-  const T alpha_f = atan((Uy + T(p.a) * r) / Ux) - delta;
-  const T alpha_r = atan((Uy - T(p.b) * r) / Ux);
+  const DynForces<T, R> F(Ux, Uy, r, delta, Fx, c);
   T Fy_f, Fy_r;
-  if (p.tyre == VC_TYRE_LINEAR) {
-    Fy_f = -T(p.Caf) * tan(alpha_f);
-    Fy_r = -T(p.Car) * tan(alpha_r);
+  if (c.tyre == VC_TYRE_LINEAR) {
+    Fy_f = -T(c.Caf) * tan(F.alpha_f);
+    Fy_r = -T(c.Car) * tan(F.alpha_r);
   } else {
-    // friction-ellipse lateral capacity (dynamic_car.py:107-108)
-    const T Fymax_f = sqrt((T(p.muf) * Fz_f) * (T(p.muf) * Fz_f) - (T(0.99) * Fx_f) * (T(0.99) * Fx_f));
-    const T Fymax_r = sqrt((T(p.mur) * Fz_r) * (T(p.mur) * Fz_r) - (T(0.99) * Fx_r) * (T(0.99) * Fx_r));
-    Fy_f = fiala_fy(alpha_f, T(p.Caf), Fymax_f, T(p.eps));
-    Fy_r = fiala_fy(alpha_r, T(p.Car), Fymax_r, T(p.eps));
+    Fy_f = fiala_fy(F.alpha_f, T(c.Caf), F.fymax_f(c), T(c.eps));
+    Fy_r = fiala_fy(F.alpha_r, T(c.Car), F.fymax_r(c), T(c.eps));
   }
-  const T Fd = T(p.Frr) + T(p.Cd) * Ux * Ux;
+  const T Fd = T(c.Frr) + T(c.Cd) * (Ux * Ux);
   const T cd = cos(delta), sd = sin(delta);
-  const T m = T(p.m);
-  f[0] = (Fx_f * cd - Fy_f * sd + Fx_r - Fd) / m + r * Uy;
-  f[1] = (Fy_f * cd + Fx_f * sd + Fy_r) / m - r * Ux;
-  f[2] = (T(p.a) * (Fy_f * cd + Fx_f * sd) - T(p.b) * Fy_r) / T(p.Izz);
+  const T m = T(c.m);
+  f[0] = (F.Fx_f * cd - Fy_f * sd + F.Fx_r - Fd) / m + r * Uy;
+  f[1] = (Fy_f * cd + F.Fx_f * sd + Fy_r) / m - r * Ux;
+  f[2] = (T(c.a) * (Fy_f * cd + F.Fx_f * sd) - T(c.b) * Fy_r) / T(c.Izz);
   f[3] = w;
   const T s_dot = (Ux * cos(epsi) - Uy * sin(epsi)) / (T(1) - kappa * ey);
   f[4] = s_dot;
@@ -143,9 +185,9 @@ __host__ __device__ inline void dyn_temporal_ode(const T* x, const T* u, T kappa
 }
 
 // Spatial ODE = temporal / s_dot with s' = 1, t' = 1/s_dot -- dynamic_car.py:169-187.
-template <typename T>
-__host__ __device__ inline void dyn_spatial_ode(const T* x, const T* u, T kappa, const vc_dyn_car& p, T* f) {
-  dyn_temporal_ode(x, u, kappa, p, f);
+template <typename T, typename R>
+__host__ __device__ inline void dyn_spatial_ode(const T* x, const T* u, T kappa, const DynCoef<R>& c, T* f) {
+  dyn_temporal_ode(x, u, kappa, c, f);
   const T s_dot = f[4];
 #pragma unroll
   for (int i = 0; i < DYN_NX; ++i) f[i] = f[i] / s_dot;
@@ -153,23 +195,59 @@ __host__ __device__ inline void dyn_spatial_ode(const T* x, const T* u, T kappa,
   f[7] = T(1) / s_dot;
 }
 
+// Per-stage nonlinear terms of the single-track NLP at (Ux, Uy, r, delta, Fx):
+//   out[0] slip_f = |tan alpha_f| - tan(alphamod_f)   (slip cost, cascaded_mpc.py:155-159)
+//   out[1] slip_r                                     (cascaded_mpc.py:161-165)
+//   out[2] peng   = Fx - Peng / Ux  <= 0              (power limit, cascaded_mpc.py:110)
+//   out[3] Fx_f - mu_f Fz_f cos(alpha_f) <= 0,  out[4] -Fx_f - mu_f Fz_f cos(alpha_f) <= 0
+//   out[5] Fx_r - mu_r Fz_r cos(alpha_r) <= 0,  out[6] -Fx_r - mu_r Fz_r cos(alpha_r) <= 0
+//                                                     (tyre force bounds, cascaded_mpc.py:124-128)
+// with Fz, Fymax, alpha, alphamod as in dynamic_car.py:78-132.
+template <typename T, typename R>
+__host__ __device__ inline void dyn_stage_terms(const T* X5, const DynCoef<R>& c, T* out) {
+  const T Ux = X5[0], Fx = X5[4];
+  const DynForces<T, R> F(Ux, X5[1], X5[2], X5[3], Fx, c);
+  const T amod_f = atan((T(3) * F.fymax_f(c) * T(c.eps)) / T(c.Caf));
+  const T amod_r = atan((T(3) * F.fymax_r(c) * T(c.eps)) / T(c.Car));
+  out[0] = fabs(tan(F.alpha_f)) - tan(amod_f);
+  out[1] = fabs(tan(F.alpha_r)) - tan(amod_r);
+  out[2] = Fx - T(c.Peng) / Ux;
+  const T bound_f = T(c.muf) * F.Fz_f * cos(F.alpha_f);
+  const T bound_r = T(c.mur) * F.Fz_r * cos(F.alpha_r);
+  out[3] = F.Fx_f - bound_f;
+  out[4] = -F.Fx_f - bound_f;
+  out[5] = F.Fx_r - bound_r;
+  out[6] = -F.Fx_r - bound_r;
+}
+
 // RK4 (utils/integrators.py:26-37): x + h (1/6) (k1 + 2k2 + 2k3 + k4).
+// The stage sum is accumulated left to right, ((k1 + 2k2) + 2k3) + k4, the evaluation
+// order of the reference expression, so only four stage vectors are live at once.
 template <typename T, int NX, typename F>
 __host__ __device__ inline void rk4_apply(const T* x, T h, F&& f, T* xn) {
-  T k1[NX], k2[NX], k3[NX], k4[NX], xs[NX];
-  f(x, k1);
+  T k[NX], acc[NX], xs[NX];
+  f(x, k);
 #pragma unroll
-  for (int i = 0; i < NX; ++i) xs[i] = x[i] + T(0.5) * h * k1[i];
-  f(xs, k2);
+  for (int i = 0; i < NX; ++i) {
+    acc[i] = k[i];
+    xs[i] = x[i] + T(0.5) * h * k[i];
+  }
+  f(xs, k);
 #pragma unroll
-  for (int i = 0; i < NX; ++i) xs[i] = x[i] + T(0.5) * h * k2[i];
-  f(xs, k3);
+  for (int i = 0; i < NX; ++i) {
+    acc[i] = acc[i] + T(2) * k[i];
+    xs[i] = x[i] + T(0.5) * h * k[i];
+  }
+  f(xs, k);
 #pragma unroll
-  for (int i = 0; i < NX; ++i) xs[i] = x[i] + h * k3[i];
-  f(xs, k4);
+  for (int i = 0; i < NX; ++i) {
+    acc[i] = acc[i] + T(2) * k[i];
+    xs[i] = x[i] + h * k[i];
+  }
+  f(xs, k);
   const T sixth = T(1.0 / 6.0);
 #pragma unroll
-  for (int i = 0; i < NX; ++i) xn[i] = x[i] + h * sixth * (k1[i] + T(2) * k2[i] + T(2) * k3[i] + k4[i]);
+  for (int i = 0; i < NX; ++i) xn[i] = x[i] + h * sixth * (acc[i] + k[i]);
 }
 
 }  // namespace vc

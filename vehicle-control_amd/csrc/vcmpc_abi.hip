@@ -108,12 +108,71 @@ vc::ModelArgs model_args(const vc_ctx* c, int B) {
   m.B = B;
   m.N = c->N;
   m.L = c->p.kin_car.l;
-  m.dyn = c->p.dyn_car;
+  m.dyn64 = vc::make_dyn_coef<double>(c->p.dyn_car);
+  m.dyn32 = vc::make_dyn_coef<float>(c->p.dyn_car);
   return m;
 }
 
 bool kin_solve_built(const vc_ctx* c) {
   return c->model == VC_MODEL_KINEMATIC && c->dtype == VC_F64 && vc::kin_ltv_smem_bytes(c->N) > 0;
+}
+bool dyn_solve_built(const vc_ctx* c) {
+  return c->model == VC_MODEL_DYNAMIC && c->dtype == VC_F32 && vc::dyn_sqp_smem_bytes(c->N) > 0;
+}
+
+// Dynamic single-track SQP (dyn_sqp.hip), fp32: xbar has N state columns.
+int dyn_solve(vc_ctx* c, int B, const void* x0, const void* kappa, const void* ds, void* xbar, void* ubar, void* u0,
+              int32_t* status, int32_t* iters, void* diag, int flags, void* dbg = nullptr) {
+  const int N = c->N, nx = 8, nu = 2;
+  const vc_dyn_mpc& w = c->p.dyn_mpc;
+  if (w.sqp_iters < 1 || w.sqp_iters > 64) return fail(c, VC_E_ARG, "dyn_mpc.sqp_iters=%d outside [1,64]", w.sqp_iters);
+  if (!(w.fx_scale > 0)) return fail(c, VC_E_ARG, "dyn_mpc.fx_scale must be > 0");
+  if (c->p.qp.max_iter < 1) return fail(c, VC_E_ARG, "qp.max_iter must be >= 1");
+  vc::DynSqpArgs a{};
+  a.B = B;
+  a.car = vc::make_dyn_coef<float>(c->p.dyn_car);
+  a.w = w;
+  a.qp = c->p.qp;
+  std::vector<Slot> slots;
+  if (flags == VC_HOST_PTRS) {
+    slots = {{x0, nullptr, (size_t)B * nx * 4, nullptr},
+             {kappa, nullptr, (size_t)B * N * 4, nullptr},
+             {ds, nullptr, (size_t)B * N * 4, nullptr},
+             {ubar, ubar, (size_t)B * N * nu * 4, nullptr},
+             {nullptr, xbar, (size_t)B * N * nx * 4, nullptr},
+             {nullptr, u0, (size_t)B * nu * 4, nullptr},
+             {nullptr, status, (size_t)B * 4, nullptr},
+             {nullptr, iters, (size_t)B * 4, nullptr},
+             {nullptr, diag, diag ? (size_t)B * 4 * 4 : 0, nullptr},
+             {nullptr, dbg, dbg ? (size_t)B * vc::dyn_sqp_debug_stride() * 4 : 0, nullptr}};
+    if (int r = stage(c, slots)) return r;
+    a.dbg = dbg ? (float*)slots[9].dev : nullptr;
+    a.x0 = (const float*)slots[0].dev;
+    a.kappa = (const float*)slots[1].dev;
+    a.ds = (const float*)slots[2].dev;
+    a.ubar = (const float*)slots[3].dev;
+    a.u_out = (float*)slots[3].dev;
+    a.x_out = (float*)slots[4].dev;
+    a.u0 = (float*)slots[5].dev;
+    a.status = (int32_t*)slots[6].dev;
+    a.iters = (int32_t*)slots[7].dev;
+    a.diag = diag ? (float*)slots[8].dev : nullptr;
+  } else {
+    a.x0 = (const float*)x0;
+    a.kappa = (const float*)kappa;
+    a.ds = (const float*)ds;
+    a.ubar = (const float*)ubar;
+    a.u_out = (float*)ubar;
+    a.x_out = (float*)xbar;
+    a.u0 = (float*)u0;
+    a.status = status;
+    a.iters = iters;
+    a.diag = (float*)diag;
+    a.dbg = (float*)dbg;
+  }
+  VC_HIP(c, vc::launch_dyn_sqp(a, N, c->stream));
+  if (flags == VC_HOST_PTRS) return unstage(c, slots);
+  return 0;
 }
 }  // namespace
 
@@ -187,11 +246,13 @@ int vc_solve(vc_ctx* c, int B, const void* x0, const void* kappa, const void* ds
 int vc_solve_diag(vc_ctx* c, int B, const void* x0, const void* kappa, const void* ds, void* xbar, void* ubar,
                   void* u0, int32_t* status, int32_t* iters, void* diag, int flags) {
   if (int r = check_common(c, B, flags)) return r;
-  if (!kin_solve_built(c))
-    return fail(c, VC_E_UNSUPPORTED, "vc_solve: model=%d dtype=%d N=%d not built (kinematic fp64 N=20 is)", c->model,
+  if (!kin_solve_built(c) && !dyn_solve_built(c))
+    return fail(c, VC_E_UNSUPPORTED,
+                "vc_solve: model=%d dtype=%d N=%d not built (kinematic fp64 N=20 and dynamic fp32 N=40 are)", c->model,
                 c->dtype, c->N);
   if (!x0 || !kappa || !ds || !xbar || !ubar || !u0 || !status || !iters) return fail(c, VC_E_ARG, "null pointer");
   if (B == 0) return 0;
+  if (c->model == VC_MODEL_DYNAMIC) return dyn_solve(c, B, x0, kappa, ds, xbar, ubar, u0, status, iters, diag, flags);
   const int N = c->N, nx = 6, nu = 2;
   vc::KinLtvArgs a{};
   a.mode = 0;
@@ -237,6 +298,18 @@ int vc_solve_diag(vc_ctx* c, int B, const void* x0, const void* kappa, const voi
   if (flags == VC_HOST_PTRS) return unstage(c, slots);
   return 0;
 }
+
+int vc_solve_debug(vc_ctx* c, int B, const void* x0, const void* kappa, const void* ds, void* xbar, void* ubar,
+                   void* u0, int32_t* status, int32_t* iters, void* dbg, int flags) {
+  if (int r = check_common(c, B, flags)) return r;
+  if (!dyn_solve_built(c)) return fail(c, VC_E_UNSUPPORTED, "vc_solve_debug: dynamic fp32 N=40 contexts only");
+  if (!x0 || !kappa || !ds || !xbar || !ubar || !u0 || !status || !iters || !dbg)
+    return fail(c, VC_E_ARG, "null pointer");
+  if (B == 0) return 0;
+  return dyn_solve(c, B, x0, kappa, ds, xbar, ubar, u0, status, iters, nullptr, flags, dbg);
+}
+
+int vc_debug_stride(void) { return vc::dyn_sqp_debug_stride(); }
 
 int vc_condense(vc_ctx* c, int B, const void* x0, const void* ubar, const void* kappa, const void* ds, void* H,
                 void* g, int flags) {

@@ -12,7 +12,7 @@ import os
 
 LIB_NAME = "libvcmpc.so"
 LIB_PATH = os.environ.get("VCMPC_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME))
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 VC_MODEL_KINEMATIC, VC_MODEL_DYNAMIC = 0, 1
 VC_F64, VC_F32 = 0, 1
@@ -42,13 +42,21 @@ class vc_kin_mpc(C.Structure):
         "v_min", "v_max", "delta_min", "delta_max", "ey_min", "ey_max")]
 
 
+class vc_dyn_mpc(C.Structure):
+    _fields_ = [(k, C.c_double) for k in (
+        "w_time", "w_speed", "w_ey", "w_epsi", "w_w", "w_Fx", "w_dev", "w_b", "w_slip",
+        "w_min", "w_max", "Ux_min", "max_speed", "delta_min", "delta_max", "ey_min", "ey_max",
+        "fx_scale", "trust_Fx")] + [("sqp_iters", C.c_int32), ("pad_", C.c_int32)]
+
+
 class vc_qp(C.Structure):
     _fields_ = [("prox", C.c_double), ("tol", C.c_double), ("trust_a", C.c_double), ("trust_w", C.c_double),
                 ("max_iter", C.c_int32), ("polish", C.c_int32)]
 
 
 class vc_params(C.Structure):
-    _fields_ = [("kin_car", vc_kin_car), ("dyn_car", vc_dyn_car), ("kin_mpc", vc_kin_mpc), ("qp", vc_qp)]
+    _fields_ = [("kin_car", vc_kin_car), ("dyn_car", vc_dyn_car), ("kin_mpc", vc_kin_mpc), ("qp", vc_qp),
+                ("dyn_mpc", vc_dyn_mpc)]
 
 
 class VcError(RuntimeError):
@@ -73,6 +81,8 @@ PROTOTYPES = {
     "vc_synchronize": (C.c_int, [_vp]),
     "vc_solve": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int]),
     "vc_solve_diag": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int]),
+    "vc_solve_debug": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int]),
+    "vc_debug_stride": (C.c_int, []),
     "vc_rollout": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, C.c_int]),
     "vc_linearize": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int]),
     "vc_condense": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int]),

@@ -16,6 +16,9 @@ CONFIG_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file
 
 # The build's LTV-QP contract defaults (no reference counterpart).
 QP_DEFAULTS = {"prox": 1e-4, "tol": 1e-10, "max_iter": 40, "polish": 10, "trust_a": 0.0, "trust_w": 0.0}
+# The dynamic SQP contract defaults (config/dynamic_mpc.yaml `qp` block).
+DYN_QP_DEFAULTS = {"prox": 1e-3, "tol": 1e-5, "max_iter": 60, "polish": 0, "trust_a": 0.0, "trust_w": 0.2,
+                   "fx_scale": 1000.0, "trust_Fx": 2000.0, "sqp_iters": 3}
 
 
 class AttrDict(dict):
@@ -65,8 +68,8 @@ def kin_mpc_struct(cfg) -> _abi.vc_kin_mpc:
         delta_max=float(sc["delta_max"]), ey_min=float(sc["ey_min"]), ey_max=float(sc["ey_max"]))
 
 
-def qp_struct(cfg=None) -> _abi.vc_qp:
-    q = dict(QP_DEFAULTS)
+def qp_struct(cfg=None, defaults=None) -> _abi.vc_qp:
+    q = dict(QP_DEFAULTS if defaults is None else defaults)
     if cfg is not None and cfg.get("qp") is not None:
         q.update(cfg["qp"])
     return _abi.vc_qp(prox=float(q["prox"]), tol=float(q["tol"]), trust_a=float(q["trust_a"]),
@@ -87,8 +90,25 @@ def dyn_car_struct(cfg, tyre: str = "fiala") -> _abi.vc_dyn_car:
         tyre=_abi.VC_TYRE_LINEAR if tyre == "linear" else _abi.VC_TYRE_FIALA)
 
 
-def make_params(kin_car=None, dyn_car=None, kin_mpc=None, tyre: str = "fiala") -> _abi.vc_params:
-    """Pack whichever configs are given into one ``vc_params`` (others zeroed)."""
+def dyn_mpc_struct(cfg) -> _abi.vc_dyn_mpc:
+    """Weights and bounds of a single-track controller config (reference schema
+    config/controllers/singletrack.yaml, read at cascaded_mpc.py:91-179,279-304)
+    plus the SQP knobs of its `qp` block."""
+    cw, ic, sc = cfg["cost_weights"], cfg["input_constraints"], cfg["state_constraints"]
+    q = dict(DYN_QP_DEFAULTS)
+    q.update(cfg.get("qp") or {})
+    return _abi.vc_dyn_mpc(
+        w_time=float(cw["time"]), w_speed=float(cw["speed"]), w_ey=float(cw["ey"]), w_epsi=float(cw["epsi"]),
+        w_w=float(cw["w"]), w_Fx=float(cw["Fx"]), w_dev=float(cw["deviation_st"]), w_b=float(cw["boundary"]),
+        w_slip=float(cw["slip"]), w_min=float(ic["w_min"]), w_max=float(ic["w_max"]),
+        Ux_min=float(sc["Ux_min"]), max_speed=float(sc["max_speed"]), delta_min=float(sc["delta_min"]),
+        delta_max=float(sc["delta_max"]), ey_min=float(sc["ey_min"]), ey_max=float(sc["ey_max"]),
+        fx_scale=float(q["fx_scale"]), trust_Fx=float(q["trust_Fx"]), sqp_iters=int(q["sqp_iters"]))
+
+
+def make_params(kin_car=None, dyn_car=None, kin_mpc=None, dyn_mpc=None, tyre: str = "fiala") -> _abi.vc_params:
+    """Pack whichever configs are given into one ``vc_params`` (others zeroed).
+    The QP knobs come from the controller config given (kinematic or dynamic)."""
     p = _abi.vc_params()
     if kin_car is not None:
         p.kin_car = _abi.vc_kin_car(l=float(kin_car["car"]["l"]))
@@ -96,5 +116,9 @@ def make_params(kin_car=None, dyn_car=None, kin_mpc=None, tyre: str = "fiala") -
         p.dyn_car = dyn_car_struct(dyn_car, tyre)
     if kin_mpc is not None:
         p.kin_mpc = kin_mpc_struct(kin_mpc)
-    p.qp = qp_struct(kin_mpc)
+    if dyn_mpc is not None:
+        p.dyn_mpc = dyn_mpc_struct(dyn_mpc)
+        p.qp = qp_struct(dyn_mpc, DYN_QP_DEFAULTS)
+    else:
+        p.qp = qp_struct(kin_mpc)
     return p

@@ -8,7 +8,10 @@ work on the context stream -- the fast path, used by ``bench.py``).
 Shapes (batch-outermost, C-contiguous, state/action orders of the reference
 FancyVector keys, see include/vcmpc.h):
 
-    x0[B, nx]  kappa[B, N]  ds[B, N]  ubar[B, N, nu]  xbar[B, N+1, nx]  u0[B, nu]
+    x0[B, nx]  kappa[B, N]  ds[B, N]  ubar[B, N, nu]  xbar[B, NS, nx]  u0[B, nu]
+
+NS = N + 1 state columns for the kinematic model (kinematic_mpc.py:59), N for the
+dynamic single-track model (cascaded_mpc.py:70); vc_rollout / vc_linearize use N + 1.
 """
 from __future__ import annotations
 
@@ -36,6 +39,7 @@ class Context:
         self.lib = _abi.load_library()
         self.model, self.N, self.max_batch, self.dtype, self.device = model, int(N), int(max_batch), dtype, device
         self.nx = NX[model]
+        self.ns_solve = self.N + 1 if model == _abi.VC_MODEL_KINEMATIC else self.N
         self.params = params if params is not None else make_params(**cfgs)
         h = self.lib.vc_create(device, model, self.N, self.max_batch, dtype, C.byref(self.params))
         if not h:
@@ -102,25 +106,27 @@ class Context:
 
     # -- entry points -------------------------------------------------------------
     def solve(self, x0, kappa, ds, ubar, xbar=None, u0=None, status=None, iters=None, diag=None):
-        """One LTV-MPC step (``vc_solve``).  ``ubar`` is the warm start and is
+        """One MPC step (``vc_solve``: LTV-QP for the kinematic model, SQP for the
+        dynamic one).  ``ubar`` is the warm start and is
         overwritten with u*; returns (u0, xbar, ubar, status, iters).  With
         ``diag=True`` (or a [B, 4] buffer) it calls ``vc_solve_diag`` and returns
         the per-problem solver diagnostics as a sixth element."""
         B, N, nx, f = self._batch(x0), self.N, self.nx, _NP_DT[self.dtype]
+        NS = self.ns_solve
         if _is_torch(x0):
             import torch
             kw = dict(device=x0.device)
-            xbar = torch.empty((B, N + 1, nx), dtype=x0.dtype, **kw) if xbar is None else xbar
+            xbar = torch.empty((B, NS, nx), dtype=x0.dtype, **kw) if xbar is None else xbar
             u0 = torch.empty((B, NU), dtype=x0.dtype, **kw) if u0 is None else u0
             status = torch.empty((B,), dtype=torch.int32, **kw) if status is None else status
             iters = torch.empty((B,), dtype=torch.int32, **kw) if iters is None else iters
         else:
-            xbar = np.empty((B, N + 1, nx), f) if xbar is None else xbar
+            xbar = np.empty((B, NS, nx), f) if xbar is None else xbar
             u0 = np.empty((B, NU), f) if u0 is None else u0
             status = np.empty((B,), np.int32) if status is None else status
             iters = np.empty((B,), np.int32) if iters is None else iters
         bufs = [x0, kappa, ds, xbar, ubar, u0, status, iters]
-        shapes = [(B, nx), (B, N), (B, N), (B, N + 1, nx), (B, N, NU), (B, NU), (B,), (B,)]
+        shapes = [(B, nx), (B, N), (B, N), (B, NS, nx), (B, N, NU), (B, NU), (B,), (B,)]
         dts = [f, f, f, f, f, f, np.int32, np.int32]
         if diag is not None and diag is not False:
             if diag is True:
@@ -131,6 +137,22 @@ class Context:
         ptrs, flags = self._marshal(bufs, shapes, dts)
         self._check(self.lib.vc_solve(self._h, B, *ptrs, flags))
         return u0, xbar, ubar, status, iters
+
+    def solve_debug(self, x0, kappa, ds, ubar):
+        """``vc_solve_debug`` (dynamic contexts): the solve plus a dump of the first
+        QP's internals (g, normal matrix, factor storage, predictor rhs and step)."""
+        B, N, nx, f = self._batch(x0), self.N, self.nx, np.float32
+        stride = self.lib.vc_debug_stride()
+        xbar, u0 = np.empty((B, self.ns_solve, nx), f), np.empty((B, NU), f)
+        status, iters, dbg = np.empty(B, np.int32), np.empty(B, np.int32), np.empty((B, stride), f)
+        ptrs, flags = self._marshal([x0, kappa, ds, xbar, ubar, u0, status, iters, dbg],
+                                    [(B, nx), (B, N), (B, N), (B, self.ns_solve, nx), (B, N, NU), (B, NU), (B,),
+                                     (B,), (B, stride)], [f] * 6 + [np.int32, np.int32, f])
+        self._check(self.lib.vc_solve_debug(self._h, B, *ptrs, flags))
+        n = 2 * N
+        return dict(u0=u0, xbar=xbar, ubar=ubar, status=status, iters=iters, g=dbg[:, :n],
+                    M=dbg[:, n:n + n * n].reshape(B, n, n), Y=dbg[:, n + n * n:n + 2 * n * n].reshape(B, n, n),
+                    rhs=dbg[:, n + 2 * n * n:2 * n + 2 * n * n], dz=dbg[:, 2 * n + 2 * n * n:3 * n + 2 * n * n])
 
     def rollout(self, x0, ubar, kappa, ds):
         B, N, nx, f = self._batch(x0), self.N, self.nx, _NP_DT[self.dtype]
