@@ -64,7 +64,7 @@ def dyn_weights(cfg: dict) -> dict:
         Ux_min=float(sc["Ux_min"]), max_speed=float(sc["max_speed"]),
         delta_min=float(sc["delta_min"]), delta_max=float(sc["delta_max"]),
         ey_min=float(sc["ey_min"]), ey_max=float(sc["ey_max"]),
-        prox=float(qp.get("prox", 1e-3)), fx_scale=float(qp.get("fx_scale", 1000.0)),
+        prox=float(qp.get("prox", 0.1)), fx_scale=float(qp.get("fx_scale", 1000.0)),
         trust_Fx=float(qp.get("trust_Fx", 0.0)), trust_w=float(qp.get("trust_w", 0.0)),
         sqp_iters=int(qp.get("sqp_iters", 3)),
     )

@@ -19,9 +19,9 @@ B = len(g["x0"])
 S = np.array([1000.0, 1.0])
 p = M.dyn_params_from_config(load_config("dynamic_car"))
 f64 = {k: g[k].astype(np.float64) for k in ("x0", "ubar", "kappa", "ds")}
-for prox in [float(a) for a in (sys.argv[1:] or ["1e-3"])]:
+for prox in [float(a) for a in (sys.argv[1:] or ["0.1"])]:
     for iters in (1, 3):
-        for tol in (1e-5, 1e-6, 1e-7):
+        for tol in (1e-5, 1e-6):
             cfg = copy.deepcopy(load_config("dynamic_mpc"))
             cfg["qp"]["sqp_iters"] = iters
             cfg["qp"]["tol"] = tol

@@ -1,0 +1,183 @@
+"""GPU parity of the dynamic single-track SQP kernel (csrc/dyn_sqp.hip, fp32, N = 40)
+through the C ABI, against the fp64 oracle (oracle/dyn_sqp.py) and its golden vectors.
+
+Tolerance (BASELINE config 3 is fp32; SURVEY 7 "Hard parts": an absolute 1e-5 on
+Fx ~ 1e3-1e4 N is below fp32 resolution, so the bar is stated on the scaled decision
+variable (Fx / fx_scale [kN], w [rad/s])):   max |u* - u*_oracle| / (1000, 1) < 1e-4.
+"""
+import copy
+
+import numpy as np
+import pytest
+
+from oracle import dyn_sqp as D
+from oracle import models as M
+
+pytestmark = pytest.mark.gpu
+
+U_TOL = 1e-4                  # scaled u*, linear tyre (config 3)
+U_TOL_FIALA = 5e-4            # the Fiala tyre's cubic region amplifies fp32 rounding across the SQP steps
+X_TOL = 5e-3                  # x* = rollout(u*), absolute, fp32 over 40 RK4 stages
+SCALE = np.array([1000.0, 1.0])
+N = 40
+
+
+def _ctx(mpc_cfg=None, tyre="linear", max_batch=4096):
+    from vcmpc import Context, _abi
+    from vcmpc.config import load_config, make_params
+    params = make_params(dyn_car=load_config("dynamic_car"),
+                         dyn_mpc=mpc_cfg if mpc_cfg is not None else load_config("dynamic_mpc"), tyre=tyre)
+    return Context(model=_abi.VC_MODEL_DYNAMIC, N=N, max_batch=max_batch, dtype=_abi.VC_F32, params=params)
+
+
+@pytest.fixture(scope="module")
+def sqp():
+    c = _ctx()
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def golden():
+    import os
+    from conftest import GOLDEN
+    return dict(np.load(os.path.join(GOLDEN, "dyn_sqp_golden.npz")))
+
+
+@pytest.fixture(scope="module")
+def W():
+    from vcmpc.config import load_config
+    return D.dyn_weights(load_config("dynamic_mpc"))
+
+
+def _err(u, ref):
+    return np.abs((np.asarray(u, np.float64) - ref) / SCALE).max(axis=(1, 2))
+
+
+def test_sqp_vs_golden(sqp, golden):
+    g = golden
+    ub = g["ubar"].copy()
+    u0, xs, us, st, it, dg = sqp.solve(g["x0"], g["kappa"], g["ds"], ub, diag=True)
+    assert (st == 0).all(), st
+    flags = dg[:, 2].astype(int)
+    assert ((flags & 6) == 6).all(), flags     # every QP converged and polish-certified
+    assert _err(us, g["u_star"]).max() < U_TOL
+    np.testing.assert_allclose(u0, us[:, 0])
+    assert np.abs(xs - g["x_star"]).max() < X_TOL
+    assert (it > 0).all() and (it <= 3 * 60).all()
+
+
+def test_first_qp_stage_by_stage(sqp, golden, dyn_params, W):
+    """The kernel's first QP: gradient, interior-point normal matrix, its inverse
+    factor, predictor right-hand side and step, each against the oracle's fp64 data."""
+    B = 6
+    sl = slice(0, B)
+    g = golden
+    r = sqp.solve_debug(g["x0"][sl].copy(), g["kappa"][sl].copy(), g["ds"][sl].copy(), g["ubar"][sl].copy())
+    f = {k: g[k][sl].astype(np.float64) for k in ("x0", "ubar", "kappa", "ds")}
+    Q = D.dyn_qp(f["x0"], f["ubar"], f["kappa"], f["ds"], dyn_params, W, "linear")
+    n = 2 * N
+    low = np.tril(np.ones((n, n), bool))
+    rel = lambda a, o: np.abs(a - o).max() / np.abs(o).max()
+    for b in range(B):
+        H, gg, C, d = Q["H"][b], Q["g"][b], Q["C"][b], Q["d"][b]
+        s0 = np.maximum(d, 1.0)
+        Mo = H + C.T @ (C / s0[:, None])
+        rhs = -gg - C.T @ ((s0 - d) / s0)
+        assert rel(r["g"][b], gg) < 1e-5
+        assert rel(r["M"][b][low], Mo[low]) < 1e-5
+        assert rel(r["rhs"][b], rhs) < 1e-5
+        assert rel(r["dz"][b], np.linalg.solve(Mo, rhs)) < 1e-3
+        Y = np.triu(r["Y"][b])
+        assert np.abs(Y @ Y.T @ Mo - np.eye(n)).max() < 1e-3
+
+
+def test_sqp_fresh_batch_vs_oracle(sqp, dyn_params, W):
+    from vcmpc.workload import dynamic_batch
+    d = dynamic_batch(12, seed=77)
+    ub = d["ubar"].copy()
+    u0, xs, us, st, it = sqp.solve(d["x0"], d["kappa"], d["ds"], ub)
+    f = {k: v.astype(np.float64) for k, v in d.items()}
+    ref = D.dyn_sqp_solve(f["x0"], f["ubar"], f["kappa"], f["ds"], dyn_params, W, "linear")
+    assert (st == 0).all()
+    assert _err(us, ref["u_star"]).max() < U_TOL
+
+
+def test_sqp_fiala_tyre(dyn_params):
+    """The contract also runs on the reference's modified-Fiala tyre (dynamic_car.py:117-142)."""
+    from vcmpc.config import load_config
+    from vcmpc.workload import dynamic_batch
+    cfg = load_config("dynamic_mpc")
+    Wf = D.dyn_weights(cfg)
+    d = dynamic_batch(8, seed=21, tyre="fiala")
+    with _ctx(cfg, tyre="fiala", max_batch=8) as c:
+        ub = d["ubar"].copy()
+        u0, xs, us, st, it = c.solve(d["x0"], d["kappa"], d["ds"], ub)
+    f = {k: v.astype(np.float64) for k, v in d.items()}
+    ref = D.dyn_sqp_solve(f["x0"], f["ubar"], f["kappa"], f["ds"], dyn_params, Wf, "fiala")
+    assert (st == 0).all()
+    assert _err(us, ref["u_star"]).max() < U_TOL_FIALA
+
+
+def test_sqp_iteration_count_and_trust_region(dyn_params):
+    """One SQP iteration = one QP step about the warm start; the step respects the
+    trust region |dFx| <= trust_Fx, |dw| <= trust_w."""
+    from vcmpc.config import load_config
+    from vcmpc.workload import dynamic_batch
+    cfg = copy.deepcopy(load_config("dynamic_mpc"))
+    cfg["qp"]["sqp_iters"] = 1
+    W1 = D.dyn_weights(cfg)
+    d = dynamic_batch(10, seed=8)
+    with _ctx(cfg, max_batch=16) as c:
+        ub = d["ubar"].copy()
+        u0, xs, us, st, it = c.solve(d["x0"], d["kappa"], d["ds"], ub)
+    f = {k: v.astype(np.float64) for k, v in d.items()}
+    ref = D.dyn_sqp_solve(f["x0"], f["ubar"], f["kappa"], f["ds"], dyn_params, W1, "linear")
+    assert _err(us, ref["u_star"]).max() < U_TOL
+    du = us.astype(np.float64) - f["ubar"]
+    assert np.abs(du[..., 0]).max() <= 2000.0 * (1 + 1e-5) and np.abs(du[..., 1]).max() <= 0.2 * (1 + 1e-5)
+
+
+def test_sqp_batch_properties(sqp, dyn_params, W):
+    """B = 4096 (BASELINE config 3): all solved, inputs inside their boxes, bit-identical
+    reruns, a sample checked against the oracle."""
+    from vcmpc.workload import dynamic_batch
+    B = 4096
+    d = dynamic_batch(B, seed=31)
+    ub1, ub2 = d["ubar"].copy(), d["ubar"].copy()
+    r1 = sqp.solve(d["x0"], d["kappa"], d["ds"], ub1)
+    r2 = sqp.solve(d["x0"], d["kappa"], d["ds"], ub2)
+    assert (r1[3] == 0).mean() >= 0.999
+    assert np.array_equal(ub1, ub2) and np.array_equal(r1[1], r2[1])
+    assert np.abs(ub1[..., 1]).max() <= 0.4 + 1e-4   # active rows certified to ~2e-6 (1 + max|d|)
+    idx = np.arange(0, B, B // 6)
+    f = {k: v[idx].astype(np.float64) for k, v in d.items()}
+    ref = D.dyn_sqp_solve(f["x0"], f["ubar"], f["kappa"], f["ds"], dyn_params, W, "linear")
+    assert _err(ub1[idx], ref["u_star"]).max() < U_TOL
+
+
+def test_sqp_edge_batches(sqp, golden):
+    from vcmpc import _abi
+    g = golden
+    # B = 0 is a no-op
+    sqp.solve(g["x0"][:0].copy(), g["kappa"][:0].copy(), g["ds"][:0].copy(), g["ubar"][:0].copy())
+    # a non-finite problem is flagged without disturbing the rest of the batch
+    x0 = g["x0"].copy(); x0[3, 0] = np.nan
+    ub = g["ubar"].copy()
+    u0, xs, us, st, it = sqp.solve(x0, g["kappa"], g["ds"], ub)
+    assert st[3] == _abi.VC_NONFINITE
+    ok = np.arange(len(x0)) != 3
+    assert (st[ok] == 0).all() and _err(us[ok], g["u_star"][ok]).max() < U_TOL
+    with pytest.raises(ValueError):
+        sqp.solve(np.zeros((5000, 8), np.float32), np.zeros((5000, N), np.float32),
+                  np.zeros((5000, N), np.float32), np.zeros((5000, N, 2), np.float32))
+
+
+def test_unsupported_dynamic_combination():
+    from vcmpc import Context, _abi
+    from vcmpc.config import load_config
+    with Context(model=_abi.VC_MODEL_DYNAMIC, N=40, max_batch=4, dtype=_abi.VC_F64,
+                 dyn_car=load_config("dynamic_car")) as c:
+        with pytest.raises(_abi.VcError) as e:
+            c.solve(np.zeros((1, 8)), np.zeros((1, N)), np.zeros((1, N)), np.zeros((1, N, 2)))
+        assert e.value.code == _abi.VC_E_UNSUPPORTED

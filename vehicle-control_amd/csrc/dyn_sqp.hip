@@ -85,7 +85,7 @@ struct DynSmem {
   float y[N][8];             // forward pass: (Ux,Uy,r,dlt,ey) of V_k z, [5] terminal epsi
   float va[2][N][8];         // adjoint inputs: (Ux,Uy,r,dlt,ey, Fx-unit, w-direct, epsi(N-1))
   float part[2][3][D::n];    // adjoint / mat-vec partial sums
-  float vz[D::n], vd[D::n], vr[D::n], vg[D::n], vt[D::n];
+  float vz[D::n], vd[D::n], vr[D::n], vg[D::n], vt[D::n], vp[D::n];
   float ddw[N];              // barrier weight on w_k (box rows)
   float red[16];
   int flag[4];
@@ -618,7 +618,7 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
   for (int e = t; e < 2 * N * 8; e += NTH) (&s.va[0][0][0])[e] = 0.f;
   __syncthreads();
 
-  int it_total = 0, it_max = 0;
+  int it_total = 0, it_max = 0, n_polished = 0;
   bool all_conv = true, any_fail = false;
   float last_res = 0.f, last_mu = 0.f;
 
@@ -794,6 +794,56 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
     const float slew_prev = (t < n && (t & 1) == 0 && kc >= 1) ? 2.f * float(W.w_Fx) / s.dsv[kc - 1] * S * S : 0.f;
     const float hdiag = prox2 + ((t & 1) ? 2.f * float(W.w_w) : slew_here + slew_prev);
 
+    // M = H + C' diag(w) C on the stage blocks (+ direct part), ready for chol_inverse.
+    // w[3]: this stage lane's row weights (barrier weights, or rho on the polish's active set)
+    auto assemble = [&](const float* w) {
+      if (stl) {
+        float w15[15], dw = 0.f;
+#pragma unroll
+        for (int e = 0; e < 15; ++e) w15[e] = wc[e];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+#pragma unroll
+          for (int a = 0; a < 5; ++a)
+#pragma unroll
+            for (int c = a; c < 5; ++c) w15[sym5(a, c)] += w[i] * R.c[i][a] * R.c[i][c];
+          dw += w[i] * R.c[i][5] * R.c[i][5];
+        }
+#pragma unroll
+        for (int e = 0; e < 15; ++e) w15[e] = quad_sum(w15[e]);
+        dw = quad_sum(dw);
+        if (q == 0) {
+#pragma unroll
+          for (int a = 0; a < 5; ++a)
+#pragma unroll
+            for (int c = 0; c < 5; ++c) s.W[k][5 * a + c] = w15[sym5(a, c)];
+          s.W[k][25] = qey;
+          s.W[k][26] = qep;
+          s.ddw[k] = dw;
+        }
+      }
+      __syncthreads();
+      build_normal(s, wv, lane);
+      for (int e = t; e < 10 * TS * TS; e += NTH) {  // upper tiles start at 0 (augmented rows)
+        int rem = e >> 8, P = 0;
+        while (rem >= DD<N>::NTL - 1 - P) { rem -= DD<N>::NTL - 1 - P; ++P; }
+        const int K = P + 1 + rem;
+        s.u.M[TS * P + ((e & 255) >> 4)][TS * K + (e & 15)] = 0.f;
+      }
+      __syncthreads();
+      if (t < n) {
+        float d = hdiag;
+        if (t & 1) d += s.ddw[kc];
+        else if (kc == 0) d += s.W[0][24];
+        s.u.M[t][t] += d;
+        if ((t & 1) == 0 && kc >= 1) {
+          s.u.M[t][t - 2] -= slew_prev;
+          if ((t & 15) >= 2) s.u.M[t - 2][t] -= slew_prev;  // same diagonal tile: keep it symmetric
+        }
+      }
+      __syncthreads();
+    };
+
     // ---------------- interior point (Mehrotra predictor-corrector) ----------------
     int it = 0;
     bool conv = false, fail = false;
@@ -861,51 +911,7 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
       if (rdm <= tol * scale && rpm <= tol * scale && mu <= tol * scale) { conv = true; break; }
 
       // (b) normal matrix M = sum_k V_k' W_k V_k + D, blocked Cholesky, Y = L^-T
-      if (stl) {
-        float w15[15], dw = 0.f;
-#pragma unroll
-        for (int e = 0; e < 15; ++e) w15[e] = wc[e];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-#pragma unroll
-          for (int a = 0; a < 5; ++a)
-#pragma unroll
-            for (int c = a; c < 5; ++c) w15[sym5(a, c)] += wg[i] * R.c[i][a] * R.c[i][c];
-          dw += wg[i] * R.c[i][5] * R.c[i][5];
-        }
-#pragma unroll
-        for (int e = 0; e < 15; ++e) w15[e] = quad_sum(w15[e]);
-        dw = quad_sum(dw);
-        if (q == 0) {
-#pragma unroll
-          for (int a = 0; a < 5; ++a)
-#pragma unroll
-            for (int c = 0; c < 5; ++c) s.W[k][5 * a + c] = w15[sym5(a, c)];
-          s.W[k][25] = qey;
-          s.W[k][26] = qep;
-          s.ddw[k] = dw;
-        }
-      }
-      __syncthreads();
-      build_normal(s, wv, lane);
-      for (int e = t; e < 10 * TS * TS; e += NTH) {  // upper tiles start at 0 (augmented rows)
-        int rem = e >> 8, P = 0;
-        while (rem >= DD<N>::NTL - 1 - P) { rem -= DD<N>::NTL - 1 - P; ++P; }
-        const int K = P + 1 + rem;
-        s.u.M[TS * P + ((e & 255) >> 4)][TS * K + (e & 15)] = 0.f;
-      }
-      __syncthreads();
-      if (t < n) {
-        float d = hdiag;
-        if (t & 1) d += s.ddw[kc];
-        else if (kc == 0) d += s.W[0][24];
-        s.u.M[t][t] += d;
-        if ((t & 1) == 0 && kc >= 1) {
-          s.u.M[t][t - 2] -= slew_prev;
-          if ((t & 15) >= 2) s.u.M[t - 2][t] -= slew_prev;  // same diagonal tile: keep it symmetric
-        }
-      }
-      __syncthreads();
+      assemble(wg);
       const bool dump = A.dbg && sq == 0 && it == 0;
       if (dump)
         for (int e = t; e < n * n; e += NTH) A.dbg[(size_t)b * DBG_STRIDE + DBG_M + e] = s.u.M[e / n][e % n];
@@ -994,8 +1000,104 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
     }
     it_total += it;
     it_max = max(it_max, it);
-    all_conv = all_conv && conv;
+
+    // ---------------- active-set polish (augmented Lagrangian on the identified set) ------------
+    // The interior point stops at mu ~ tol * scale, which leaves O(mu / lambda) errors along
+    // weakly active rows.  Fix the active set it identified (lambda > s), solve
+    //   min 1/2 z'Hz + g'z  s.t.  C_A z = d_A
+    // by augmented-Lagrangian passes on one factorisation of H + rho C_A'C_A (multipliers
+    // warm-started from the interior point), then certify: inactive rows feasible, active
+    // multipliers >= 0.  A failed certificate adds every violated row and drops every
+    // negative multiplier for the next round (the oracle changes one row per round);
+    // after A.qp.polish rounds without a certificate the interior-point iterate is kept.
+    bool polished = false;
+    if (!fail && A.qp.polish > 0) {
+      const float rho = 1.0e4f;  // AL converges in ~4 passes; H + rho C_A'C_A stays ~1e5-conditioned
+      // tolerances on the O(1) rows (scaled units), not on the gradient-inflated `scale`
+      float dm = 0.f;
+      if (stl) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) dm = fmaxf(dm, R.m[i] * fabsf(R.d[i]));
+      }
+      const float dscale = 1.f + block_max(s, dm, wv, lane, 8);
+      const float eps_r = 5.0e-7f * dscale, eps_p = 1.0e-5f * dscale;
+      if (t < n) s.vp[t] = s.vz[t];  // interior-point solution (restored if not certified)
+      float act[3], nu[3], res[3];
+      if (stl) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          act[i] = (R.m[i] > 0.f && R.la[i] > R.sl[i]) ? 1.f : 0.f;
+          nu[i] = act[i] * R.la[i];
+          res[i] = 0.f;
+        }
+      }
+#pragma unroll 1
+      for (int round = 0; round < A.qp.polish; ++round) {
+        float w3[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) w3[i] = stl ? rho * act[i] : 0.f;
+        assemble(w3);
+        if (!chol_inverse(s, wv, lane, t)) break;
+        float rlast = 0.f;
+#pragma unroll 1
+        for (int pass = 0; pass < 12; ++pass) {
+          // rhs = -g - C' (nu - rho a d)
+          if (stl) {
+            float u6[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+              const float cf = nu[i] - rho * act[i] * R.d[i];
+#pragma unroll
+              for (int c = 0; c < 6; ++c) u6[c] += cf * R.c[i][c];
+            }
+            write_adj(s, 1, k, q, u6, 0.f, 0.f);
+          }
+          __syncthreads();
+          {
+            float o1[1];
+            adj_pass<N, 1>(s, t, o1, 1);
+            if (t < n) s.vr[t] = -s.vg[t] - o1[0];
+          }
+          __syncthreads();
+          solve(s, s.vr, s.vz, t);
+          fwd_pass(s, s.vz, t);
+          __syncthreads();
+          float rmax = 0.f;
+          if (stl) {
+            float bx[6];
+            stage_basis(s, s.vz, k, bx);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+              res[i] = R.m[i] * (row_val(R.c[i], bx) - R.d[i]);
+              nu[i] += rho * act[i] * res[i];
+              rmax = fmaxf(rmax, act[i] * fabsf(res[i]));
+            }
+          }
+          rlast = block_max(s, rmax, wv, lane, 0);
+          if (rlast <= eps_r) break;
+        }
+        // certificate
+        float bad = 0.f;
+        if (stl) {
+          const float nscale = 1e-5f * (1.f + fmaxf(fabsf(nu[0]), fmaxf(fabsf(nu[1]), fabsf(nu[2]))));
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            const bool viol = act[i] == 0.f && R.m[i] > 0.f && res[i] > eps_p;
+            const bool neg = act[i] > 0.f && nu[i] < -nscale;
+            if (viol || neg) bad = 1.f;
+            if (viol) act[i] = 1.f;
+            if (neg) { act[i] = 0.f; nu[i] = 0.f; }
+          }
+        }
+        // certified only with the equality-constrained solve converged as well
+        if (block_max(s, bad, wv, lane, 8) == 0.f && rlast <= 10.f * eps_r) { polished = true; break; }
+      }
+      if (!polished && t < n) s.vz[t] = s.vp[t];
+      __syncthreads();
+    }
+    all_conv = all_conv && (conv || polished);
     any_fail = any_fail || fail;
+    n_polished += polished ? 1 : 0;
 
     // ---------------- SQP update: ubar += du ----------------
     if (t < n) s.ub[t >> 1][t & 1] += s.vz[t] * ((t & 1) ? 1.f : S);
@@ -1028,7 +1130,8 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
     if (A.diag) {
       A.diag[(size_t)b * 4 + 0] = last_res;
       A.diag[(size_t)b * 4 + 1] = last_mu;
-      A.diag[(size_t)b * 4 + 2] = float((any_fail ? 1 : 0) | (all_conv ? 2 : 0));
+      A.diag[(size_t)b * 4 + 2] =
+          float((any_fail ? 1 : 0) | (all_conv ? 2 : 0) | (n_polished == W.sqp_iters ? 4 : 0) | (n_polished << 4));
       A.diag[(size_t)b * 4 + 3] = float(it_max);
     }
   }

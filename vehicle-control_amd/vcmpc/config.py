@@ -17,7 +17,7 @@ CONFIG_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file
 # The build's LTV-QP contract defaults (no reference counterpart).
 QP_DEFAULTS = {"prox": 1e-4, "tol": 1e-10, "max_iter": 40, "polish": 10, "trust_a": 0.0, "trust_w": 0.0}
 # The dynamic SQP contract defaults (config/dynamic_mpc.yaml `qp` block).
-DYN_QP_DEFAULTS = {"prox": 1e-3, "tol": 1e-5, "max_iter": 60, "polish": 0, "trust_a": 0.0, "trust_w": 0.2,
+DYN_QP_DEFAULTS = {"prox": 0.1, "tol": 1e-5, "max_iter": 60, "polish": 3, "trust_a": 0.0, "trust_w": 0.2,
                    "fx_scale": 1000.0, "trust_Fx": 2000.0, "sqp_iters": 3}
 
 
