@@ -135,7 +135,7 @@ def test_sqp_iteration_count_and_trust_region(dyn_params):
     ref = D.dyn_sqp_solve(f["x0"], f["ubar"], f["kappa"], f["ds"], dyn_params, W1, "linear")
     assert _err(us, ref["u_star"]).max() < U_TOL
     du = us.astype(np.float64) - f["ubar"]
-    assert np.abs(du[..., 0]).max() <= 2000.0 * (1 + 1e-5) and np.abs(du[..., 1]).max() <= 0.2 * (1 + 1e-5)
+    assert np.abs(du[..., 0]).max() <= 2000.0 * (1 + 1e-4) and np.abs(du[..., 1]).max() <= 0.2 * (1 + 1e-4)
 
 
 def test_sqp_batch_properties(sqp, dyn_params, W):

@@ -78,7 +78,7 @@ struct DynSmem {
     float M[D::n][D::LDM];   // normal matrix; lower tiles -> L (transient); upper + diag -> Y = L^-T
     float AB[N - 1][7][8];   // Jacobians [stage][row Ux,Uy,r,dlt,ey,eps,t][col Ux,Uy,r,dlt,ey,eps,Fx*S,w]
   } u;
-  float W[N][28];            // per-stage weight block: 5x5 over (Ux,Uy,r,dlt,Fx) row-major, [25] q_ey, [26] q_ep
+  float W[N][32];            // per-stage weight block: 5x5 over (Ux,Uy,r,dlt,Fx) at row stride 6, [30] q_ey, [31] q_ep
   float xb[N][8];
   float ub[N][2];
   float kap[N], dsv[N];
@@ -129,7 +129,7 @@ __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
 
 // ---- phase 1: predict (wave 0; every lane redundantly, lane 0 stores) ------------------
 template <int N>
-__device__ void predict(DynSmem<N>& s, const DynCoef<float>& p, int lane) {
+__device__ __forceinline__ void predict(DynSmem<N>& s, const DynCoef<float>& p, int lane) {
   float x[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) x[i] = s.xb[0][i];
@@ -151,7 +151,7 @@ __device__ void predict(DynSmem<N>& s, const DynCoef<float>& p, int lane) {
 // ---- phase 2: Jacobians of the RK4 spatial step by dual numbers (task = stage x seed pair)
 // seeds 0..7 = (Ux, Uy, r, dlt, ey, eps, Fx, w); output rows (Ux, Uy, r, dlt, ey, eps, t)
 template <int N>
-__device__ void linearize(DynSmem<N>& s, const DynCoef<float>& p, float S, int task) {
+__device__ __forceinline__ void linearize(DynSmem<N>& s, const DynCoef<float>& p, float S, int task) {
   const int k = task >> 2, pr = task & 3;
   using T = Dual<2>;
   T x[8], u[2];
@@ -187,7 +187,7 @@ __device__ void linearize(DynSmem<N>& s, const DynCoef<float>& p, float S, int t
 // G_{k0+1}[:, j] = B_{k0}[:, j&1] (k0 = j/2), G_{k+1} = A_k G_k; rows stored per stage.
 // Returns the terminal t-row entry G_t[N-1][j] (the time cost is linear in it).
 template <int N>
-__device__ float condense(DynSmem<N>& s, int j) {
+__device__ __forceinline__ float condense(DynSmem<N>& s, int j) {
   float g[7] = {0, 0, 0, 0, 0, 0, 0};  // Ux, Uy, r, dlt, ey, eps, t
   const int k0 = j >> 1;
 #pragma unroll 1
@@ -220,8 +220,9 @@ __device__ float condense(DynSmem<N>& s, int j) {
 
 // ---- forward pass: y_k = V_k z (Ux, Uy, r, dlt, ey), y[N-1][5] = epsi row --------------
 template <int N>
-__device__ void fwd_pass(DynSmem<N>& s, const float* z, int t) {
+__device__ __forceinline__ void fwd_pass(DynSmem<N>& s, const float* z, int t) {
   constexpr int NK = 4 * (N - 1);
+  no_hoist();  // G is invariant over an interior-point solve: keep its reads inside this pass
   if (t < NK) {
     const int k = 1 + (t >> 2), q = t & 3;
     const int len = 2 * k, per = (len + 3) >> 2;
@@ -230,7 +231,6 @@ __device__ void fwd_pass(DynSmem<N>& s, const float* z, int t) {
     const float* e = &s.Vey[voff(k)];
     float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f, a4 = 0.f;
     for (int j = j0; j < j1; ++j) {
-      no_hoist();
       const float4 v = g[j];
       const float zj = z[j];
       a0 += v.x * zj;
@@ -262,9 +262,10 @@ __device__ void fwd_pass(DynSmem<N>& s, const float* z, int t) {
 // Stage ranges [1,23), [23,33), [33,N) split the triangular work in thirds.  Valid in
 // threads t < n after the call (the call contains one barrier).
 template <int N, int NV>
-__device__ void adj_pass(DynSmem<N>& s, int t, float* out, int v0 = 0) {
+__device__ __forceinline__ void adj_pass(DynSmem<N>& s, int t, float* out, int v0 = 0) {
   constexpr int n = 2 * N;
   constexpr int lo[3] = {1, 23, 33}, hi[3] = {23, 33, N};
+  no_hoist();
   if (t < 3 * n) {
     const int j = t % n, gp = t / n;
     float acc[NV];
@@ -273,7 +274,6 @@ __device__ void adj_pass(DynSmem<N>& s, int t, float* out, int v0 = 0) {
     int off = voff(lo[gp]);
 #pragma unroll 1
     for (int k = lo[gp]; k < hi[gp]; ++k) {
-      no_hoist();
       const int w = vw(k);
       if (j < w) {
         const float4 g = s.Vg[off + j];
@@ -302,50 +302,79 @@ __device__ void adj_pass(DynSmem<N>& s, int t, float* out, int v0 = 0) {
 }
 
 // ---- normal matrix on the matrix cores ---------------------------------------------------
-// tiles (I, J), I >= J, assigned to waves by the number of contributing stages
-// (stage k contributes to row block I iff k >= 8 I).
-__constant__ int8_t kBuildTiles[4][4][2] = {
-    {{0, 0}, {3, 0}, {4, 0}, {4, 1}},
-    {{1, 0}, {1, 1}, {4, 2}, {-1, -1}},
-    {{2, 0}, {2, 1}, {3, 1}, {4, 3}},
-    {{2, 2}, {3, 2}, {3, 3}, {4, 4}},
-};
+// M = sum_k V_k' W_k V_k over stages k >= 1, lower 16x16 tiles (I, J), one K = 8 block per
+// stage: rows (Ux, Uy, r, dlt) and (ey, Fx-unit, epsi [k = N-1], 0).  Stage k contributes to
+// row block I iff k >= 8 I (its G rows are zero in columns >= 2k).  Each wave owns a fixed
+// tile list (balanced by contributing stages) and walks the stages once, reusing a stage's
+// operands across its tiles; operand selection by the lane's K row is branch-free.
+// W layout per stage: rows (Ux, Uy, r, dlt, Fx) of the 5x5 block at 6-float stride, then
+// q_ey at [30] and q_ep at [31].
+constexpr int WROW = 6;
 
-template <int N>
-__device__ void build_normal(DynSmem<N>& s, int wv, int lane) {
+// lane-row selection as an arithmetic blend (m[i] = [kk == i]): a select on a lane-varying
+// index otherwise becomes exec-masked control flow around the operand loads
+__device__ __forceinline__ float blend4(const float* m, float a, float b, float c, float d) {
+  return m[0] * a + m[1] * b + m[2] * c + m[3] * d;
+}
+
+template <int N, int I0, int J0, int I1, int J1, int I2, int J2, int I3, int J3>
+__device__ __forceinline__ void build_wave(DynSmem<N>& s, int lane) {
+  constexpr int TI[4] = {I0, I1, I2, I3}, TJ[4] = {J0, J1, J2, J3};
   const int i16 = lane & 15, kk = lane >> 4;
+  const float km[4] = {kk == 0 ? 1.f : 0.f, kk == 1 ? 1.f : 0.f, kk == 2 ? 1.f : 0.f, kk == 3 ? 1.f : 0.f};
+  f4 acc0[4], acc1[4];
+#pragma unroll
+  for (int tt = 0; tt < 4; ++tt) {
+    acc0[tt] = f4{0.f, 0.f, 0.f, 0.f};
+    acc1[tt] = f4{0.f, 0.f, 0.f, 0.f};
+  }
+  no_hoist();
 #pragma unroll 1
-  for (int q = 0; q < 4; ++q) {
-    const int I = kBuildTiles[wv][q][0], J = kBuildTiles[wv][q][1];
-    if (I < 0) break;
-    const int ci = TS * I + i16, cj = TS * J + i16;
-    f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-    const int k1 = I == 0 ? 1 : 8 * I;
-#pragma unroll 2
-    for (int k = k1; k < N; ++k) {
-      no_hoist();
-      const int off = voff(k);
-      const float* w = s.W[k];
-      const float4 vi = s.Vg[off + ci];
-      const float4 vj = s.Vg[off + cj];
-      const float fi = (ci == 2 * k) ? 1.f : 0.f, fj = (cj == 2 * k) ? 1.f : 0.f;
-      // K-block 0: rows (Ux, Uy, r, dlt); B = (W V)[row kk]
-      const float a0 = kk == 0 ? vi.x : kk == 1 ? vi.y : kk == 2 ? vi.z : vi.w;
-      const float* wr = w + 5 * kk;
-      const float b0 = wr[0] * vj.x + wr[1] * vj.y + wr[2] * vj.z + wr[3] * vj.w + wr[4] * fj;
-      acc0 = mfma4(a0, b0, acc0);
-      // K-block 1: rows (ey, Fx-unit, epsi [k = N-1], 0)
+  for (int k = 1; k < N; ++k) {
+    const int off = voff(k);
+    const float* w = s.W[k];
+    const float* wr = w + WROW * kk;  // W row kk (kk < 4) for K block 0
+    const float wk0 = wr[0], wk1 = wr[1], wk2 = wr[2], wk3 = wr[3], wk4 = wr[4];
+    const float wf0 = w[24], wf1 = w[25], wf2 = w[26], wf3 = w[27], wf4 = w[28];
+    const float qey = w[30], qep = w[31];
+    const bool last = (k == N - 1);
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      const int I = TI[tt], J = TJ[tt];
+      if (I < 0 || k < (I == 0 ? 1 : 8 * I)) continue;  // wave-uniform
+      const int ci = TS * I + i16, cj = TS * J + i16;
+      const float4 vi = s.Vg[off + ci], vj = s.Vg[off + cj];
       const float eyi = s.Vey[off + ci], eyj = s.Vey[off + cj];
-      const bool last = (k == N - 1);
-      const float epi = last ? s.Vep[ci] : 0.f, epj = last ? s.Vep[cj] : 0.f;
-      const float a1 = kk == 0 ? eyi : kk == 1 ? fi : kk == 2 ? epi : 0.f;
-      const float bF = w[20] * vj.x + w[21] * vj.y + w[22] * vj.z + w[23] * vj.w + w[24] * fj;
-      const float b1 = kk == 0 ? w[25] * eyj : kk == 1 ? bF : kk == 2 ? w[26] * epj : 0.f;
-      acc1 = mfma4(a1, b1, acc1);
+      const float lm = last ? 1.f : 0.f;  // Vep is read every stage (no load under a branch)
+      const float epi = lm * s.Vep[ci], epj = lm * s.Vep[cj];
+      const float fi = (ci == 2 * k) ? 1.f : 0.f, fj = (cj == 2 * k) ? 1.f : 0.f;
+      const float a0 = blend4(km, vi.x, vi.y, vi.z, vi.w);
+      const float b0 = wk0 * vj.x + wk1 * vj.y + wk2 * vj.z + wk3 * vj.w + wk4 * fj;
+      acc0[tt] = mfma4(a0, b0, acc0[tt]);
+      const float bF = wf0 * vj.x + wf1 * vj.y + wf2 * vj.z + wf3 * vj.w + wf4 * fj;
+      const float a1 = blend4(km, eyi, fi, epi, 0.f);
+      const float b1 = blend4(km, qey * eyj, bF, qep * epj, 0.f);
+      acc1[tt] = mfma4(a1, b1, acc1[tt]);
     }
-    const f4 acc = acc0 + acc1;
+  }
+#pragma unroll
+  for (int tt = 0; tt < 4; ++tt) {
+    const int I = TI[tt], J = TJ[tt];
+    if (I < 0) continue;
+    const f4 acc = acc0[tt] + acc1[tt];
 #pragma unroll
     for (int r = 0; r < 4; ++r) s.u.M[TS * I + 4 * kk + r][TS * J + i16] = acc[r];
+  }
+}
+
+// tile lists per wave: 71 / 72 / 72 / 64 contributing (tile, stage) pairs at N = 40
+template <int N>
+__device__ __forceinline__ void build_normal(DynSmem<N>& s, int wv, int lane) {
+  switch (wv) {
+    case 0: build_wave<N, 0, 0, 3, 0, 4, 0, 4, 1>(s, lane); break;
+    case 1: build_wave<N, 1, 0, 1, 1, 4, 2, -1, -1>(s, lane); break;
+    case 2: build_wave<N, 2, 0, 2, 1, 3, 1, 4, 3>(s, lane); break;
+    default: build_wave<N, 2, 2, 3, 2, 3, 3, 4, 4>(s, lane); break;
   }
 }
 
@@ -380,7 +409,7 @@ __device__ __forceinline__ void store_tile(DynSmem<N>& s, int R, int C, int lane
 // factor the diagonal tile (J,J) in one wave and overwrite it with Y_JJ = L_JJ^-T
 // (upper triangular, zeros below).  Returns false if a pivot is not positive/finite.
 template <int N>
-__device__ bool diag_block(DynSmem<N>& s, int J, int lane) {
+__device__ __forceinline__ bool diag_block(DynSmem<N>& s, int J, int lane) {
   constexpr int LDM = DD<N>::LDM;
   float* T0 = &s.u.M[TS * J][TS * J];
   const int j = lane & 15;
@@ -428,7 +457,7 @@ __device__ bool diag_block(DynSmem<N>& s, int J, int lane) {
 }
 
 template <int N>
-__device__ bool chol_inverse(DynSmem<N>& s, int wv, int lane, int t) {
+__device__ __forceinline__ bool chol_inverse(DynSmem<N>& s, int wv, int lane, int t) {
   constexpr int NT = DD<N>::NTL, LDM = DD<N>::LDM;
   if (t == 0) s.flag[0] = 1;
 #pragma unroll 1
@@ -482,16 +511,13 @@ __device__ bool chol_inverse(DynSmem<N>& s, int wv, int lane, int t) {
 
 // dz = Y (Y' rhs) with Y = L^-T in the upper triangle of M (rows split in thirds)
 template <int N>
-__device__ void solve(DynSmem<N>& s, const float* rhs, float* out, int t) {
+__device__ __forceinline__ void solve(DynSmem<N>& s, const float* rhs, float* out, int t) {
   constexpr int n = 2 * N, CH = (n + 2) / 3;
   if (t < 3 * n) {  // u_j = sum_{i <= j} Y[i][j] rhs_i
     const int j = t % n, gp = t / n;
     const int i0 = gp * CH, i1 = min(j + 1, min(n, i0 + CH));
     float a = 0.f;
-    for (int i = i0; i < i1; ++i) {
-      no_hoist();
-      a += s.u.M[i][j] * rhs[i];
-    }
+    for (int i = i0; i < i1; ++i) a += s.u.M[i][j] * rhs[i];
     s.part[0][gp][j] = a;
   }
   __syncthreads();
@@ -501,10 +527,7 @@ __device__ void solve(DynSmem<N>& s, const float* rhs, float* out, int t) {
     const int i = t % n, gp = t / n;
     const int j0 = max(i, gp * CH), j1 = min(n, gp * CH + CH);
     float a = 0.f;
-    for (int j = j0; j < j1; ++j) {
-      no_hoist();
-      a += s.u.M[i][j] * s.vt[j];
-    }
+    for (int j = j0; j < j1; ++j) a += s.u.M[i][j] * s.vt[j];
     s.part[1][gp][i] = a;
   }
   __syncthreads();
@@ -589,18 +612,42 @@ __device__ __forceinline__ void write_adj(DynSmem<N>& s, int slot, int k, int q,
   }
 }
 
+// Section timing (debug builds only, -DVC_TIMING, `make timing`): thread 0's s_memtime
+// stamps between barriers, accumulated per section and written to diag[b][4 + slot].
+enum { DT_PRED = 0, DT_LIN, DT_COND, DT_SETUP, DT_RESID, DT_BUILD, DT_CHOL, DT_PREDICTOR, DT_CORRECTOR,
+       DT_POLISH, DT_OUT, DT_TOTAL, DT_BW, DT_BMFMA, DT_BDIAG, DT_NSLOT };
+#ifdef VC_TIMING
+#define DT_STAMP(var)                               \
+  __builtin_amdgcn_sched_barrier(0);                \
+  const uint64_t var = __builtin_amdgcn_s_memtime(); \
+  __builtin_amdgcn_sched_barrier(0);
+#define DT_ACC(slot, t0)                                  \
+  {                                                       \
+    __builtin_amdgcn_sched_barrier(0);                    \
+    tacc[slot] += __builtin_amdgcn_s_memtime() - (t0);    \
+    __builtin_amdgcn_sched_barrier(0);                    \
+  }
+#else
+#define DT_STAMP(var)
+#define DT_ACC(slot, t0)
+#endif
+
 // ---- the fused kernel ---------------------------------------------------------------------
-template <int N>
+template <int N, int TYRE>
 __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
   constexpr int n = 2 * N;
   constexpr int NS = 4 * N;  // stage lanes
   __shared__ DynSmem<N> s;
   const int b = blockIdx.x;
-  const int t = threadIdx.x, lane = t & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform (scalar branches)
-  const int k = t >> 2, q = t & 3;  // stage lane role (t < NS)
+  // Thread coordinates are re-laundered (asm "+v") at the top of every solver loop so the
+  // hundreds of LDS addresses derived from them are recomputed per iteration instead of
+  // being hoisted out of the loops into live registers (which spilled to scratch).
+  int t = threadIdx.x, lane = t & 63;
+  int wv = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform (scalar branches)
+  int k = t >> 2, q = t & 3;  // stage lane role (t < NS)
   const bool stl = t < NS;
-  const DynCoef<float>& p = A.car;
+  DynCoef<float> p = A.car;
+  p.tyre = TYRE;  // compile-time tyre model: the other branch of the ODE is not generated
   const vc_dyn_mpc& W = A.w;
   const float S = float(W.fx_scale);
   const float prox2 = float(2.0 * A.qp.prox);
@@ -619,14 +666,23 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
   __syncthreads();
 
   int it_total = 0, it_max = 0, n_polished = 0;
+#ifdef VC_TIMING
+  uint64_t tacc[DT_NSLOT] = {};
+  const uint64_t t_start = __builtin_amdgcn_s_memtime();
+#endif
   bool all_conv = true, any_fail = false;
   float last_res = 0.f, last_mu = 0.f;
 
 #pragma unroll 1
   for (int sq = 0; sq < W.sqp_iters; ++sq) {
+    asm volatile("" : "+v"(t), "+v"(lane), "+v"(k), "+v"(q));
+    asm volatile("" : "+s"(wv));
     // ---------------- predict ----------------
+    DT_STAMP(t_p0)
     if (wv == 0) predict(s, p, lane);
     __syncthreads();
+    DT_ACC(DT_PRED, t_p0)
+    DT_STAMP(t_l0)
 
     // ---------------- linearize (waves 1-3) | stage terms (stage lanes of wave 0-2) ----------
     if (t >= 64 && t < 64 + 4 * (N - 1)) linearize(s, p, S, t - 64);
@@ -663,10 +719,14 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
       gr[r][4] = fgF[r];
     }
 
+    DT_ACC(DT_LIN, t_l0)
     // ---------------- condense ----------------
+    DT_STAMP(t_c0)
     float gt = 0.f;
     if (t < n) gt = condense(s, t);
     __syncthreads();
+    DT_ACC(DT_COND, t_c0)
+    DT_STAMP(t_s0)
 
     // ---------------- QP setup (branch-free in q: selects, not divergent ifs) ----------------
     StageRows R;
@@ -788,8 +848,9 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
       scale = 1.f + block_max(s, m, wv, lane, 0);
       mcount = fmaxf(block_sum(s, c, wv, lane, 4), 1.f);
     }
+    DT_ACC(DT_SETUP, t_s0)
     // Hessian direct part: prox, w_w, Fx slew (tridiagonal in the Fx columns)
-    const int kc = t >> 1;
+    int kc = t >> 1;
     const float slew_here = (t < n && (t & 1) == 0 && kc < N - 1) ? 2.f * float(W.w_Fx) / s.dsv[kc] * S * S : 0.f;
     const float slew_prev = (t < n && (t & 1) == 0 && kc >= 1) ? 2.f * float(W.w_Fx) / s.dsv[kc - 1] * S * S : 0.f;
     const float hdiag = prox2 + ((t & 1) ? 2.f * float(W.w_w) : slew_here + slew_prev);
@@ -797,6 +858,7 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
     // M = H + C' diag(w) C on the stage blocks (+ direct part), ready for chol_inverse.
     // w[3]: this stage lane's row weights (barrier weights, or rho on the polish's active set)
     auto assemble = [&](const float* w) {
+      DT_STAMP(t_a0)
       if (stl) {
         float w15[15], dw = 0.f;
 #pragma unroll
@@ -816,13 +878,15 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
 #pragma unroll
           for (int a = 0; a < 5; ++a)
 #pragma unroll
-            for (int c = 0; c < 5; ++c) s.W[k][5 * a + c] = w15[sym5(a, c)];
-          s.W[k][25] = qey;
-          s.W[k][26] = qep;
+            for (int c = 0; c < 5; ++c) s.W[k][WROW * a + c] = w15[sym5(a, c)];
+          s.W[k][30] = qey;
+          s.W[k][31] = qep;
           s.ddw[k] = dw;
         }
       }
       __syncthreads();
+      DT_ACC(DT_BW, t_a0)
+      DT_STAMP(t_a1)
       build_normal(s, wv, lane);
       for (int e = t; e < 10 * TS * TS; e += NTH) {  // upper tiles start at 0 (augmented rows)
         int rem = e >> 8, P = 0;
@@ -831,10 +895,12 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
         s.u.M[TS * P + ((e & 255) >> 4)][TS * K + (e & 15)] = 0.f;
       }
       __syncthreads();
+      DT_ACC(DT_BMFMA, t_a1)
+      DT_STAMP(t_a2)
       if (t < n) {
         float d = hdiag;
         if (t & 1) d += s.ddw[kc];
-        else if (kc == 0) d += s.W[0][24];
+        else if (kc == 0) d += s.W[0][WROW * 4 + 4];
         s.u.M[t][t] += d;
         if ((t & 1) == 0 && kc >= 1) {
           s.u.M[t][t - 2] -= slew_prev;
@@ -842,6 +908,7 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
         }
       }
       __syncthreads();
+      DT_ACC(DT_BDIAG, t_a2)
     };
 
     // ---------------- interior point (Mehrotra predictor-corrector) ----------------
@@ -851,7 +918,11 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
 #pragma unroll 1
     for (; it < A.qp.max_iter; ++it) {
       no_hoist();
+      asm volatile("" : "+v"(t), "+v"(lane), "+v"(k), "+v"(q), "+v"(kc));
+      asm volatile("" : "+s"(wv));
+
       // (a) residuals at z: rp = C z + s - d (stage lanes), rd = H z + g + C' lam (columns)
+      DT_STAMP(t_r0)
       fwd_pass(s, s.vz, t);
       __syncthreads();
       float rp[3], wg[3];
@@ -907,11 +978,15 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
       const float rdm = block_max(s, rdmax, wv, lane, 8);
       last_res = fmaxf(rdm, rpm) / scale;
       last_mu = mu / scale;
+      DT_ACC(DT_RESID, t_r0)
       if (!(rdm == rdm) || !(rpm == rpm) || !(mu == mu) || rdm > 3.0e38f) { fail = true; break; }
       if (rdm <= tol * scale && rpm <= tol * scale && mu <= tol * scale) { conv = true; break; }
 
       // (b) normal matrix M = sum_k V_k' W_k V_k + D, blocked Cholesky, Y = L^-T
+      DT_STAMP(t_b0)
       assemble(wg);
+      DT_ACC(DT_BUILD, t_b0)
+      DT_STAMP(t_ch0)
       const bool dump = A.dbg && sq == 0 && it == 0;
       if (dump)
         for (int e = t; e < n * n; e += NTH) A.dbg[(size_t)b * DBG_STRIDE + DBG_M + e] = s.u.M[e / n][e % n];
@@ -921,7 +996,9 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
         if (t < n) A.dbg[(size_t)b * DBG_STRIDE + DBG_RHS + t] = s.vr[t];
       }
 
+      DT_ACC(DT_CHOL, t_ch0)
       // (c) predictor (affine-scaling) direction
+      DT_STAMP(t_pr0)
       solve(s, s.vr, s.vd, t);
       if (dump && t < n) A.dbg[(size_t)b * DBG_STRIDE + DBG_DZ + t] = s.vd[t];
       fwd_pass(s, s.vd, t);
@@ -968,7 +1045,9 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
       }
       __syncthreads();
 
+      DT_ACC(DT_PREDICTOR, t_pr0)
       // (d) corrector direction, step to the boundary, update
+      DT_STAMP(t_co0)
       solve(s, s.vr, s.vd, t);
       fwd_pass(s, s.vd, t);
       __syncthreads();
@@ -997,6 +1076,7 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
       }
       if (t < n) s.vz[t] += alpha * s.vd[t];
       __syncthreads();
+      DT_ACC(DT_CORRECTOR, t_co0)
     }
     it_total += it;
     it_max = max(it_max, it);
@@ -1011,6 +1091,7 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
     // negative multiplier for the next round (the oracle changes one row per round);
     // after A.qp.polish rounds without a certificate the interior-point iterate is kept.
     bool polished = false;
+    DT_STAMP(t_po0)
     if (!fail && A.qp.polish > 0) {
       const float rho = 1.0e4f;  // AL converges in ~4 passes; H + rho C_A'C_A stays ~1e5-conditioned
       // tolerances on the O(1) rows (scaled units), not on the gradient-inflated `scale`
@@ -1033,6 +1114,9 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
       }
 #pragma unroll 1
       for (int round = 0; round < A.qp.polish; ++round) {
+        asm volatile("" : "+v"(t), "+v"(lane), "+v"(k), "+v"(q), "+v"(kc));
+        asm volatile("" : "+s"(wv));
+
         float w3[3];
 #pragma unroll
         for (int i = 0; i < 3; ++i) w3[i] = stl ? rho * act[i] : 0.f;
@@ -1095,6 +1179,7 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
       if (!polished && t < n) s.vz[t] = s.vp[t];
       __syncthreads();
     }
+    DT_ACC(DT_POLISH, t_po0)
     all_conv = all_conv && (conv || polished);
     any_fail = any_fail || fail;
     n_polished += polished ? 1 : 0;
@@ -1105,8 +1190,10 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
   }
 
   // ---------------- outputs: u*, x* = rollout(u*), u0, status ----------------
+  DT_STAMP(t_o0)
   if (wv == 0) predict(s, p, lane);
   __syncthreads();
+  DT_ACC(DT_OUT, t_o0)
   bool finite = true;
   if (t < n) {
     const float v = s.ub[t >> 1][t & 1];
@@ -1128,11 +1215,18 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
     A.status[b] = st;
     A.iters[b] = it_total;
     if (A.diag) {
-      A.diag[(size_t)b * 4 + 0] = last_res;
-      A.diag[(size_t)b * 4 + 1] = last_mu;
-      A.diag[(size_t)b * 4 + 2] =
+#ifdef VC_TIMING
+      constexpr size_t DS = 4 + DT_NSLOT;
+      tacc[DT_TOTAL] = __builtin_amdgcn_s_memtime() - t_start;
+      for (int i = 0; i < DT_NSLOT; ++i) A.diag[(size_t)b * DS + 4 + i] = float(tacc[i]);
+#else
+      constexpr size_t DS = 4;
+#endif
+      A.diag[(size_t)b * DS + 0] = last_res;
+      A.diag[(size_t)b * DS + 1] = last_mu;
+      A.diag[(size_t)b * DS + 2] =
           float((any_fail ? 1 : 0) | (all_conv ? 2 : 0) | (n_polished == W.sqp_iters ? 4 : 0) | (n_polished << 4));
-      A.diag[(size_t)b * 4 + 3] = float(it_max);
+      A.diag[(size_t)b * DS + 3] = float(it_max);
     }
   }
 }
@@ -1153,7 +1247,10 @@ hipError_t launch_dyn_sqp(const DynSqpArgs& a, int N, hipStream_t stream) {
   if (a.B <= 0) return hipSuccess;
   switch (N) {
     case 40:
-      hipLaunchKernelGGL(dyn_sqp_kernel<40>, dim3(a.B), dim3(NTH), 0, stream, a);
+      if (a.car.tyre == VC_TYRE_LINEAR)
+        hipLaunchKernelGGL((dyn_sqp_kernel<40, VC_TYRE_LINEAR>), dim3(a.B), dim3(NTH), 0, stream, a);
+      else
+        hipLaunchKernelGGL((dyn_sqp_kernel<40, VC_TYRE_FIALA>), dim3(a.B), dim3(NTH), 0, stream, a);
       return hipGetLastError();
     default:
       return hipErrorInvalidValue;

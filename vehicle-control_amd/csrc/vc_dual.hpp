@@ -10,16 +10,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
-namespace vc {
+#include "vc_models.hpp"
 
-// keep the scalar overloads visible next to the Dual ones (unqualified calls inside vc)
-using ::atan;
-using ::cos;
-using ::fabs;
-using ::sin;
-using ::sqrt;
-using ::tan;
-using ::tanh;
+namespace vc {
 
 template <int K>
 struct Dual {
@@ -102,27 +95,27 @@ template <int K>
 __device__ __forceinline__ bool operator<=(const Dual<K>& a, const Dual<K>& b) { return a.v <= b.v; }
 
 template <int K>
-__device__ __forceinline__ Dual<K> sin(const Dual<K>& a) { return dmap(a, sinf(a.v), cosf(a.v)); }
+__device__ __forceinline__ Dual<K> vsin(const Dual<K>& a) { return dmap(a, vsin(a.v), vcos(a.v)); }
 template <int K>
-__device__ __forceinline__ Dual<K> cos(const Dual<K>& a) { return dmap(a, cosf(a.v), -sinf(a.v)); }
+__device__ __forceinline__ Dual<K> vcos(const Dual<K>& a) { return dmap(a, vcos(a.v), -vsin(a.v)); }
 template <int K>
-__device__ __forceinline__ Dual<K> tan(const Dual<K>& a) {
-  const float t = tanf(a.v);
+__device__ __forceinline__ Dual<K> vtan(const Dual<K>& a) {
+  const float t = vtan(a.v);
   return dmap(a, t, 1.0f + t * t);
 }
 template <int K>
-__device__ __forceinline__ Dual<K> atan(const Dual<K>& a) { return dmap(a, atanf(a.v), 1.0f / (1.0f + a.v * a.v)); }
+__device__ __forceinline__ Dual<K> vatan(const Dual<K>& a) { return dmap(a, vatan(a.v), 1.0f / (1.0f + a.v * a.v)); }
 template <int K>
-__device__ __forceinline__ Dual<K> tanh(const Dual<K>& a) {
-  const float t = tanhf(a.v);
+__device__ __forceinline__ Dual<K> vtanh(const Dual<K>& a) {
+  const float t = vtanh(a.v);
   return dmap(a, t, 1.0f - t * t);
 }
 template <int K>
-__device__ __forceinline__ Dual<K> sqrt(const Dual<K>& a) {
-  const float s = sqrtf(a.v);
-  return dmap(a, s, 0.5f / s);
+__device__ __forceinline__ Dual<K> vsqrt(const Dual<K>& a) {
+  const float r = vsqrt(a.v);
+  return dmap(a, r, 0.5f / r);
 }
 template <int K>
-__device__ __forceinline__ Dual<K> fabs(const Dual<K>& a) { return a.v < 0.f ? -a : a; }
+__device__ __forceinline__ Dual<K> vfabs(const Dual<K>& a) { return a.v < 0.f ? -a : a; }
 
 }  // namespace vc

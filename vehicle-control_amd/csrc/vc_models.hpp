@@ -9,6 +9,33 @@
 
 namespace vc {
 
+// Transcendental entry points of the models.  double: libm precision (the fp64 paths
+// are pinned to the reference traces at 1e-12).  float on the device: gfx950's native
+// forms (v_sin_f32 / v_cos_f32 / v_exp_f32 based, ~1e-6 absolute error on the
+// angles and forces here) -- the fp32 SQP path is compared with the fp64 oracle at a
+// scaled 1e-4 and its rollouts were a quarter of its time with the libm versions.
+__host__ __device__ inline double vsin(double x) { return sin(x); }
+__host__ __device__ inline double vcos(double x) { return cos(x); }
+__host__ __device__ inline double vtan(double x) { return tan(x); }
+__host__ __device__ inline double vatan(double x) { return atan(x); }
+__host__ __device__ inline double vtanh(double x) { return tanh(x); }
+__host__ __device__ inline double vsqrt(double x) { return sqrt(x); }
+__host__ __device__ inline double vfabs(double x) { return fabs(x); }
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ inline float vsin(float x) { return __sinf(x); }
+__device__ inline float vcos(float x) { return __cosf(x); }
+__device__ inline float vtan(float x) { return __sinf(x) / __cosf(x); }
+__device__ inline float vtanh(float x) { return 1.0f - 2.0f / (1.0f + __expf(2.0f * x)); }
+#else
+inline float vsin(float x) { return sinf(x); }
+inline float vcos(float x) { return cosf(x); }
+inline float vtan(float x) { return tanf(x); }
+inline float vtanh(float x) { return tanhf(x); }
+#endif
+__host__ __device__ inline float vatan(float x) { return atanf(x); }
+__host__ __device__ inline float vsqrt(float x) { return sqrtf(x); }
+__host__ __device__ inline float vfabs(float x) { return fabsf(x); }
+
 constexpr int KIN_NX = 6, KIN_NU = 2;
 constexpr int DYN_NX = 8, DYN_NU = 2;
 constexpr double GRAVITY = 9.88;  // models/dynamic_car.py:61
@@ -118,10 +145,10 @@ __host__ __device__ inline DynCoef<R> make_dyn_coef(const vc_dyn_car& p) {
 // Modified Fiala / brush tyre -- models/dynamic_car.py:119-142.
 template <typename T>
 __host__ __device__ inline T fiala_fy(T alpha, T Ca, T Fymax, T eps) {
-  const T ta = tan(alpha);
-  const T alphamod = atan((T(3) * Fymax * eps) / Ca);
-  if (fabs(alpha) <= alphamod) {
-    return -Ca * ta + Ca * Ca * fabs(ta) * ta / (T(3) * Fymax) -
+  const T ta = vtan(alpha);
+  const T alphamod = vatan((T(3) * Fymax * eps) / Ca);
+  if (vfabs(alpha) <= alphamod) {
+    return -Ca * ta + Ca * Ca * vfabs(ta) * ta / (T(3) * Fymax) -
            (Ca * Ca * Ca * ta * ta * ta) / (T(27) * Fymax * Fymax);
   }
   const T sgn = alpha > T(0) ? T(1) : (alpha < T(0) ? T(-1) : T(0));
@@ -134,24 +161,24 @@ struct DynForces {
   T Fx_f, Fx_r, Fz_f, Fz_r, alpha_f, alpha_r;
   __host__ __device__ DynForces(T Ux, T Uy, T r, T delta, T Fx, const DynCoef<R>& c) {
     // drive/brake split (dynamic_car.py:78-86)
-    const T Xf = T(c.xf_a) * tanh(T(2) * (Fx / T(1000) + T(0.5))) + T(c.xf_b);
+    const T Xf = T(c.xf_a) * vtanh(T(2) * (Fx / T(1000) + T(0.5))) + T(c.xf_b);
     Fx_f = Fx * Xf;
-    const T Xr = T(c.xr_a) * tanh(T(-2) * (Fx / T(1000) + T(0.5))) + T(c.xr_b);
+    const T Xr = T(c.xr_a) * vtanh(T(-2) * (Fx / T(1000) + T(0.5))) + T(c.xr_b);
     Fx_r = Fx * Xr;
     // loads (dynamic_car.py:98-102); l = car.l
     const T gz = T(c.gz0) + T(c.Av2) * (Ux * Ux);
     Fz_f = T(c.fzf_m) * gz - T(c.h) * Fx / T(c.l);
     Fz_r = T(c.fzr_m) * gz + T(c.h) * Fx / T(c.l);
     // slip angles (dynamic_car.py:111-115)
-    alpha_f = atan((Uy + T(c.a) * r) / Ux) - delta;
-    alpha_r = atan((Uy - T(c.b) * r) / Ux);
+    alpha_f = vatan((Uy + T(c.a) * r) / Ux) - delta;
+    alpha_r = vatan((Uy - T(c.b) * r) / Ux);
   }
   // friction-ellipse lateral capacity (dynamic_car.py:107-108)
   __host__ __device__ T fymax_f(const DynCoef<R>& c) const {
-    return sqrt((T(c.muf) * Fz_f) * (T(c.muf) * Fz_f) - (T(0.99) * Fx_f) * (T(0.99) * Fx_f));
+    return vsqrt((T(c.muf) * Fz_f) * (T(c.muf) * Fz_f) - (T(0.99) * Fx_f) * (T(0.99) * Fx_f));
   }
   __host__ __device__ T fymax_r(const DynCoef<R>& c) const {
-    return sqrt((T(c.mur) * Fz_r) * (T(c.mur) * Fz_r) - (T(0.99) * Fx_r) * (T(0.99) * Fx_r));
+    return vsqrt((T(c.mur) * Fz_r) * (T(c.mur) * Fz_r) - (T(0.99) * Fx_r) * (T(0.99) * Fx_r));
   }
 };
 
@@ -164,22 +191,22 @@ __host__ __device__ inline void dyn_temporal_ode(const T* x, const T* u, T kappa
   const DynForces<T, R> F(Ux, Uy, r, delta, Fx, c);
   T Fy_f, Fy_r;
   if (c.tyre == VC_TYRE_LINEAR) {
-    Fy_f = -T(c.Caf) * tan(F.alpha_f);
-    Fy_r = -T(c.Car) * tan(F.alpha_r);
+    Fy_f = -T(c.Caf) * vtan(F.alpha_f);
+    Fy_r = -T(c.Car) * vtan(F.alpha_r);
   } else {
     Fy_f = fiala_fy(F.alpha_f, T(c.Caf), F.fymax_f(c), T(c.eps));
     Fy_r = fiala_fy(F.alpha_r, T(c.Car), F.fymax_r(c), T(c.eps));
   }
   const T Fd = T(c.Frr) + T(c.Cd) * (Ux * Ux);
-  const T cd = cos(delta), sd = sin(delta);
+  const T cd = vcos(delta), sd = vsin(delta);
   const T m = T(c.m);
   f[0] = (F.Fx_f * cd - Fy_f * sd + F.Fx_r - Fd) / m + r * Uy;
   f[1] = (Fy_f * cd + F.Fx_f * sd + Fy_r) / m - r * Ux;
   f[2] = (T(c.a) * (Fy_f * cd + F.Fx_f * sd) - T(c.b) * Fy_r) / T(c.Izz);
   f[3] = w;
-  const T s_dot = (Ux * cos(epsi) - Uy * sin(epsi)) / (T(1) - kappa * ey);
+  const T s_dot = (Ux * vcos(epsi) - Uy * vsin(epsi)) / (T(1) - kappa * ey);
   f[4] = s_dot;
-  f[5] = Ux * sin(epsi) + Uy * cos(epsi);
+  f[5] = Ux * vsin(epsi) + Uy * vcos(epsi);
   f[6] = r - kappa * s_dot;
   f[7] = T(1);
 }
@@ -196,24 +223,24 @@ __host__ __device__ inline void dyn_spatial_ode(const T* x, const T* u, T kappa,
 }
 
 // Per-stage nonlinear terms of the single-track NLP at (Ux, Uy, r, delta, Fx):
-//   out[0] slip_f = |tan alpha_f| - tan(alphamod_f)   (slip cost, cascaded_mpc.py:155-159)
+//   out[0] slip_f = |tan alpha_f| - vtan(alphamod_f)   (slip cost, cascaded_mpc.py:155-159)
 //   out[1] slip_r                                     (cascaded_mpc.py:161-165)
 //   out[2] peng   = Fx - Peng / Ux  <= 0              (power limit, cascaded_mpc.py:110)
-//   out[3] Fx_f - mu_f Fz_f cos(alpha_f) <= 0,  out[4] -Fx_f - mu_f Fz_f cos(alpha_f) <= 0
-//   out[5] Fx_r - mu_r Fz_r cos(alpha_r) <= 0,  out[6] -Fx_r - mu_r Fz_r cos(alpha_r) <= 0
+//   out[3] Fx_f - mu_f Fz_f vcos(alpha_f) <= 0,  out[4] -Fx_f - mu_f Fz_f vcos(alpha_f) <= 0
+//   out[5] Fx_r - mu_r Fz_r vcos(alpha_r) <= 0,  out[6] -Fx_r - mu_r Fz_r vcos(alpha_r) <= 0
 //                                                     (tyre force bounds, cascaded_mpc.py:124-128)
 // with Fz, Fymax, alpha, alphamod as in dynamic_car.py:78-132.
 template <typename T, typename R>
 __host__ __device__ inline void dyn_stage_terms(const T* X5, const DynCoef<R>& c, T* out) {
   const T Ux = X5[0], Fx = X5[4];
   const DynForces<T, R> F(Ux, X5[1], X5[2], X5[3], Fx, c);
-  const T amod_f = atan((T(3) * F.fymax_f(c) * T(c.eps)) / T(c.Caf));
-  const T amod_r = atan((T(3) * F.fymax_r(c) * T(c.eps)) / T(c.Car));
-  out[0] = fabs(tan(F.alpha_f)) - tan(amod_f);
-  out[1] = fabs(tan(F.alpha_r)) - tan(amod_r);
+  const T amod_f = vatan((T(3) * F.fymax_f(c) * T(c.eps)) / T(c.Caf));
+  const T amod_r = vatan((T(3) * F.fymax_r(c) * T(c.eps)) / T(c.Car));
+  out[0] = vfabs(vtan(F.alpha_f)) - vtan(amod_f);
+  out[1] = vfabs(vtan(F.alpha_r)) - vtan(amod_r);
   out[2] = Fx - T(c.Peng) / Ux;
-  const T bound_f = T(c.muf) * F.Fz_f * cos(F.alpha_f);
-  const T bound_r = T(c.mur) * F.Fz_r * cos(F.alpha_r);
+  const T bound_f = T(c.muf) * F.Fz_f * vcos(F.alpha_f);
+  const T bound_r = T(c.mur) * F.Fz_r * vcos(F.alpha_r);
   out[3] = F.Fx_f - bound_f;
   out[4] = -F.Fx_f - bound_f;
   out[5] = F.Fx_r - bound_r;

@@ -16,9 +16,11 @@
 
 
 #ifdef VC_TIMING
-#define VC_DIAG_COLS 13  // 4 diagnostics + 9 section-cycle counters (kin_ltv.hip T_*)
+#define VC_DIAG_COLS 13      // 4 diagnostics + 9 section-cycle counters (kin_ltv.hip T_*)
+#define VC_DYN_DIAG_COLS 19  // 4 diagnostics + 15 section-cycle counters (dyn_sqp.hip DT_*)
 #else
 #define VC_DIAG_COLS 4
+#define VC_DYN_DIAG_COLS 4
 #endif
 
 struct vc_ctx {
@@ -143,7 +145,7 @@ int dyn_solve(vc_ctx* c, int B, const void* x0, const void* kappa, const void* d
              {nullptr, u0, (size_t)B * nu * 4, nullptr},
              {nullptr, status, (size_t)B * 4, nullptr},
              {nullptr, iters, (size_t)B * 4, nullptr},
-             {nullptr, diag, diag ? (size_t)B * 4 * 4 : 0, nullptr},
+             {nullptr, diag, diag ? (size_t)B * VC_DYN_DIAG_COLS * 4 : 0, nullptr},
              {nullptr, dbg, dbg ? (size_t)B * vc::dyn_sqp_debug_stride() * 4 : 0, nullptr}};
     if (int r = stage(c, slots)) return r;
     a.dbg = dbg ? (float*)slots[9].dev : nullptr;
