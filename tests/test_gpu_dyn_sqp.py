@@ -181,3 +181,28 @@ def test_unsupported_dynamic_combination():
         with pytest.raises(_abi.VcError) as e:
             c.solve(np.zeros((1, 8)), np.zeros((1, N)), np.zeros((1, N)), np.zeros((1, N, 2)))
         assert e.value.code == _abi.VC_E_UNSUPPORTED
+
+
+@pytest.mark.parametrize("tyre", ["linear", "fiala"])
+def test_cascaded_mpc_drop_in_closed_loop(tyre):
+    """CascadedMPC(car, point_mass, config).command(state) -> action, then car.drive (the
+    reference's fp64 RK4 plant): the RacingSimulator step (racing.py:416-423) on a
+    constant-curvature track, single-track mode."""
+    from vcmpc.config import load_config
+    from vcmpc.controllers import CascadedMPC
+    from vcmpc.environment import CurvatureTrack
+    from vcmpc.models import DynamicCar
+    np.random.seed(31)
+    car = DynamicCar(load_config("dynamic_car"), CurvatureTrack(constant=1 / 60), tyre=tyre)
+    car.state = car.create_state(Ux=12.0, s=1.0, ey=0.5)
+    mpc = CascadedMPC(car, None, load_config("dynamic_mpc"))
+    solved = 0
+    for _ in range(60):
+        a = mpc.command(car.state)
+        solved += int(mpc.status[0] == 0)
+        assert -0.4 - 1e-4 <= a.w <= 0.4 + 1e-4 and np.isfinite(a.Fx)
+        car.drive(a)
+    assert mpc.state_prediction.shape == (8, N) and mpc.action_prediction.shape == (2, N)
+    assert solved >= 58, solved
+    s = car.state
+    assert np.isfinite(s.values).all() and abs(s.ey) < 3.0 and s.Ux > 5.0 and s.s > 1.0 + 60 * 0.05 * 5.0
