@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Benchmark: batched kinematic LTV-MPC solves/s on MI355X (BASELINE.json metric).
+"""Benchmark: batched MPC solves/s on MI355X (BASELINE.json metric).
 
 One step = one fused predict -> linearize -> condense -> interior-point solve of
 every problem of this rank's batch (vc_solve, csrc/kin_ltv.hip), inputs resident
@@ -7,7 +7,13 @@ in HBM.  Default workload: BASELINE config 2 -- B = 1024 kinematic-bicycle
 problems, N = 20, fp64, per GPU.  With --gpus N under torchrun each rank solves
 its own batch (weak scaling, no data-path collective); rank 0 prints one JSON line.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-cpu-baseline]
+The same line carries, under "c3", BASELINE config 3 -- B = 4096 dynamic-bicycle
+(linear tyre) single-track NMPC problems per GPU, N = 40, fp32, 3 SQP iterations
+(vc_solve on a dynamic context, csrc/dyn_sqp.hip) -- measured the same way; it is a
+secondary workload, not `value`.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--c3-batch B3]
+                    [--no-c3] [--no-cpu-baseline]
 """
 from __future__ import annotations
 
@@ -42,6 +48,30 @@ FLOP_ITER = (2 * N_DEC * sum(2 * (1 + r % (N_HORIZON - 1)) for r in range(NC_ROW
 FP64_VALU_PEAK = 78.6  # TFLOP/s
 PMC_PROFILE = os.path.join(ROOT, "profiles", "r01", "pmc_b1024.json")
 
+# ---- C3: dynamic single-track SQP (fp32, N = 40) ------------------------------------
+C3_N, C3_NX = 40, 8
+FP32_PEAK_TFS = 157.3          # MI355X FP32 vector = FP32 MFMA (MI355X_MICROARCH.md)
+# compulsory bytes: in x0 + kappa + ds + ubar, out u* + x* (N columns) + u0 (fp32) + status + iters
+C3_BYTES_PER_SOLVE = (C3_NX + 2 * C3_N + 2 * C3_N) * 4 + (2 * C3_N + C3_N * C3_NX + 2) * 4 + 8
+C3_n = 2 * C3_N
+# Algorithmic fp32 FLOPs: per interior-point iteration the normal-matrix
+# build sum_k V_k' W_k V_k over the triangular stage blocks (7 basis rows, columns < 2k),
+# the blocked Cholesky with the augmented inverse (~ n^3), two explicit-inverse solves
+# (2 x 2 n^2) and the forward/adjoint G passes (3 + 3 x 2 x 5 x sum_k 2k); per SQP
+# iteration the rollout + dual-number Jacobians (~ 40 RK4 evaluations x 9 directions x
+# ~300 flops) and the condensing (80 columns x 39 stages x 7 x 7 x 2).
+C3_G_NNZ = sum(2 * k for k in range(1, C3_N))                      # nonzeros of one G row set
+C3_FLOP_ITER = (sum(2 * (2 * k) * 7 * 7 + (2 * k) ** 2 * 7 for k in range(1, C3_N))  # build: W V, then V'(W V) half
+                + C3_n ** 3 + 2 * 2 * 2 * C3_n * C3_n                         # factor + 2 solves
+                + 6 * 2 * 5 * C3_G_NNZ)                                       # G passes
+C3_FLOP_SQP = 4 * (C3_N - 1) * 9 * 300 + C3_n * (C3_N - 1) * 7 * 7 * 2
+
+
+def c3_flops(pdip_iters_total, sqp_iters=3, polish_rounds=2):
+    """fp32 FLOPs of one C3 solve given its total interior-point iterations."""
+    return (sqp_iters * C3_FLOP_SQP + (pdip_iters_total + sqp_iters * polish_rounds) * C3_FLOP_ITER
+            + C3_N * 4 * 300)
+
 
 def pmc_traffic(batch):
     """HBM bytes per launch from the committed rocprofv3 PMC passes (FETCH_SIZE +
@@ -65,6 +95,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=31)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1024, help="problems in the CPU-baseline sample")
+    ap.add_argument("--c3-batch", type=int, default=4096, help="C3 problems per GPU (config 3: 4096)")
+    ap.add_argument("--no-c3", action="store_true", help="skip the secondary C3 measurement")
     return ap.parse_args()
 
 
@@ -93,6 +125,88 @@ def cpu_baseline(batch, sample):
     return {"value": len(d["x0"]) / dt, "unit": "solves/s", "cores": 1, "kind": "port",
             "sample": f"{len(d['x0'])} problems of the C2 workload, one oracle pass (PDIP + active-set polish, "
                       f"numpy fp64, 1 thread) in {dt:.2f} s on {cpu}"}
+
+
+def cpu_baseline_c3(data, sample):
+    """The fp64 numpy oracle of the SQP contract (oracle/dyn_sqp.py, 3 exact QPs per
+    solve), one host thread, on the first `sample` problems of the C3 workload."""
+    from threadpoolctl import threadpool_limits
+
+    from oracle import dyn_sqp as D
+    from oracle import models as M
+    from vcmpc.config import load_config
+    W = D.dyn_weights(load_config("dynamic_mpc"))
+    p = M.dyn_params_from_config(load_config("dynamic_car"))
+    d = {k: v[:sample].astype("float64") for k, v in data.items()}
+    with threadpool_limits(limits=1):
+        t0 = time.perf_counter()
+        D.dyn_sqp_solve(d["x0"], d["ubar"], d["kappa"], d["ds"], p, W, "linear")
+        dt = time.perf_counter() - t0
+    return {"value": len(d["x0"]) / dt, "unit": "solves/s", "cores": 1, "kind": "port",
+            "sample": f"{len(d['x0'])} problems of the C3 workload, one oracle pass (3 SQP iterations of "
+                      f"complex-step linearisation + exact QP, numpy fp64, 1 thread) in {dt:.2f} s"}
+
+
+def run_c3(args, dev, stream, rank, dist, steps):
+    """Secondary measurement: BASELINE config 3 on this rank (weak scaling)."""
+    import numpy as np
+    import torch
+
+    from vcmpc import Context, _abi
+    from vcmpc.config import load_config, make_params
+    from vcmpc.workload import dynamic_batch
+
+    B = args.c3_batch
+    data = dynamic_batch(B, N=C3_N, seed=args.seed + 104729 * rank)
+    t = {k: torch.from_numpy(v).to(dev) for k, v in data.items()}
+    ubar0 = t["ubar"].clone()
+    params = make_params(dyn_car=load_config("dynamic_car"), dyn_mpc=load_config("dynamic_mpc"), tyre="linear")
+    ctx = Context(model=_abi.VC_MODEL_DYNAMIC, N=C3_N, max_batch=B, dtype=_abi.VC_F32, device=dev.index,
+                  params=params)
+    ctx.set_stream(stream.cuda_stream)
+    xbar = torch.empty((B, C3_N, C3_NX), dtype=torch.float32, device=dev)
+    u0 = torch.empty((B, 2), dtype=torch.float32, device=dev)
+    status = torch.empty((B,), dtype=torch.int32, device=dev)
+    iters = torch.empty((B,), dtype=torch.int32, device=dev)
+
+    def step(ev=None):
+        t["ubar"].copy_(ubar0)
+        if ev is not None:
+            ev[0].record(stream)
+        ctx.solve(t["x0"], t["kappa"], t["ds"], t["ubar"], xbar, u0, status, iters)
+        if ev is not None:
+            ev[1].record(stream)
+
+    step()
+    torch.cuda.synchronize(dev)
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(events[i])
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    st, it = status.cpu().numpy(), iters.cpu().numpy()
+    solves, elapsed_max, kern_ms_max = dist.aggregate(float(B * steps), elapsed, kern_ms, dev)
+    ctx.close()
+    flops = c3_flops(float(it.mean()))
+    out = {"metric": "MPC solves/sec (batched, N=40, 3 SQP iterations)", "value": solves / elapsed_max,
+           "unit": "solves/s", "steps": steps, "ms_per_step": elapsed_max / steps * 1e3, "dtype": "f32",
+           "config": {"workload": f"C3 dynamic-bicycle (linear tyre) single-track NMPC via SQP, B={B} per GPU, "
+                                  f"N={C3_N}, fp32", "batch_per_gpu": B, "horizon": C3_N},
+           "roofline": {"bound": "mfma", "kernel": "dyn_sqp_kernel<40, linear>", "kernel_ms": kern_ms,
+                        "flops_per_solve": flops, "achieved": flops * B / (kern_ms / 1e3) / 1e12,
+                        "peak": FP32_PEAK_TFS, "unit": "TFLOP/s",
+                        "frac": flops * B / (kern_ms / 1e3) / 1e12 / FP32_PEAK_TFS,
+                        "hbm": {"bytes_per_solve": C3_BYTES_PER_SOLVE,
+                                "achieved": C3_BYTES_PER_SOLVE * B / (kern_ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
+                                "unit": "GB/s"}},
+           "solver": {"solved_frac": float((st == 0).mean()), "pdip_iters_mean": float(it.mean()),
+                      "pdip_iters_max": int(it.max())}}
+    return out, data
 
 
 def main():
@@ -160,6 +274,12 @@ def main():
         ctx.solve(host["x0"], host["kappa"], host["ds"], host["ubar"].copy())
     host_rate = B * reps / (time.perf_counter() - th)
     solves, elapsed_max, kern_ms_max = dist.aggregate(float(B * args.steps), elapsed, kern_ms, dev)
+    c3 = c3_data = None
+    if not args.no_c3:
+        try:
+            c3, c3_data = run_c3(args, dev, stream, rank, dist, max(3, args.steps // 4))
+        except Exception as e:  # the headline line must still print
+            c3 = {"error": f"{type(e).__name__}: {e}"}
 
     if rank == 0:
         value = solves / elapsed_max
@@ -196,6 +316,10 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(data, min(args.cpu_sample, B))
+            if c3_data is not None and "error" not in c3:
+                c3["cpu_baseline"] = cpu_baseline_c3(c3_data, 8)
+        if c3 is not None:
+            out["c3"] = c3
         print(json.dumps(out), flush=True)
     ctx.close()
     dist.shutdown()
