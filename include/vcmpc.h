@@ -19,6 +19,13 @@
  *   vc_plant_step    RacingCar.drive / Robot.transition  vehicle_control/models/racing_car.py:34-46,
  *                    kinematic_car.py:34-45,66-68 (Euler), dynamic_car.py:144-167,193-195 (RK4)
  *   vc_spatial_step  <Model>.spatial_transition       kinematic_car.py:70-72, dynamic_car.py:169-199
+ *   vc_track_set     Track._precompute_curvatures     environment/track.py:156-167 (the bspline k(s) table)
+ *   vc_track_k       Track.k                          track.py:162-166
+ *   vc_horizon       KinematicMPC._init_horizon       kinematic_mpc.py:170-187
+ *                    CascadedMPC._init_horizon        cascaded_mpc.py:316-330 (horizon_pm = 0)
+ *   vc_drive         RacingCar.drive                  models/racing_car.py:34-46 (k = track.k(s), fp64 plant)
+ *   vc_simulate      RacingSimulator.update / step    simulation/racing.py:217-242,416-423 (command ->
+ *                                                     drive -> log, every vehicle, `steps` times)
  *
  * Conventions
  *   - All arrays are C-contiguous, batch-outermost ("AoS"):
@@ -49,7 +56,7 @@
 extern "C" {
 #endif
 
-#define VCMPC_ABI_VERSION 2
+#define VCMPC_ABI_VERSION 3
 
 typedef struct vc_ctx vc_ctx;
 
@@ -187,6 +194,51 @@ int vc_plant_step(vc_ctx* ctx, int B, const void* x, const void* u, const void* 
 /* Spatial step x_next = spatial_transition(x, u, kappa, ds): ds[B]. */
 int vc_spatial_step(vc_ctx* ctx, int B, const void* x, const void* u, const void* kappa,
                     const void* ds, void* x_next, int flags);
+
+/* ---- Track curvature and the batched closed loop ---------------
+ *
+ * The curvature k(s) is a piecewise cubic on a uniform grid, uploaded once per context:
+ *   k(s) = c0 + c1 t + c2 t^2 + c3 t^3,  i = clamp(floor(s' / h), 0, n_pieces - 1),
+ *   t = s' - i h,  coef[i] = (c0, c1, c2, c3),  s' = fmod(s, length)
+ * i.e. the not-a-knot cubic through the curvature samples every h = 0.05 m of
+ * track.py:156-167 (the CasADi bspline), extrapolating its last piece up to `length`.
+ * Evaluated in fp64 on the device whatever the context dtype.  Deviation: the
+ * reference's k does not wrap s (its simulator stops after one lap, racing.py:219);
+ * the table is lap-periodic like get_curvature (track.py:111).
+ * coef is host memory [n_pieces][4]; the call copies it and synchronises. */
+int vc_track_set(vc_ctx* ctx, int n_pieces, double h, double length, const double* coef);
+
+/* k[b] = k(s[b]) for B points (context dtype). */
+int vc_track_k(vc_ctx* ctx, int B, const void* s, void* k, int flags);
+
+/* Horizon parameters from the unshifted warm start (context dtype):
+ *   kinematic (kinematic_mpc.py:178-187), xbar[B][N+1][6]:
+ *     d_j = mpc_dt * v_j + 0.5 (j = 0..N), ds = d[0:N],
+ *     kappa_k = k(s0 + (d_1 + ... + d_k)),  k = 0..N-1
+ *   dynamic (cascaded_mpc.py:323-330), xbar[B][N][8]:
+ *     ds_k = mpc_dt * Ux_k,  kappa_k = k(((ds_0 + ... + ds_k) - ds_0) + s0)
+ * computed in fp64 in numpy's operation order, rounded to the context dtype on store. */
+int vc_horizon(vc_ctx* ctx, int B, const void* x0, const void* xbar, double mpc_dt, void* kappa, void* ds,
+               int flags);
+
+/* Plant step of RacingCar.drive: x64 <- transition(x64, u0, k(s), dt) in fp64 (the
+ * reference's plant is an fp64 CasADi function; kinematic Euler, dynamic RK4), with
+ * k from the track table.  x64[B][nx] fp64 in/out, u0[B][nu] context dtype;
+ * x_ctx[B][nx] (context dtype, may be NULL) receives the new state for the next solve. */
+int vc_drive(vc_ctx* ctx, int B, double* x64, const void* u0, double dt, void* x_ctx, int flags);
+
+/* `steps` closed-loop steps for B vehicles, all on the device (one HIP stream):
+ *   vc_horizon(x, xbar) -> vc_solve(x, kappa, ds, xbar, ubar) -> vc_drive(x, u0)
+ * x64[B][nx] fp64 in/out (plant state), xbar/ubar the warm starts in/out (context
+ * dtype, shapes of vc_solve).  A problem whose status is not VC_SOLVED still applies
+ * its u0 (zero if non-finite), increments nfail[b] (int32, may be NULL; not cleared),
+ * and restarts from the neutral warm start (ubar = 0, xbar = the new state) -- the
+ * reference's simulator swallows the solver exception instead (racing.py:416-423).
+ * Optional logs (may be NULL): log_x[steps+1][B][nx] fp64 (the state before each step
+ * and after the last), log_u[steps][B][nu] context dtype (the applied u0).
+ * Requires vc_track_set and a built vc_solve combination. */
+int vc_simulate(vc_ctx* ctx, int B, int steps, double mpc_dt, double dt, double* x64, void* xbar, void* ubar,
+                double* log_x, void* log_u, int32_t* nfail, int flags);
 
 #ifdef __cplusplus
 }

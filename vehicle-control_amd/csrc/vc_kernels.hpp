@@ -65,6 +65,20 @@ __host__ __device__ inline const DynCoef<double>& dyn_coef<double>(const ModelAr
 template <>
 __host__ __device__ inline const DynCoef<float>& dyn_coef<float>(const ModelArgs& m) { return m.dyn32; }
 
+// Curvature table k(s) (track.hip, vc_track_set): n cubic pieces on a uniform grid h,
+// coef[n][4] = (c0, c1, c2, c3) in the local coordinate t = s - i h, lap length `length`.
+struct TrackTable {
+  const double* coef;
+  int n;
+  double h, length;
+};
+
+hipError_t launch_track_k(const TrackTable& tt, int dtype, int B, const void* s, void* k, hipStream_t st);
+hipError_t launch_horizon(const TrackTable& tt, int model, int dtype, int B, int N, const void* x0, bool x0_fp64,
+                          const void* xbar, double mpc_dt, void* kappa, void* ds, void* x0_out, hipStream_t st);
+hipError_t launch_drive(const ModelArgs& m, int dtype, const TrackTable& tt, double* x64, const void* u0, double dt,
+                        void* x_ctx, const int32_t* status, void* xbar, void* ubar, int32_t* nfail, double* log_x,
+                        void* log_u, hipStream_t st);
 hipError_t launch_kin_ltv(const KinLtvArgs& a, int N, hipStream_t stream);
 hipError_t launch_dyn_sqp(const DynSqpArgs& a, int N, hipStream_t stream);
 size_t dyn_sqp_smem_bytes(int N);

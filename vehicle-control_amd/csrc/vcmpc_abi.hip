@@ -5,6 +5,7 @@
 // the host: every numeric result comes from a gfx950 kernel.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -30,6 +31,11 @@ struct vc_ctx {
   hipStream_t stream = nullptr;
   void* arena = nullptr;
   size_t arena_bytes = 0;
+  void* track = nullptr;  // vc_track_set: [n][4] fp64 curvature pieces
+  int track_n = 0;
+  double track_h = 0.0, track_len = 0.0;
+  void* sim = nullptr;    // vc_simulate scratch (kappa, ds, x, u0, status, iters)
+  size_t sim_bytes = 0;
   std::string err;
 };
 
@@ -113,6 +119,12 @@ vc::ModelArgs model_args(const vc_ctx* c, int B) {
   m.dyn64 = vc::make_dyn_coef<double>(c->p.dyn_car);
   m.dyn32 = vc::make_dyn_coef<float>(c->p.dyn_car);
   return m;
+}
+
+int ns_of(const vc_ctx* c) { return c->model == VC_MODEL_KINEMATIC ? c->N + 1 : c->N; }
+size_t al256(size_t b) { return (b + 255) & ~size_t(255); }
+vc::TrackTable track_table(const vc_ctx* c) {
+  return vc::TrackTable{static_cast<const double*>(c->track), c->track_n, c->track_h, c->track_len};
 }
 
 bool kin_solve_built(const vc_ctx* c) {
@@ -221,6 +233,8 @@ void vc_destroy(vc_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->arena) (void)hipFree(c->arena);
+  if (c->track) (void)hipFree(c->track);
+  if (c->sim) (void)hipFree(c->sim);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
 }
@@ -445,6 +459,148 @@ int vc_spatial_step(vc_ctx* c, int B, const void* x, const void* u, const void* 
     return unstage(c, slots);
   }
   VC_HIP(c, vc::launch_spatial_step(m, c->dtype, x, u, kappa, ds, x_next, c->stream));
+  return 0;
+}
+
+int vc_track_set(vc_ctx* c, int n_pieces, double h, double length, const double* coef) {
+  if (!c) return VC_E_ARG;
+  if (n_pieces < 1 || !(h > 0) || !(length > 0) || !coef)
+    return fail(c, VC_E_ARG, "vc_track_set: need n_pieces >= 1, h > 0, length > 0, coef");
+  for (int i = 0; i < 4 * n_pieces; ++i)
+    if (!std::isfinite(coef[i])) return fail(c, VC_E_ARG, "vc_track_set: coef[%d] not finite", i);
+  VC_HIP(c, hipSetDevice(c->device));
+  VC_HIP(c, hipStreamSynchronize(c->stream));  // no kernel may still read the old table
+  if (c->track) VC_HIP(c, hipFree(c->track));
+  c->track = nullptr;
+  c->track_n = 0;
+  VC_HIP(c, hipMalloc(&c->track, (size_t)n_pieces * 4 * sizeof(double)));
+  VC_HIP(c, hipMemcpy(c->track, coef, (size_t)n_pieces * 4 * sizeof(double), hipMemcpyHostToDevice));
+  c->track_n = n_pieces;
+  c->track_h = h;
+  c->track_len = length;
+  return 0;
+}
+
+int vc_track_k(vc_ctx* c, int B, const void* s, void* k, int flags) {
+  if (int r = check_common(c, B, flags)) return r;
+  if (!s || !k) return fail(c, VC_E_ARG, "null pointer");
+  if (!c->track) return fail(c, VC_E_ARG, "vc_track_k: no track table (vc_track_set)");
+  if (B == 0) return 0;
+  const size_t es = esize(c);
+  if (flags == VC_HOST_PTRS) {
+    std::vector<Slot> slots = {{s, nullptr, B * es, nullptr}, {nullptr, k, B * es, nullptr}};
+    if (int r = stage(c, slots)) return r;
+    VC_HIP(c, vc::launch_track_k(track_table(c), c->dtype, B, slots[0].dev, slots[1].dev, c->stream));
+    return unstage(c, slots);
+  }
+  VC_HIP(c, vc::launch_track_k(track_table(c), c->dtype, B, s, k, c->stream));
+  return 0;
+}
+
+int vc_horizon(vc_ctx* c, int B, const void* x0, const void* xbar, double mpc_dt, void* kappa, void* ds,
+               int flags) {
+  if (int r = check_common(c, B, flags)) return r;
+  if (!x0 || !xbar || !kappa || !ds) return fail(c, VC_E_ARG, "null pointer");
+  if (!c->track) return fail(c, VC_E_ARG, "vc_horizon: no track table (vc_track_set)");
+  if (B == 0) return 0;
+  const int N = c->N, nx = nx_of(c), NS = ns_of(c);
+  const size_t es = esize(c);
+  if (flags == VC_HOST_PTRS) {
+    std::vector<Slot> slots = {{x0, nullptr, (size_t)B * nx * es, nullptr},
+                               {xbar, nullptr, (size_t)B * NS * nx * es, nullptr},
+                               {nullptr, kappa, (size_t)B * N * es, nullptr},
+                               {nullptr, ds, (size_t)B * N * es, nullptr}};
+    if (int r = stage(c, slots)) return r;
+    VC_HIP(c, vc::launch_horizon(track_table(c), c->model, c->dtype, B, N, slots[0].dev, c->dtype == VC_F64,
+                                 slots[1].dev, mpc_dt, slots[2].dev, slots[3].dev, nullptr, c->stream));
+    return unstage(c, slots);
+  }
+  VC_HIP(c, vc::launch_horizon(track_table(c), c->model, c->dtype, B, N, x0, c->dtype == VC_F64, xbar, mpc_dt, kappa,
+                               ds, nullptr, c->stream));
+  return 0;
+}
+
+int vc_drive(vc_ctx* c, int B, double* x64, const void* u0, double dt, void* x_ctx, int flags) {
+  if (int r = check_common(c, B, flags)) return r;
+  if (!x64 || !u0) return fail(c, VC_E_ARG, "null pointer");
+  if (!c->track) return fail(c, VC_E_ARG, "vc_drive: no track table (vc_track_set)");
+  if (B == 0) return 0;
+  const int nx = nx_of(c);
+  const size_t es = esize(c);
+  vc::ModelArgs m = model_args(c, B);
+  if (flags == VC_HOST_PTRS) {
+    std::vector<Slot> slots = {{x64, x64, (size_t)B * nx * 8, nullptr},
+                               {u0, nullptr, (size_t)B * 2 * es, nullptr},
+                               {nullptr, x_ctx, x_ctx ? (size_t)B * nx * es : 0, nullptr}};
+    if (int r = stage(c, slots)) return r;
+    VC_HIP(c, vc::launch_drive(m, c->dtype, track_table(c), (double*)slots[0].dev, slots[1].dev, dt,
+                               x_ctx ? slots[2].dev : nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                               c->stream));
+    return unstage(c, slots);
+  }
+  VC_HIP(c, vc::launch_drive(m, c->dtype, track_table(c), x64, u0, dt, x_ctx, nullptr, nullptr, nullptr, nullptr,
+                             nullptr, nullptr, c->stream));
+  return 0;
+}
+
+int vc_simulate(vc_ctx* c, int B, int steps, double mpc_dt, double dt, double* x64, void* xbar, void* ubar,
+                double* log_x, void* log_u, int32_t* nfail, int flags) {
+  if (int r = check_common(c, B, flags)) return r;
+  if (!x64 || !xbar || !ubar) return fail(c, VC_E_ARG, "null pointer");
+  if (steps < 0) return fail(c, VC_E_ARG, "steps %d < 0", steps);
+  if (!c->track) return fail(c, VC_E_ARG, "vc_simulate: no track table (vc_track_set)");
+  if (!kin_solve_built(c) && !dyn_solve_built(c))
+    return fail(c, VC_E_UNSUPPORTED, "vc_simulate: model=%d dtype=%d N=%d has no built vc_solve", c->model, c->dtype,
+                c->N);
+  if (B == 0 || steps == 0) return 0;
+  const int N = c->N, nx = nx_of(c), NS = ns_of(c);
+  const size_t es = esize(c);
+  std::vector<Slot> slots;
+  double* dx = x64;
+  void *dxbar = xbar, *dubar = ubar, *dlu = log_u;
+  double* dlx = log_x;
+  int32_t* dnf = nfail;
+  if (flags == VC_HOST_PTRS) {
+    slots = {{x64, x64, (size_t)B * nx * 8, nullptr},
+             {xbar, xbar, (size_t)B * NS * nx * es, nullptr},
+             {ubar, ubar, (size_t)B * N * 2 * es, nullptr},
+             {nullptr, log_x, log_x ? (size_t)(steps + 1) * B * nx * 8 : 0, nullptr},
+             {nullptr, log_u, log_u ? (size_t)steps * B * 2 * es : 0, nullptr},
+             {nfail, nfail, nfail ? (size_t)B * 4 : 0, nullptr}};
+    if (int r = stage(c, slots)) return r;
+    dx = (double*)slots[0].dev;
+    dxbar = slots[1].dev;
+    dubar = slots[2].dev;
+    dlx = log_x ? (double*)slots[3].dev : nullptr;
+    dlu = log_u ? slots[4].dev : nullptr;
+    dnf = nfail ? (int32_t*)slots[5].dev : nullptr;
+  }
+  // scratch: kappa[B][N], ds[B][N], x[B][nx], u0[B][2] (context dtype), status[B], iters[B]
+  const size_t o_kap = 0, o_ds = o_kap + al256((size_t)B * N * es), o_x = o_ds + al256((size_t)B * N * es),
+               o_u0 = o_x + al256((size_t)B * nx * es), o_st = o_u0 + al256((size_t)B * 2 * es),
+               o_it = o_st + al256((size_t)B * 4), total = o_it + al256((size_t)B * 4);
+  if (total > c->sim_bytes) {
+    VC_HIP(c, hipStreamSynchronize(c->stream));
+    if (c->sim) VC_HIP(c, hipFree(c->sim));
+    c->sim = nullptr;
+    c->sim_bytes = 0;
+    VC_HIP(c, hipMalloc(&c->sim, total));
+    c->sim_bytes = total;
+  }
+  char* base = static_cast<char*>(c->sim);
+  void *kap = base + o_kap, *dsv = base + o_ds, *xc = base + o_x, *u0 = base + o_u0;
+  int32_t *st = (int32_t*)(base + o_st), *it = (int32_t*)(base + o_it);
+  const vc::TrackTable tt = track_table(c);
+  vc::ModelArgs m = model_args(c, B);
+  if (dlx) VC_HIP(c, hipMemcpyAsync(dlx, dx, (size_t)B * nx * 8, hipMemcpyDeviceToDevice, c->stream));
+  for (int step = 0; step < steps; ++step) {
+    VC_HIP(c, vc::launch_horizon(tt, c->model, c->dtype, B, N, dx, true, dxbar, mpc_dt, kap, dsv, xc, c->stream));
+    if (int r = vc_solve_diag(c, B, xc, kap, dsv, dxbar, dubar, u0, st, it, nullptr, VC_DEVICE_PTRS)) return r;
+    VC_HIP(c, vc::launch_drive(m, c->dtype, tt, dx, u0, dt, nullptr, st, dxbar, dubar, dnf,
+                               dlx ? dlx + (size_t)(step + 1) * B * nx : nullptr,
+                               dlu ? (char*)dlu + (size_t)step * B * 2 * es : nullptr, c->stream));
+  }
+  if (flags == VC_HOST_PTRS) return unstage(c, slots);
   return 0;
 }
 

@@ -12,7 +12,7 @@ import os
 
 LIB_NAME = "libvcmpc.so"
 LIB_PATH = os.environ.get("VCMPC_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME))
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 VC_MODEL_KINEMATIC, VC_MODEL_DYNAMIC = 0, 1
 VC_F64, VC_F32 = 0, 1
@@ -88,6 +88,11 @@ PROTOTYPES = {
     "vc_condense": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int]),
     "vc_plant_step": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, C.c_double, _vp, C.c_int]),
     "vc_spatial_step": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, C.c_int]),
+    "vc_track_set": (C.c_int, [_vp, C.c_int, C.c_double, C.c_double, _vp]),
+    "vc_track_k": (C.c_int, [_vp, C.c_int, _vp, _vp, C.c_int]),
+    "vc_horizon": (C.c_int, [_vp, C.c_int, _vp, _vp, C.c_double, _vp, _vp, C.c_int]),
+    "vc_drive": (C.c_int, [_vp, C.c_int, _vp, _vp, C.c_double, _vp, C.c_int]),
+    "vc_simulate": (C.c_int, [_vp, C.c_int, C.c_int, C.c_double, C.c_double, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int]),
 }
 
 _LIB = None

@@ -1,1 +1,2 @@
 from .curvature import CurvatureTrack  # noqa: F401
+from .track import Track  # noqa: F401

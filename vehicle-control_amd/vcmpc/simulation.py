@@ -1,0 +1,144 @@
+"""Batched closed-loop racing simulator on the device (BASELINE config 5).
+
+The reference's ``RacingSimulator`` (simulation/racing.py:217-242, :416-423) steps
+each car in a Python loop: ``controller.command(car.state)`` (IPOPT), then
+``car.drive(action)`` (a CasADi plant call with ``track.k(s)``), then logs the
+state and action.  ``BatchedRacingSimulator`` runs the same loop for B vehicles
+with every step on the GPU (``vc_simulate``): horizon parameters from the
+unshifted warm start and the curvature table, the fused MPC solve, the fp64
+plant step -- no host round trip between steps.
+
+Per-vehicle failure handling (the reference prints and drops the step,
+racing.py:417-422): a solve whose status is not VC_SOLVED still applies its u0
+(zero if non-finite), is counted in ``nfail``, and the next step starts from the
+neutral warm start.  The single-vehicle controllers instead re-solve at once from
+the neutral warm start (controllers/*.py); both are documented deviations.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _abi
+from .config import make_params
+from .solver import Context
+
+IV_KIN, IS_KIN = 0, 2
+IUX, IS_DYN = 0, 4
+
+
+def _is_dynamic(car) -> bool:
+    return getattr(car, "MODEL", _abi.VC_MODEL_KINEMATIC) == _abi.VC_MODEL_DYNAMIC
+
+
+class BatchedRacingSimulator:
+    """B vehicles of one model on one track, one controller config, one GPU.
+
+    ``car`` is a ``KinematicCar`` or ``DynamicCar`` (its config and tyre are used),
+    ``controller_config`` the matching controller yaml (``kinematic_mpc`` /
+    ``dynamic_mpc``), ``track`` a ``vcmpc.environment.Track``.  Buffers live on
+    ``cuda:<device>`` as torch tensors when torch is importable (the fast path),
+    else in host numpy arrays staged by every call."""
+
+    def __init__(self, car, controller_config, track, batch: int, device: int = 0, seed: int | None = 31,
+                 use_torch: bool = True):
+        cfg = controller_config
+        if int(cfg.get("horizon_pm", 0)) > 0:
+            raise NotImplementedError("the cascaded point-mass tail (cascaded_mpc.py:181-277) is SURVEY 8(f) row 3")
+        if cfg.get("obstacles", False):
+            raise NotImplementedError("obstacle barrier terms are SURVEY 8(f) row 4")
+        self.car, self.config, self.track = car, cfg, track
+        self.dynamic = _is_dynamic(car)
+        self.B, self.N = int(batch), int(cfg["horizon"])
+        self.mpc_dt = float(cfg["mpc_dt"])
+        self.dt = float(car.dt)
+        if self.dynamic:
+            params = make_params(dyn_car=car.config, dyn_mpc=cfg, tyre=getattr(car, "tyre", "fiala"))
+            model, dtype = _abi.VC_MODEL_DYNAMIC, _abi.VC_F32
+        else:
+            params = make_params(kin_car=car.config, kin_mpc=cfg)
+            model, dtype = _abi.VC_MODEL_KINEMATIC, _abi.VC_F64
+        self.ctx = Context(model=model, N=self.N, max_batch=self.B, dtype=dtype, device=device, params=params)
+        self.ctx.set_track(track)
+        self.nx, self.ns = self.ctx.nx, self.ctx.ns_solve
+        self.np_dtype = np.float32 if dtype == _abi.VC_F32 else np.float64
+        self.torch = None
+        if use_torch:
+            try:
+                import torch
+                if torch.cuda.is_available():
+                    self.torch = torch
+            except ImportError:
+                pass
+        if self.torch is not None:  # one stream for torch's copies and the vc_* kernels
+            self.ctx.set_stream(self.torch.cuda.current_stream(device).cuda_stream)
+        self._init_warm_start(seed)
+        self.x = None
+        self.nfail = self._to_dev(np.zeros(self.B, np.int32))
+
+    # -- buffers ----------------------------------------------------------------------
+    def _to_dev(self, a):
+        a = np.ascontiguousarray(a)
+        if self.torch is None:
+            return a.copy()
+        return self.torch.from_numpy(a).to(f"cuda:{self.ctx.device}")
+
+    @staticmethod
+    def _to_host(a):
+        return a.detach().cpu().numpy() if hasattr(a, "detach") else np.array(a)
+
+    def _init_warm_start(self, seed):
+        """The controllers' initial predictions: kinematic_mpc.py:64-68 (zeros, v = 0.1)
+        and cascaded_mpc.py:72-76 (ones, Ux + 3); actions 1 + U[0, 1), projected onto
+        the input box (see controllers/*.py)."""
+        rng = np.random.RandomState(seed) if seed is not None else np.random
+        B, N, ns, nx = self.B, self.N, self.ns, self.nx
+        ic = self.config["input_constraints"]
+        if self.dynamic:
+            xbar = np.ones((B, ns, nx))
+            xbar[..., IUX] += 3
+        else:
+            xbar = np.zeros((B, ns, nx))
+            xbar[..., IV_KIN] += 0.1
+        ubar = np.ones((B, N, 2)) + np.swapaxes(rng.random_sample((B, 2, N)), 1, 2)
+        if self.dynamic:
+            np.clip(ubar[..., 1], ic["w_min"], ic["w_max"], out=ubar[..., 1])
+        else:
+            np.clip(ubar[..., 0], ic["a_min"], ic["a_max"], out=ubar[..., 0])
+            np.clip(ubar[..., 1], ic["w_min"], ic["w_max"], out=ubar[..., 1])
+        self.xbar = self._to_dev(xbar.astype(self.np_dtype))
+        self.ubar = self._to_dev(ubar.astype(self.np_dtype))
+
+    def reset(self, states):
+        """Set the B plant states (fp64 [B, nx], reference FancyVector order)."""
+        states = np.asarray(states, np.float64).reshape(self.B, self.nx)
+        self.x = self._to_dev(states)
+        return self
+
+    # -- loop ---------------------------------------------------------------------------
+    def run(self, steps: int, log: bool = True):
+        """``steps`` closed-loop steps of every vehicle.  Returns a dict with
+        ``state_traj`` [steps+1, B, nx] (fp64) and ``action_traj`` [steps, B, nu]
+        (host numpy, when ``log``) and ``nfail`` [B] (cumulative)."""
+        if self.x is None:
+            raise RuntimeError("reset(states) first")
+        log_x, log_u, nf = self.ctx.simulate(self.x, self.xbar, self.ubar, steps, self.mpc_dt, self.dt, log=log,
+                                             nfail=self.nfail)
+        self.ctx.synchronize()
+        out = {"nfail": self._to_host(nf)}
+        if log:
+            out["state_traj"] = self._to_host(log_x)
+            out["action_traj"] = self._to_host(log_u)
+        return out
+
+    @property
+    def states(self):
+        return self._to_host(self.x)
+
+    @property
+    def state_prediction(self):
+        """(B, nx, NS) like the controllers' ``state_prediction``."""
+        return np.swapaxes(self._to_host(self.xbar), 1, 2)
+
+    @property
+    def action_prediction(self):
+        return np.swapaxes(self._to_host(self.ubar), 1, 2)

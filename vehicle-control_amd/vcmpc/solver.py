@@ -197,6 +197,75 @@ class Context:
         self._check(self.lib.vc_spatial_step(self._h, B, *ptrs, flags))
         return xn
 
+    # -- track table and closed loop ----------------------------
+    def set_track(self, track):
+        """Upload ``track``'s curvature table (``vc_track_set``); ``track`` is a
+        ``vcmpc.environment.Track`` (or anything with ``kappa_table()``)."""
+        coef, h, length = track.kappa_table()
+        coef = np.ascontiguousarray(coef, np.float64)
+        self._check(self.lib.vc_track_set(self._h, int(coef.shape[0]), float(h), float(length),
+                                          C.c_void_p(coef.ctypes.data)))
+        self.track = track
+
+    def track_k(self, s):
+        B, f = self._batch(s), _NP_DT[self.dtype]
+        k = self._like(s, (B,))
+        ptrs, flags = self._marshal([s, k], [(B,), (B,)], [f, f])
+        self._check(self.lib.vc_track_k(self._h, B, *ptrs, flags))
+        return k
+
+    def horizon(self, x0, xbar, mpc_dt):
+        """``_init_horizon`` on the device: (kappa[B, N], ds[B, N]) from the state and
+        the unshifted warm start xbar[B, NS, nx]."""
+        B, N, nx, f = self._batch(x0), self.N, self.nx, _NP_DT[self.dtype]
+        kappa, ds = self._like(x0, (B, N)), self._like(x0, (B, N))
+        ptrs, flags = self._marshal([x0, xbar, kappa, ds], [(B, nx), (B, self.ns_solve, nx), (B, N), (B, N)], [f] * 4)
+        self._check(self.lib.vc_horizon(self._h, B, ptrs[0], ptrs[1], float(mpc_dt), ptrs[2], ptrs[3], flags))
+        return kappa, ds
+
+    def drive(self, x64, u0, dt, x_ctx=None):
+        """``RacingCar.drive`` for B vehicles: x64[B, nx] (fp64) is advanced in place
+        with k(s) from the track table; returns x64 (and fills x_ctx if given)."""
+        B, nx, f = self._batch(x64), self.nx, _NP_DT[self.dtype]
+        arrs, shapes, dts = [x64, u0], [(B, nx), (B, NU)], [np.float64, f]
+        if x_ctx is not None:
+            arrs, shapes, dts = arrs + [x_ctx], shapes + [(B, nx)], dts + [f]
+        ptrs, flags = self._marshal(arrs, shapes, dts)
+        xc = ptrs[2] if x_ctx is not None else None
+        self._check(self.lib.vc_drive(self._h, B, ptrs[0], ptrs[1], float(dt), xc, flags))
+        return x64
+
+    def simulate(self, x64, xbar, ubar, steps, mpc_dt, dt, log=False, nfail=None):
+        """``vc_simulate``: ``steps`` closed-loop steps (horizon -> solve -> drive) on the
+        device.  x64, xbar, ubar are updated in place.  With ``log=True`` returns
+        (log_x[steps+1, B, nx] fp64, log_u[steps, B, nu], nfail[B]); else (None, None, nfail)."""
+        B, N, nx, f = self._batch(x64), self.N, self.nx, _NP_DT[self.dtype]
+        steps = int(steps)
+        dev = _is_torch(x64)
+        if nfail is None:
+            if dev:
+                import torch
+                nfail = torch.zeros((B,), dtype=torch.int32, device=x64.device)
+            else:
+                nfail = np.zeros((B,), np.int32)
+        arrs = [x64, xbar, ubar, nfail]
+        shapes = [(B, nx), (B, self.ns_solve, nx), (B, N, NU), (B,)]
+        dts = [np.float64, f, f, np.int32]
+        log_x = log_u = None
+        if log:
+            if dev:
+                import torch
+                log_x = torch.empty((steps + 1, B, nx), dtype=torch.float64, device=x64.device)
+                log_u = torch.empty((steps, B, NU), dtype=xbar.dtype, device=x64.device)
+            else:
+                log_x, log_u = np.empty((steps + 1, B, nx)), np.empty((steps, B, NU), f)
+            arrs, shapes, dts = arrs + [log_x, log_u], shapes + [(steps + 1, B, nx), (steps, B, NU)], dts + [np.float64, f]
+        ptrs, flags = self._marshal(arrs, shapes, dts)
+        lx, lu = (ptrs[4], ptrs[5]) if log else (None, None)
+        self._check(self.lib.vc_simulate(self._h, B, steps, float(mpc_dt), float(dt), ptrs[0], ptrs[1], ptrs[2],
+                                         lx, lu, ptrs[3], flags))
+        return log_x, log_u, nfail
+
     def _like(self, ref, shape):
         if _is_torch(ref):
             import torch
