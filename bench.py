@@ -10,10 +10,12 @@ its own batch (weak scaling, no data-path collective); rank 0 prints one JSON li
 The same line carries, under "c3", BASELINE config 3 -- B = 4096 dynamic-bicycle
 (linear tyre) single-track NMPC problems per GPU, N = 40, fp32, 3 SQP iterations
 (vc_solve on a dynamic context, csrc/dyn_sqp.hip) -- measured the same way; it is a
-secondary workload, not `value`.
+secondary workload, not `value`.  Under "c5": BASELINE config 5 -- the closed-loop
+Monte-Carlo, 8192 vehicles x 500 steps on ippodromo (horizon -> NMPC solve -> fp64
+plant, all on the device, vc_simulate), vehicles sharded over the ranks.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--c3-batch B3]
-                    [--no-c3] [--no-cpu-baseline]
+                    [--c5-vehicles V] [--c5-steps S] [--no-c3] [--no-c5] [--no-cpu-baseline]
 """
 from __future__ import annotations
 
@@ -97,6 +99,9 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=1024, help="problems in the CPU-baseline sample")
     ap.add_argument("--c3-batch", type=int, default=4096, help="C3 problems per GPU (config 3: 4096)")
     ap.add_argument("--no-c3", action="store_true", help="skip the secondary C3 measurement")
+    ap.add_argument("--c5-vehicles", type=int, default=C5_VEHICLES, help="C5 vehicles in total (config 5: 8192)")
+    ap.add_argument("--c5-steps", type=int, default=C5_STEPS, help="C5 closed-loop steps (config 5: 500)")
+    ap.add_argument("--no-c5", action="store_true", help="skip the secondary C5 closed-loop measurement")
     return ap.parse_args()
 
 
@@ -209,6 +214,99 @@ def run_c3(args, dev, stream, rank, dist, steps):
     return out, data
 
 
+C5_VEHICLES, C5_STEPS = 8192, 500
+
+
+def cpu_baseline_c5(x0, track, sample_vehicles=8, sample_steps=8):
+    """The oracle closed loop (oracle/dyn_sqp.py SQP + oracle/models.py fp64 RK4 plant +
+    oracle/track.py curvature), one host thread, on the first vehicles of the C5 job."""
+    import numpy as np
+    from threadpoolctl import threadpool_limits
+
+    from oracle import dyn_sqp as D
+    from oracle import models as M
+    from vcmpc.config import load_config
+    from vcmpc.workload import C5_MPC_DT
+    cfg = load_config("dynamic_mpc")
+    W = D.dyn_weights(cfg)
+    p = M.dyn_params_from_config(load_config("dynamic_car"))
+    B, N = sample_vehicles, C3_N
+    x = np.array(x0[:B], np.float64)
+    xbar = np.ones((B, N, C3_NX)); xbar[..., 0] += 3
+    ubar = np.zeros((B, N, 2))
+    with threadpool_limits(limits=1):
+        t0 = time.perf_counter()
+        for _ in range(sample_steps):
+            ds = np.empty((B, N)); kap = np.empty((B, N))
+            for b in range(B):
+                ds[b], kap[b] = D.dyn_horizon_params(x[b], xbar[b].T, C5_MPC_DT, N, track.k_periodic)
+            r = D.dyn_sqp_solve(x, ubar, kap, ds, p, W, "fiala")
+            ubar, xbar = r["u_star"], r["x_star"]
+            x = M.dyn_transition(x, r["u0"], track.k_periodic(x[:, 4]), 0.05, p, "fiala")
+        dt = time.perf_counter() - t0
+    return {"value": B * sample_steps / dt, "unit": "vehicle-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{B} vehicles x {sample_steps} closed-loop steps of the C5 job through the oracle "
+                      f"(horizon + 3-iteration SQP + RK4 plant, numpy fp64, 1 thread) in {dt:.2f} s"}
+
+
+def run_c5(args, dev, stream, rank, world, dist):
+    """BASELINE config 5: closed-loop Monte-Carlo, 8192 vehicles x 500 steps on ippodromo,
+    dynamic-bicycle (Fiala) NMPC N = 40 + fp64 RK4 plant, all on the device (vc_simulate).
+    The 8192 vehicles are split into contiguous shards over the ranks (strong scaling)."""
+    import numpy as np
+    import torch
+
+    from vcmpc.config import load_config
+    from vcmpc.environment import Track
+    from vcmpc.models import DynamicCar
+    from vcmpc.simulation import BatchedRacingSimulator
+    from vcmpc.workload import C5_MPC_DT, closed_loop_states, shard
+
+    track = Track.load("ippodromo")
+    x_all = closed_loop_states(args.c5_vehicles, track.length, seed=args.seed)
+    lo, hi = shard(args.c5_vehicles, rank, world)
+    B, K = hi - lo, args.c5_steps
+    cfg = load_config("dynamic_mpc")
+    cfg["mpc_dt"] = C5_MPC_DT
+    car = DynamicCar(load_config("dynamic_car"), track, tyre="fiala")
+    sim = BatchedRacingSimulator(car, cfg, track, batch=B, device=dev.index)
+    sim.ctx.set_stream(stream.cuda_stream)
+    sim.reset(x_all[lo:hi])
+    sim.run(3, log=False)                      # warm-up (module load, first-touch)
+    sim.reset(x_all[lo:hi])
+    sim._init_warm_start(args.seed)
+    sim.nfail.zero_()
+    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ev[0].record(stream)
+    log_x, _, nfail = sim.ctx.simulate(sim.x, sim.xbar, sim.ubar, K, sim.mpc_dt, sim.dt, log=True, nfail=sim.nfail)
+    ev[1].record(stream)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    gpu_ms = ev[0].elapsed_time(ev[1])
+    ey = log_x[:, :, 5].abs()
+    on_track = float((ey.max(dim=0).values < track.width / 2).double().mean())
+    max_ey = float(ey.max())
+    progress = float((log_x[-1, :, 4] - log_x[0, :, 4]).mean())
+    nf = float(nfail.sum())
+    del log_x
+    vsteps, elapsed_max, gpu_ms_max = dist.aggregate(float(B * K), elapsed, gpu_ms, dev)
+    out = {"metric": "closed-loop vehicle-steps/s (N=40 NMPC solve + fp64 plant per vehicle-step)",
+           "value": vsteps / elapsed_max, "unit": "vehicle-steps/s", "solves_per_s": vsteps / elapsed_max,
+           "steps": K, "ms_per_step": elapsed_max / K * 1e3, "gpu_ms_total": gpu_ms_max, "dtype": "f32 solve, f64 plant",
+           "scaling": "strong",
+           "config": {"workload": f"C5 closed loop on ippodromo: {args.c5_vehicles} vehicles x {K} steps (dt 0.05 s), "
+                                  f"dynamic-bicycle (Fiala) single-track NMPC N={C3_N}, mpc_dt {C5_MPC_DT}, "
+                                  f"3 SQP iterations", "vehicles_total": args.c5_vehicles, "vehicles_per_gpu": B,
+                      "horizon": C3_N, "parallelism": f"dp{world} (contiguous vehicle shards)"},
+           "closed_loop_rank0": {"on_track_frac": on_track, "max_abs_ey": max_ey, "mean_progress_m": progress,
+                                 "nonsolved_frac": nf / (B * K)}}
+    return out, x_all, track
+
+
 def main():
     args = parse()
     import numpy as np
@@ -280,6 +378,12 @@ def main():
             c3, c3_data = run_c3(args, dev, stream, rank, dist, max(3, args.steps // 4))
         except Exception as e:  # the headline line must still print
             c3 = {"error": f"{type(e).__name__}: {e}"}
+    c5 = c5_aux = None
+    if not args.no_c5:
+        try:
+            c5, *c5_aux = run_c5(args, dev, stream, rank, world, dist)
+        except Exception as e:
+            c5 = {"error": f"{type(e).__name__}: {e}"}
 
     if rank == 0:
         value = solves / elapsed_max
@@ -318,8 +422,14 @@ def main():
             out["cpu_baseline"] = cpu_baseline(data, min(args.cpu_sample, B))
             if c3_data is not None and "error" not in c3:
                 c3["cpu_baseline"] = cpu_baseline_c3(c3_data, 8)
+            if c5_aux and "error" not in c5:
+                from oracle.track import load_track
+                otrack = load_track(os.path.join(ROOT, "vehicle-control_amd", "config", "tracks", "ippodromo.yaml"))
+                c5["cpu_baseline"] = cpu_baseline_c5(c5_aux[0], otrack)
         if c3 is not None:
             out["c3"] = c3
+        if c5 is not None:
+            out["c5"] = c5
         print(json.dumps(out), flush=True)
     ctx.close()
     dist.shutdown()

@@ -125,3 +125,23 @@ def dynamic_batch(B: int, N: int = 40, seed: int = 31, mpc_dt: float = 0.03, tyr
             out[k].append(v[ok])
         have += int(ok.sum())
     return {k: np.ascontiguousarray(np.concatenate(v)[:B].astype(np.float32)) for k, v in out.items()}
+
+
+# ---- C5: closed-loop Monte-Carlo on a track --------------------------------------------
+C5_MPC_DT = 0.045   # N = 40 stages x 0.045 s = the reference's 1.8 s preview (singletrack.yaml: 60 x 0.03 s)
+
+
+def closed_loop_states(B: int, length: float, seed: int = 31) -> np.ndarray:
+    """Initial plant states [B, 8] (dynamic_car.py:209 order) for BASELINE config 5:
+    vehicles spread uniformly along the lap, at speeds, yaw rates, steering angles and
+    track errors inside the ranges of the reference's recorded runs."""
+    rng = np.random.default_rng(seed)
+    x = np.zeros((B, 8))
+    x[:, 0] = rng.uniform(8, 14, B)          # Ux
+    x[:, 1] = rng.uniform(-0.1, 0.1, B)      # Uy
+    x[:, 2] = rng.uniform(-0.05, 0.2, B)     # r
+    x[:, 3] = rng.uniform(-0.03, 0.1, B)     # delta
+    x[:, 4] = rng.uniform(0, length, B)      # s
+    x[:, 5] = rng.uniform(-1.5, 1.5, B)      # ey
+    x[:, 6] = rng.uniform(-0.1, 0.1, B)      # epsi
+    return x
