@@ -138,7 +138,7 @@ __device__ __forceinline__ void predict(DynSmem<N>& s, const DynCoef<float>& p, 
     const float u[2] = {s.ub[k][0], s.ub[k][1]};
     const float kap = s.kap[k];
     float xn[8];
-    rk4_apply<float, 8>(x, s.dsv[k], [&](const float* xs, float* f) { dyn_spatial_ode(xs, u, kap, p, f); }, xn);
+    rk4_apply<float, 8>(x, s.dsv[k], [&](const float* xs, float* f) { dyn_spatial_ode_alg(xs, u, kap, p, f); }, xn);
 #pragma unroll
     for (int i = 0; i < 8; ++i) x[i] = xn[i];
     if (lane == 0) {
@@ -172,7 +172,7 @@ __device__ __forceinline__ void linearize(DynSmem<N>& s, const DynCoef<float>& p
   const T kap(s.kap[k]);
   const T h(s.dsv[k]);
   T xn[8];
-  rk4_apply<T, 8>(x, h, [&](const T* xs, T* f) { dyn_spatial_ode(xs, u, kap, p, f); }, xn);
+  rk4_apply<T, 8>(x, h, [&](const T* xs, T* f) { dyn_spatial_ode_alg(xs, u, kap, p, f); }, xn);
   constexpr int row_of[7] = {0, 1, 2, 3, 5, 6, 7};
 #pragma unroll
   for (int r = 0; r < 7; ++r)
@@ -700,7 +700,7 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
       X5[4] = T2(s.ub[k][0]);
       X5[4].d[1] = 1.f;
       T2 o[7];
-      dyn_stage_terms(X5, p, o);
+      dyn_stage_terms_alg(X5, p, o);
 #pragma unroll
       for (int r = 0; r < 7; ++r) {
         fv[r] = o[r].v;

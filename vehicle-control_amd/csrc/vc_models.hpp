@@ -124,6 +124,10 @@ struct DynCoef {
   R xf_a, xf_b, xr_a, xr_b;  // (Xdf - Xbf)/2, (Xdf + Xbf)/2, (Xbr - Xdr)/2, (Xdr + Xbr)/2
   R gz0;                     // g cos(theta) cos(phi)
   R fzf_m, fzr_m;            // (b / l) m, (a / l) m
+  // extra constants of the algebraic-slip form (dyn_*_alg, fp32 SQP kernel only)
+  R h_l, inv_m, inv_Izz;     // h / l, 1 / m, 1 / Izz
+  R tamf_k, tamr_k;          // 3 eps / Caf, 3 eps / Car   (tan alphamod = Fymax * tam_k)
+  R fi1, fi2;                // 1 - 2 eps + eps^2, 3 eps^2 - 2 eps^3  (Fiala sliding branch)
   int tyre;
 };
 
@@ -138,6 +142,13 @@ __host__ __device__ inline DynCoef<R> make_dyn_coef(const vc_dyn_car& p) {
   c.gz0 = R(GRAVITY * cos(p.theta) * cos(p.phi));
   c.fzf_m = R(p.b / p.l * p.m);
   c.fzr_m = R(p.a / p.l * p.m);
+  c.h_l = R(p.h / p.l);
+  c.inv_m = R(1.0 / p.m);
+  c.inv_Izz = R(1.0 / p.Izz);
+  c.tamf_k = R(3.0 * p.eps / p.Caf);
+  c.tamr_k = R(3.0 * p.eps / p.Car);
+  c.fi1 = R(1.0 - 2.0 * p.eps + p.eps * p.eps);
+  c.fi2 = R(3.0 * p.eps * p.eps - 2.0 * p.eps * p.eps * p.eps);
   c.tyre = p.tyre;
   return c;
 }
@@ -241,6 +252,110 @@ __host__ __device__ inline void dyn_stage_terms(const T* X5, const DynCoef<R>& c
   out[2] = Fx - T(c.Peng) / Ux;
   const T bound_f = T(c.muf) * F.Fz_f * vcos(F.alpha_f);
   const T bound_r = T(c.mur) * F.Fz_r * vcos(F.alpha_r);
+  out[3] = F.Fx_f - bound_f;
+  out[4] = -F.Fx_f - bound_f;
+  out[5] = F.Fx_r - bound_r;
+  out[6] = -F.Fx_r - bound_r;
+}
+
+// ---------------------------------------------------------------------------
+// Algebraic-slip form of the same model, for the fp32 SQP kernel (dyn_sqp.hip).
+//
+// The slip angles enter the model only through tan(alpha), the comparison
+// |alpha| <= alphamod, sign(alpha) and cos(alpha), and alphamod = atan(3 Fymax eps / Ca)
+// only through tan(alphamod).  With z_f = (Uy + a r) / Ux, z_r = (Uy - b r) / Ux:
+//   tan(alpha_f) = tan(atan z_f - delta) = (z_f - tan delta) / (1 + z_f tan delta)
+//   tan(alpha_r) = z_r,            tan(alphamod) = 3 Fymax eps / Ca
+//   |alpha| <= alphamod  <=>  |tan alpha| <= tan alphamod,  sgn alpha = sgn tan alpha
+//   cos(alpha) = 1 / sqrt(1 + tan^2 alpha)          (|alpha| < pi/2)
+// so an evaluation needs no atan/tan and one sin/cos pair less, and divisions by
+// constants become products.  Same function as dyn_temporal_ode / dyn_stage_terms
+// (identities exact for |alpha| < pi/2); the fp64 plant and the oracle keep the
+// reference's literal form.
+// ---------------------------------------------------------------------------
+template <typename T, typename R>
+struct DynForcesAlg {
+  T Fx_f, Fx_r, Fz_f, Fz_r, ta_f, ta_r, cd, sd, iU;
+  __host__ __device__ DynForcesAlg(T Ux, T Uy, T r, T delta, T Fx, const DynCoef<R>& c) {
+    const T th = vtanh(T(2) * (Fx * T(1e-3) + T(0.5)));   // tanh(-y) = -tanh(y) for the rear split
+    Fx_f = Fx * (T(c.xf_a) * th + T(c.xf_b));
+    Fx_r = Fx * (T(c.xr_b) - T(c.xr_a) * th);
+    const T gz = T(c.gz0) + T(c.Av2) * (Ux * Ux);
+    Fz_f = T(c.fzf_m) * gz - T(c.h_l) * Fx;
+    Fz_r = T(c.fzr_m) * gz + T(c.h_l) * Fx;
+    iU = T(1) / Ux;
+    const T zf = (Uy + T(c.a) * r) * iU;
+    ta_r = (Uy - T(c.b) * r) * iU;
+    cd = vcos(delta);
+    sd = vsin(delta);
+    // tan(atan zf - delta) = (zf cd - sd) / (cd + zf sd)
+    ta_f = (zf * cd - sd) / (cd + zf * sd);
+  }
+  __host__ __device__ T fymax_f(const DynCoef<R>& c) const {
+    return vsqrt((T(c.muf) * Fz_f) * (T(c.muf) * Fz_f) - (T(0.99) * Fx_f) * (T(0.99) * Fx_f));
+  }
+  __host__ __device__ T fymax_r(const DynCoef<R>& c) const {
+    return vsqrt((T(c.mur) * Fz_r) * (T(c.mur) * Fz_r) - (T(0.99) * Fx_r) * (T(0.99) * Fx_r));
+  }
+};
+
+// Modified Fiala in tan(alpha) (dynamic_car.py:119-142): Ca ta (-1 + |q|/3 - q^2/27),
+// q = Ca ta / Fymax, inside |ta| <= tan alphamod; -Ca fi1 ta - Fymax fi2 sgn(ta) outside.
+template <typename T, typename R>
+__host__ __device__ inline T fiala_fy_alg(T ta, R Ca, T Fymax, R tam_k, R fi1, R fi2) {
+  const T q = (T(Ca) * ta) / Fymax;
+  const T inside = T(Ca) * ta * (T(-1) + vfabs(q) * T(1.f / 3.f) - q * q * T(1.f / 27.f));
+  const T sg = ta > T(0) ? T(1) : (ta < T(0) ? T(-1) : T(0));
+  const T outside = -T(Ca * fi1) * ta - Fymax * T(fi2) * sg;
+  return vfabs(ta) <= Fymax * T(tam_k) ? inside : outside;
+}
+
+template <typename T, typename R>
+__host__ __device__ inline void dyn_temporal_ode_alg(const T* x, const T* u, T kappa, const DynCoef<R>& c, T* f) {
+  const T Ux = x[0], Uy = x[1], r = x[2], ey = x[5], epsi = x[6];
+  const T Fx = u[0], w = u[1];
+  const DynForcesAlg<T, R> F(Ux, Uy, r, x[3], Fx, c);
+  T Fy_f, Fy_r;
+  if (c.tyre == VC_TYRE_LINEAR) {
+    Fy_f = -T(c.Caf) * F.ta_f;
+    Fy_r = -T(c.Car) * F.ta_r;
+  } else {
+    Fy_f = fiala_fy_alg(F.ta_f, c.Caf, F.fymax_f(c), c.tamf_k, c.fi1, c.fi2);
+    Fy_r = fiala_fy_alg(F.ta_r, c.Car, F.fymax_r(c), c.tamr_k, c.fi1, c.fi2);
+  }
+  const T Fd = T(c.Frr) + T(c.Cd) * (Ux * Ux);
+  const T lat_f = Fy_f * F.cd + F.Fx_f * F.sd;
+  f[0] = (F.Fx_f * F.cd - Fy_f * F.sd + F.Fx_r - Fd) * T(c.inv_m) + r * Uy;
+  f[1] = (lat_f + Fy_r) * T(c.inv_m) - r * Ux;
+  f[2] = (T(c.a) * lat_f - T(c.b) * Fy_r) * T(c.inv_Izz);
+  f[3] = w;
+  const T ce = vcos(epsi), se = vsin(epsi);
+  const T s_dot = (Ux * ce - Uy * se) / (T(1) - kappa * ey);
+  f[4] = s_dot;
+  f[5] = Ux * se + Uy * ce;
+  f[6] = r - kappa * s_dot;
+  f[7] = T(1);
+}
+
+template <typename T, typename R>
+__host__ __device__ inline void dyn_spatial_ode_alg(const T* x, const T* u, T kappa, const DynCoef<R>& c, T* f) {
+  dyn_temporal_ode_alg(x, u, kappa, c, f);
+  const T inv = T(1) / f[4];
+#pragma unroll
+  for (int i = 0; i < DYN_NX; ++i) f[i] = f[i] * inv;
+  f[4] = T(1);
+  f[7] = inv;
+}
+
+template <typename T, typename R>
+__host__ __device__ inline void dyn_stage_terms_alg(const T* X5, const DynCoef<R>& c, T* out) {
+  const T Ux = X5[0], Fx = X5[4];
+  const DynForcesAlg<T, R> F(Ux, X5[1], X5[2], X5[3], Fx, c);
+  out[0] = vfabs(F.ta_f) - F.fymax_f(c) * T(c.tamf_k);
+  out[1] = vfabs(F.ta_r) - F.fymax_r(c) * T(c.tamr_k);
+  out[2] = Fx - T(c.Peng) * F.iU;
+  const T bound_f = T(c.muf) * F.Fz_f / vsqrt(T(1) + F.ta_f * F.ta_f);
+  const T bound_r = T(c.mur) * F.Fz_r / vsqrt(T(1) + F.ta_r * F.ta_r);
   out[3] = F.Fx_f - bound_f;
   out[4] = -F.Fx_f - bound_f;
   out[5] = F.Fx_r - bound_r;
