@@ -19,6 +19,8 @@
  *   vc_plant_step    RacingCar.drive / Robot.transition  vehicle_control/models/racing_car.py:34-46,
  *                    kinematic_car.py:34-45,66-68 (Euler), dynamic_car.py:144-167,193-195 (RK4)
  *   vc_spatial_step  <Model>.spatial_transition       kinematic_car.py:70-72, dynamic_car.py:169-199
+ *   vc_set_obstacles Track._construct_obstacles       environment/track.py:131-138 (the obstacle list the
+ *                                                     barrier terms kinematic_mpc.py:130-133 read)
  *   vc_track_set     Track._precompute_curvatures     environment/track.py:156-167 (the bspline k(s) table)
  *   vc_track_k       Track.k                          track.py:162-166
  *   vc_horizon       KinematicMPC._init_horizon       kinematic_mpc.py:170-187
@@ -56,7 +58,8 @@
 extern "C" {
 #endif
 
-#define VCMPC_ABI_VERSION 3
+#define VCMPC_ABI_VERSION 4
+#define VC_MAX_OBSTACLES 16
 
 typedef struct vc_ctx vc_ctx;
 
@@ -92,6 +95,7 @@ typedef struct vc_kin_mpc {
   double w_time, w_ey, w_epsi, w_v, w_w, w_a, w_dev, w_b; /* cost_weights */
   double a_min, a_max, w_min, w_max;                      /* input_constraints */
   double v_min, v_max, delta_min, delta_max, ey_min, ey_max; /* state_constraints */
+  double w_obs;     /* cost_weights.obstacles (kinematic_mpc.py:130-133; used when obs.n > 0) */
 } vc_kin_mpc;
 
 /* Dynamic single-track MPC weights and bounds (config/controllers/singletrack.yaml,
@@ -104,6 +108,7 @@ typedef struct vc_dyn_mpc {
   double trust_Fx;   /* SQP trust region |Fx - Fxbar| <= trust_Fx [N] (0 = off) */
   int32_t sqp_iters; /* SQP iterations per solve (BASELINE config 3: 3) */
   int32_t pad_;
+  double w_obs;      /* cost_weights.obstacles (cascaded_mpc.py:173-176; used when obs.n > 0) */
 } vc_dyn_mpc;
 
 /* The build's LTV-QP contract knobs (no reference counterpart). */
@@ -116,12 +121,27 @@ typedef struct vc_qp {
   int32_t polish;   /* active-set polish rounds after the interior point (0 = off) */
 } vc_qp;
 
+/* Circular obstacles in track coordinates (Track._construct_obstacles, environment/
+ * track.py:131-138, data `obstacle_data: [s, ey, r]` of config/environment/*.yaml).
+ * n = 0 switches the barrier terms off (the controller's `obstacles: False`).
+ * The reference's stage cost w_obs ds / (dist - (r + 0.1)), dist = |(s, ey) - (s_j, ey_j)|
+ * (kinematic_mpc.py:130-133, cascaded_mpc.py:173-176) enters each QP as the convexified
+ * second-order model of its sum over obstacles in ey at the prediction; the margin
+ * dist - (r + 0.1) is floored at margin_min. */
+typedef struct vc_obstacles {
+  int32_t n;          /* number of obstacles, 0..VC_MAX_OBSTACLES */
+  int32_t pad_;
+  double margin_min;  /* floor of dist - (r + 0.1) in the barrier's derivatives [m] */
+  double s[VC_MAX_OBSTACLES], ey[VC_MAX_OBSTACLES], radius[VC_MAX_OBSTACLES];
+} vc_obstacles;
+
 typedef struct vc_params {
   vc_kin_car kin_car;
   vc_dyn_car dyn_car;
   vc_kin_mpc kin_mpc;
   vc_qp qp;         /* trust_a is the kinematic acceleration trust region; trust_w serves both */
   vc_dyn_mpc dyn_mpc;
+  vc_obstacles obs;
 } vc_params;
 
 int vc_abi_version(void);
@@ -140,6 +160,12 @@ const char* vc_last_error(const vc_ctx* ctx);
 /* Use an external HIP stream (hipStream_t passed as void*; NULL = the context's
  * own stream).  Lets a caller time the work with events on that stream. */
 int vc_set_stream(vc_ctx* ctx, void* stream);
+
+/* Replace the context's obstacle set (vc_params.obs) for later solves: n <= VC_MAX_OBSTACLES
+ * obstacles at host arrays s[n], ey[n], radius[n] (track.py:131-138); n = 0 turns the
+ * barrier terms off.  margin_min <= 0 keeps the current floor. */
+int vc_set_obstacles(vc_ctx* ctx, int n, const double* s, const double* ey, const double* radius,
+                     double margin_min);
 int vc_synchronize(vc_ctx* ctx);
 
 /* One MPC step for B problems (B <= max_batch):

@@ -29,6 +29,7 @@ QP cost = the reference NLP cost in Gauss-Newton form about (xbar, ubar), with e
   w_slip (|tan a_f| - tan amod_f(Fx))^2 if active at the prediction  :155-159 (front)
   w_slip (|tan a_r| - tan amod_r(Fx))^2 likewise                     :161-165 (rear)
   (w_Fx / ds_k) (Fx_{k+1} - Fx_k)^2, k < N-1                         :167-171
+  obstacle barrier, convexified in ey_k (W["obstacles"] set)          :173-176, obstacles.py
   terminal (state column N-1, cascaded_mpc.py:283 with M = 0):
   w_speed (Ux - max_speed)^2 if Uxbar >= max_speed, w_time t, w_ey ey^2, w_epsi epsi^2  :290-303
 Constraints (one-sided rows, each linearised at the prediction; state rows for
@@ -45,6 +46,7 @@ from __future__ import annotations
 import numpy as np
 
 from . import models as M
+from . import obstacles as OB
 
 IUX, IUY, IR, ID, IS, IEY, IEP, IT = range(8)
 IFX, IW = 0, 1
@@ -66,7 +68,8 @@ def dyn_weights(cfg: dict) -> dict:
         ey_min=float(sc["ey_min"]), ey_max=float(sc["ey_max"]),
         prox=float(qp.get("prox", 0.1)), fx_scale=float(qp.get("fx_scale", 1000.0)),
         trust_Fx=float(qp.get("trust_Fx", 0.0)), trust_w=float(qp.get("trust_w", 0.0)),
-        sqp_iters=int(qp.get("sqp_iters", 3)),
+        sqp_iters=int(qp.get("sqp_iters", 3)), w_obs=float(cw.get("obstacles", 0.0)), obstacles=[],
+        obs_margin_min=OB.MARGIN_MIN,
     )
 
 
@@ -183,6 +186,11 @@ def dyn_qp(x0, ubar, kappa, ds, p, W, tyre="linear"):
         add_square(W["w_dev"] * ds[:, k], ey, row)
         add_square(np.where(ey < W["ey_min"], W["w_b"] * ds[:, k], 0.0), ey - W["ey_min"], row)
         add_square(np.where(ey > W["ey_max"], W["w_b"] * ds[:, k], 0.0), ey - W["ey_max"], row)
+        if W.get("obstacles"):  # cascaded_mpc.py:173-176, convexified in ey (obstacles.py)
+            p_o, q_o = OB.ey_model(xbar[:, k, IS], ey, W["w_obs"] * ds[:, k], W["obstacles"],
+                                   W.get("obs_margin_min", OB.MARGIN_MIN))
+            H[:] += q_o[:, None, None] * row[:, :, None] * row[:, None, :]
+            g[:] += p_o[:, None] * row
         add_square(W["w_w"], ubar[:, k, IW], np.broadcast_to(eye[2 * k + 1], (B, n)))
         for ax in ("f", "r"):
             v, gr = T["slip_" + ax]

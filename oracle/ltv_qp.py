@@ -12,7 +12,7 @@ implemented identically by the HIP kernel:
 4. QP         min 1/2 dz'H dz + g'dz  s.t. input boxes and state rows below,
               where the cost is the reference NLP cost (kinematic_mpc.py:101-158)
               written exactly in the linearised states, with every ``if_else``
-              branch frozen at the predicted trajectory, ``obstacles`` off, plus
+              branch frozen at the predicted trajectory, plus
               a proximal term  prox * ||dz||^2  (the NLP Hessian is
               singular along the acceleration directions).
 5. output     u* = ubar + dz*,  x* = xbar + G dz*,  u0 = u*_0.
@@ -23,6 +23,7 @@ Cost terms (stage n = 0..N-1, terminal state x_N):
   w_dev ds_n ey_n^2                                          kinematic_mpc.py:122
   w_w w_n^2                                                  kinematic_mpc.py:124
   w_a (a_{n+1} - a_n)^2   for n < N-1                        kinematic_mpc.py:126-128
+  obstacle barrier, convexified in ey_n (W["obstacles"] set)  kinematic_mpc.py:130-133, obstacles.py
   w_v (v_N - v_max)^2     if  vbar_N >= v_max                kinematic_mpc.py:144-148
   w_time t_N + w_ey ey_N^2 + w_epsi epsi_N^2                 kinematic_mpc.py:149-157
 Constraints:
@@ -37,6 +38,7 @@ from __future__ import annotations
 import numpy as np
 
 from . import models as M
+from . import obstacles as OB
 
 IV, ID, IS, IEY, IEP, IT = range(6)
 IA, IW = 0, 1
@@ -56,7 +58,8 @@ def kin_weights(cfg: dict) -> dict:
         v_min=float(sc["v_min"]), v_max=float(sc["v_max"]),
         delta_min=float(sc["delta_min"]), delta_max=float(sc["delta_max"]),
         ey_min=float(sc["ey_min"]), ey_max=float(sc["ey_max"]),
-        prox=float(qp.get("prox", 1e-4)),
+        prox=float(qp.get("prox", 1e-4)), w_obs=float(cw.get("obstacles", 0.0)), obstacles=[],
+        obs_margin_min=OB.MARGIN_MIN,
         trust_a=float(qp.get("trust_a", 0.0)), trust_w=float(qp.get("trust_w", 0.0)),
     )
 
@@ -118,6 +121,11 @@ def kin_qp(x0, ubar, kappa, ds, L, W):
         hi = ey > W["ey_max"]
         add_square(np.where(lo, W["w_b"] * ds[:, k], 0.0), ey - W["ey_min"], row)
         add_square(np.where(hi, W["w_b"] * ds[:, k], 0.0), ey - W["ey_max"], row)
+        if W.get("obstacles"):  # kinematic_mpc.py:130-133, convexified in ey (obstacles.py)
+            p_o, q_o = OB.ey_model(xbar[:, k, IS], ey, W["w_obs"] * ds[:, k], W["obstacles"],
+                                   W.get("obs_margin_min", OB.MARGIN_MIN))
+            H[:] += q_o[:, None, None] * row[:, :, None] * row[:, None, :]
+            g[:] += p_o[:, None] * row
     # input costs: w_w w^2 and slew w_a (a_{n+1}-a_n)^2
     for k in range(N):
         e = np.zeros((B, n)); e[:, 2 * k + IW] = 1.0

@@ -741,10 +741,13 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
       // ---- Gauss-Newton cost (cascaded_mpc.py:139-171, 279-304), nonzero on q == 0 only ----
       const float blo = ey < float(W.ey_min) ? float(W.w_b) : 0.f;
       const float bhi = ey > float(W.ey_max) ? float(W.w_b) : 0.f;
-      qey = c0 * (2.f * ds * (float(W.w_dev) + blo + bhi) + term * 2.f * float(W.w_ey));
+      // obstacle barrier (cascaded_mpc.py:173-176), convexified quadratic in ey_k
+      float po = 0.f, qo = 0.f;
+      if (A.obs.n > 0) obstacle_ey_model<float>(A.obs, s.xb[k][4], ey, float(W.w_obs) * ds, po, qo);
+      qey = c0 * (2.f * ds * (float(W.w_dev) + blo + bhi) + term * 2.f * float(W.w_ey) + qo);
       const float gey = c0 * (2.f * ds * (float(W.w_dev) * ey + blo * (ey - float(W.ey_min)) +
                                           bhi * (ey - float(W.ey_max))) +
-                              term * 2.f * float(W.w_ey) * ey);
+                              term * 2.f * float(W.w_ey) * ey + po);
       qep = c0 * term * 2.f * float(W.w_epsi);
       const float gep = c0 * term * 2.f * float(W.w_epsi) * ep;
       float gv[5] = {0.f, 0.f, 0.f, 0.f, 0.f};

@@ -524,6 +524,14 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
     double* jr = s.jac[lane < N ? lane : N];  // row N: dummy
     jr[0] = J.q; jr[1] = J.qv; jr[2] = J.qey; jr[3] = J.qep;
     jr[4] = J.J33; jr[5] = J.J34; jr[6] = J.J41; jr[7] = J.J43; jr[8] = J.J44;
+    // obstacle barrier of stage k = 1..N-1 (kinematic_mpc.py:130-133) as a convexified
+    // quadratic in ey_k: adds to the ey_k weight / linear term S1 left in vc/vz[k-1]
+    if (A.obs.n > 0 && lane >= 1 && lane < N) {
+      double p, q;
+      obstacle_ey_model<double>(A.obs, xk[2], xk[3], W.w_obs * s.ds[k], p, q);
+      s.vc[k - 1] += q;
+      s.vz[k - 1] += p;
+    }
   }
   wave_sync();
   double gj = 0.0;

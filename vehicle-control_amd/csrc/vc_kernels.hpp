@@ -8,7 +8,39 @@
 #include "vc_models.hpp"
 #include "vcmpc.h"
 
+// Default floor of the obstacle barrier margin dist - (r + 0.1) [m] (vc_obstacles.margin_min).
+#define VC_OBS_MARGIN_MIN 0.05
+
 namespace vc {
+
+// Obstacle barrier of one stage as a convexified quadratic in ey:
+//   phi(ey) = sum_j w ds / (d_j - (r_j + 0.1)),  d_j = |(s, ey) - (s_j, ey_j)|
+// (kinematic_mpc.py:130-133, cascaded_mpc.py:173-176).  s is not a decision function
+// (s' = 1 in both spatial models), so the term is one-dimensional in ey.  Returns the
+// slope p = phi'(ey) and the curvature q = max(phi''(ey), 0), with the margin floored at
+// margin_min.  Operation order mirrored by oracle/obstacles.py.
+template <typename T>
+__device__ __forceinline__ void obstacle_ey_model(const vc_obstacles& o, T s, T ey, T wds, T& p, T& q) {
+  T ps = T(0), qs = T(0);
+  const T mmin = T(o.margin_min);
+  for (int j = 0; j < o.n; ++j) {
+    const T a = s - T(o.s[j]);
+    const T e = ey - T(o.ey[j]);
+    const T d2 = a * a + e * e;
+    const T d = sqrt(d2);
+    const T dc = d > T(1e-6) ? d : T(1e-6);
+    const T m0 = d - (T(o.radius[j]) + T(0.1));
+    const T m = m0 > mmin ? m0 : mmin;
+    const T d1 = e / dc;                  // d'(ey)
+    const T dd = (a * a) / (dc * dc * dc);  // d''(ey)
+    const T im = T(1) / m;
+    const T c1 = wds * im * im;           // w ds / m^2
+    ps -= c1 * d1;
+    qs += c1 * (T(2) * d1 * d1 * im - dd);
+  }
+  p = ps;
+  q = qs > T(0) ? qs : T(0);
+}
 
 // Fused kinematic LTV-MPC step (kin_ltv.hip).
 struct KinLtvArgs {
@@ -29,6 +61,7 @@ struct KinLtvArgs {
   double L;             // wheelbase
   vc_kin_mpc w;
   vc_qp qp;
+  vc_obstacles obs;
 };
 
 // Fused dynamic-bicycle SQP step (dyn_sqp.hip), fp32.
@@ -48,6 +81,7 @@ struct DynSqpArgs {
   DynCoef<float> car;
   vc_dyn_mpc w;
   vc_qp qp;
+  vc_obstacles obs;
 };
 
 // Elementwise model kernels (models.hip).

@@ -147,6 +147,7 @@ int dyn_solve(vc_ctx* c, int B, const void* x0, const void* kappa, const void* d
   a.car = vc::make_dyn_coef<float>(c->p.dyn_car);
   a.w = w;
   a.qp = c->p.qp;
+  a.obs = c->p.obs;
   std::vector<Slot> slots;
   if (flags == VC_HOST_PTRS) {
     slots = {{x0, nullptr, (size_t)B * nx * 4, nullptr},
@@ -217,7 +218,12 @@ vc_ctx* vc_create(int device, int model, int N, int max_batch, int dtype, const 
   c->N = N;
   c->max_batch = max_batch;
   c->dtype = dtype;
+  if (params->obs.n < 0 || params->obs.n > VC_MAX_OBSTACLES) {
+    fail(nullptr, VC_E_ARG, "obs.n=%d outside [0,%d]", params->obs.n, VC_MAX_OBSTACLES);
+    return nullptr;
+  }
   c->p = *params;
+  if (!(c->p.obs.margin_min > 0)) c->p.obs.margin_min = VC_OBS_MARGIN_MIN;
   e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking);
   if (e != hipSuccess) {
     fail(nullptr, VC_E_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
@@ -244,6 +250,24 @@ const char* vc_last_error(const vc_ctx* c) { return c ? c->err.c_str() : g_creat
 int vc_set_stream(vc_ctx* c, void* stream) {
   if (!c) return VC_E_ARG;
   c->stream = stream ? static_cast<hipStream_t>(stream) : c->own;
+  return 0;
+}
+
+int vc_set_obstacles(vc_ctx* c, int n, const double* s, const double* ey, const double* radius, double margin_min) {
+  if (!c) return VC_E_ARG;
+  if (n < 0 || n > VC_MAX_OBSTACLES) return fail(c, VC_E_ARG, "n=%d obstacles outside [0,%d]", n, VC_MAX_OBSTACLES);
+  if (n > 0 && (!s || !ey || !radius)) return fail(c, VC_E_ARG, "null pointer");
+  vc_obstacles o{};
+  o.n = n;
+  o.margin_min = margin_min > 0 ? margin_min : c->p.obs.margin_min;
+  for (int j = 0; j < n; ++j) {
+    if (!std::isfinite(s[j]) || !std::isfinite(ey[j]) || !std::isfinite(radius[j]))
+      return fail(c, VC_E_ARG, "obstacle %d is not finite", j);
+    o.s[j] = s[j];
+    o.ey[j] = ey[j];
+    o.radius[j] = radius[j];
+  }
+  c->p.obs = o;
   return 0;
 }
 
@@ -276,6 +300,7 @@ int vc_solve_diag(vc_ctx* c, int B, const void* x0, const void* kappa, const voi
   a.L = c->p.kin_car.l;
   a.w = c->p.kin_mpc;
   a.qp = c->p.qp;
+  a.obs = c->p.obs;
   std::vector<Slot> slots;
   if (flags == VC_HOST_PTRS) {
     slots = {{x0, nullptr, (size_t)B * nx * 8, nullptr},
@@ -341,6 +366,7 @@ int vc_condense(vc_ctx* c, int B, const void* x0, const void* ubar, const void* 
   a.L = c->p.kin_car.l;
   a.w = c->p.kin_mpc;
   a.qp = c->p.qp;
+  a.obs = c->p.obs;
   std::vector<Slot> slots;
   if (flags == VC_HOST_PTRS) {
     slots = {{x0, nullptr, (size_t)B * 6 * 8, nullptr},

@@ -12,7 +12,9 @@ import os
 
 LIB_NAME = "libvcmpc.so"
 LIB_PATH = os.environ.get("VCMPC_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME))
-ABI_VERSION = 3
+ABI_VERSION = 4
+VC_MAX_OBSTACLES = 16
+OBS_MARGIN_MIN = 0.05  # VC_OBS_MARGIN_MIN (csrc/vc_kernels.hpp)
 
 VC_MODEL_KINEMATIC, VC_MODEL_DYNAMIC = 0, 1
 VC_F64, VC_F32 = 0, 1
@@ -39,14 +41,14 @@ class vc_kin_mpc(C.Structure):
     _fields_ = [(k, C.c_double) for k in (
         "w_time", "w_ey", "w_epsi", "w_v", "w_w", "w_a", "w_dev", "w_b",
         "a_min", "a_max", "w_min", "w_max",
-        "v_min", "v_max", "delta_min", "delta_max", "ey_min", "ey_max")]
+        "v_min", "v_max", "delta_min", "delta_max", "ey_min", "ey_max", "w_obs")]
 
 
 class vc_dyn_mpc(C.Structure):
     _fields_ = [(k, C.c_double) for k in (
         "w_time", "w_speed", "w_ey", "w_epsi", "w_w", "w_Fx", "w_dev", "w_b", "w_slip",
         "w_min", "w_max", "Ux_min", "max_speed", "delta_min", "delta_max", "ey_min", "ey_max",
-        "fx_scale", "trust_Fx")] + [("sqp_iters", C.c_int32), ("pad_", C.c_int32)]
+        "fx_scale", "trust_Fx")] + [("sqp_iters", C.c_int32), ("pad_", C.c_int32), ("w_obs", C.c_double)]
 
 
 class vc_qp(C.Structure):
@@ -54,9 +56,15 @@ class vc_qp(C.Structure):
                 ("max_iter", C.c_int32), ("polish", C.c_int32)]
 
 
+class vc_obstacles(C.Structure):
+    _fields_ = [("n", C.c_int32), ("pad_", C.c_int32), ("margin_min", C.c_double),
+                ("s", C.c_double * VC_MAX_OBSTACLES), ("ey", C.c_double * VC_MAX_OBSTACLES),
+                ("radius", C.c_double * VC_MAX_OBSTACLES)]
+
+
 class vc_params(C.Structure):
     _fields_ = [("kin_car", vc_kin_car), ("dyn_car", vc_dyn_car), ("kin_mpc", vc_kin_mpc), ("qp", vc_qp),
-                ("dyn_mpc", vc_dyn_mpc)]
+                ("dyn_mpc", vc_dyn_mpc), ("obs", vc_obstacles)]
 
 
 class VcError(RuntimeError):
@@ -79,6 +87,7 @@ PROTOTYPES = {
     "vc_last_error": (C.c_char_p, [_vp]),
     "vc_set_stream": (C.c_int, [_vp, _vp]),
     "vc_synchronize": (C.c_int, [_vp]),
+    "vc_set_obstacles": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, C.c_double]),
     "vc_solve": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int]),
     "vc_solve_diag": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int]),
     "vc_solve_debug": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int]),

@@ -65,7 +65,33 @@ def kin_mpc_struct(cfg) -> _abi.vc_kin_mpc:
         w_w=float(cw["w"]), w_a=float(cw["a"]), w_dev=float(cw["deviation"]), w_b=float(cw["boundary"]),
         a_min=float(ic["a_min"]), a_max=float(ic["a_max"]), w_min=float(ic["w_min"]), w_max=float(ic["w_max"]),
         v_min=float(sc["v_min"]), v_max=float(sc["v_max"]), delta_min=float(sc["delta_min"]),
-        delta_max=float(sc["delta_max"]), ey_min=float(sc["ey_min"]), ey_max=float(sc["ey_max"]))
+        delta_max=float(sc["delta_max"]), ey_min=float(sc["ey_min"]), ey_max=float(sc["ey_max"]),
+        w_obs=float(cw.get("obstacles", 0.0)))
+
+
+def obstacles_struct(obstacles=None, margin_min: float = _abi.OBS_MARGIN_MIN) -> _abi.vc_obstacles:
+    """Pack an obstacle list [(s, ey, radius), ...] (the `obstacle_data` rows of the
+    reference's config/environment/*.yaml, read at environment/track.py:131-138).
+    None / [] = no barrier terms (the controller's ``obstacles: False``)."""
+    o = _abi.vc_obstacles()
+    rows = [tuple(float(v) for v in r) for r in (obstacles or [])]
+    if len(rows) > _abi.VC_MAX_OBSTACLES:
+        raise ValueError(f"{len(rows)} obstacles > VC_MAX_OBSTACLES = {_abi.VC_MAX_OBSTACLES}")
+    o.n = len(rows)
+    o.margin_min = float(margin_min)
+    for j, (s, ey, r) in enumerate(rows):
+        o.s[j], o.ey[j], o.radius[j] = s, ey, r
+    return o
+
+
+def obstacle_list(car_or_track, controller_config):
+    """The obstacle rows the barrier terms use: the track's obstacles when the
+    controller config says ``obstacles: True`` (kinematic_mpc.py:130-131,
+    cascaded_mpc.py:173-174 loop over ``car.track.obstacles``), else []."""
+    if not controller_config.get("obstacles", False):
+        return []
+    track = getattr(car_or_track, "track", car_or_track)
+    return [(o.s, o.ey, o.radius) for o in getattr(track, "obstacles", [])]
 
 
 def qp_struct(cfg=None, defaults=None) -> _abi.vc_qp:
@@ -103,13 +129,17 @@ def dyn_mpc_struct(cfg) -> _abi.vc_dyn_mpc:
         w_slip=float(cw["slip"]), w_min=float(ic["w_min"]), w_max=float(ic["w_max"]),
         Ux_min=float(sc["Ux_min"]), max_speed=float(sc["max_speed"]), delta_min=float(sc["delta_min"]),
         delta_max=float(sc["delta_max"]), ey_min=float(sc["ey_min"]), ey_max=float(sc["ey_max"]),
-        fx_scale=float(q["fx_scale"]), trust_Fx=float(q["trust_Fx"]), sqp_iters=int(q["sqp_iters"]))
+        fx_scale=float(q["fx_scale"]), trust_Fx=float(q["trust_Fx"]), sqp_iters=int(q["sqp_iters"]),
+        w_obs=float(cw.get("obstacles", 0.0)))
 
 
-def make_params(kin_car=None, dyn_car=None, kin_mpc=None, dyn_mpc=None, tyre: str = "fiala") -> _abi.vc_params:
+def make_params(kin_car=None, dyn_car=None, kin_mpc=None, dyn_mpc=None, tyre: str = "fiala",
+                obstacles=None) -> _abi.vc_params:
     """Pack whichever configs are given into one ``vc_params`` (others zeroed).
-    The QP knobs come from the controller config given (kinematic or dynamic)."""
+    The QP knobs come from the controller config given (kinematic or dynamic);
+    ``obstacles`` is the [(s, ey, radius), ...] list the barrier terms use."""
     p = _abi.vc_params()
+    p.obs = obstacles_struct(obstacles)
     if kin_car is not None:
         p.kin_car = _abi.vc_kin_car(l=float(kin_car["car"]["l"]))
     if dyn_car is not None:

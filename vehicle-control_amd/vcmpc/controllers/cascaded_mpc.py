@@ -14,14 +14,15 @@ What changes is the solve (cascaded_mpc.py:308, IPOPT + HSL MA27 on the NLP): a 
 number of sequential-QP iterations in one fused fp32 gfx950 kernel (csrc/dyn_sqp.hip;
 contract: oracle/dyn_sqp.py).  ``BatchedSingleTrackMPC`` is the same controller for B
 vehicles at once.  The cascaded point-mass tail (``horizon_pm > 0``,
-cascaded_mpc.py:181-277) and obstacle terms are SURVEY 8(f) rows 3-4 and raise.
+cascaded_mpc.py:181-277) is SURVEY 8(f) row 3 and raises; obstacle barrier terms
+(`obstacles: True`, cascaded_mpc.py:173-176) enter each QP as in DESIGN.md 2c.
 """
 from __future__ import annotations
 
 import numpy as np
 
 from .. import _abi
-from ..config import make_params
+from ..config import make_params, obstacle_list
 from ..solver import Context
 from .controller import Controller
 
@@ -47,8 +48,6 @@ class BatchedSingleTrackMPC(Controller):
         super().__init__()
         if int(config.get("horizon_pm", 0)) > 0:
             raise NotImplementedError("the cascaded point-mass tail (cascaded_mpc.py:181-277) is SURVEY 8(f) row 3")
-        if config.get("obstacles", False):
-            raise NotImplementedError("obstacle barrier terms (cascaded_mpc.py:173-176) are SURVEY 8(f) row 4")
         self.config = config
         self.car = car
         self.N = int(config["horizon"])
@@ -56,7 +55,8 @@ class BatchedSingleTrackMPC(Controller):
         self.ns, self.na = len(car.state), len(car.input)
         self.B = int(batch)
         self.ctx = Context(model=_abi.VC_MODEL_DYNAMIC, N=self.N, max_batch=self.B, dtype=_abi.VC_F32, device=device,
-                           params=make_params(dyn_car=car.config, dyn_mpc=config, tyre=getattr(car, "tyre", "fiala")))
+                           params=make_params(dyn_car=car.config, dyn_mpc=config, tyre=getattr(car, "tyre", "fiala"),
+                                              obstacles=obstacle_list(car, config)))
         # warm starts: cascaded_mpc.py:72-76
         rng = np.random.RandomState(seed) if seed is not None else np.random
         self.state_prediction = np.ones((self.B, self.ns, self.N))

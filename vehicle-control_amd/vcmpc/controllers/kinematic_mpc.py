@@ -17,7 +17,7 @@ from __future__ import annotations
 import numpy as np
 
 from .. import _abi
-from ..config import make_params
+from ..config import make_params, obstacle_list
 from ..solver import Context
 from .controller import Controller
 
@@ -55,14 +55,13 @@ class BatchedKinematicMPC(Controller):
         self.dt = float(config["mpc_dt"])
         self.ns, self.na = len(car.state), len(car.input)
         self.B = int(batch)
-        if config.get("obstacles", False):
-            raise NotImplementedError("obstacle barrier terms (kinematic_mpc.py:130-133) are SURVEY 8(f) row 4")
         qp = dict(RTI_TRUST)
         qp.update(config.get("qp") or {})
         cfg = dict(config)
         cfg["qp"] = qp
         self.ctx = Context(model=_abi.VC_MODEL_KINEMATIC, N=self.N, max_batch=self.B, dtype=_abi.VC_F64,
-                           device=device, params=make_params(kin_car=car.config, kin_mpc=cfg))
+                           device=device, params=make_params(kin_car=car.config, kin_mpc=cfg,
+                                                             obstacles=obstacle_list(car, config)))
         # warm starts: kinematic_mpc.py:64-68 (zeros, v = 0.1; actions 1 + U[0,1) seeded)
         rng = np.random.RandomState(seed) if seed is not None else np.random
         self.state_prediction = np.zeros((self.B, self.ns, self.N + 1))

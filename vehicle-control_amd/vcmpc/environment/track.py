@@ -114,6 +114,17 @@ def centre_line(corners, resolution, smoothing):
     return x, y
 
 
+class Obstacle:
+    """Circular obstacle (environment/track.py:55-70): centre (cx, cy) in world
+    coordinates, (s, ey) in track coordinates, radius in m."""
+
+    def __init__(self, cx, cy, s, ey, radius):
+        self.cx, self.cy, self.s, self.ey, self.radius = cx, cy, s, ey, radius
+
+    def __repr__(self) -> str:
+        return f"Obstacle(cx={self.cx}, cy={self.cy}, radius={self.radius})"
+
+
 class Track:
     def __init__(self, config):
         self.name = config["name"]
@@ -131,6 +142,15 @@ class Track:
         self.s_samples = np.arange(0, self.length - K_TAIL, K_DS)
         self.k_samples = self.get_curvature(self.s_samples)
         self._ck = natural_pieces(self.k_samples, K_DS)
+        self.obstacles = self._construct_obstacles(self.obstacle_data)
+
+    def _construct_obstacles(self, obstacle_data):
+        """track.py:131-138 (the occupancy grid of :140-153 is plotting-only, out of scope)."""
+        out = []
+        for s, ey, radius in obstacle_data:
+            x, y, _ = self.rel2glob(s, ey, 0.0)
+            out.append(Obstacle(float(x), float(y), float(s), float(ey), float(radius)))
+        return out
 
     @classmethod
     def load(cls, name_or_path: str) -> "Track":

@@ -19,7 +19,7 @@ from __future__ import annotations
 import numpy as np
 
 from . import _abi
-from .config import make_params
+from .config import make_params, obstacle_list
 from .solver import Context
 
 IV_KIN, IS_KIN = 0, 2
@@ -44,18 +44,24 @@ class BatchedRacingSimulator:
         cfg = controller_config
         if int(cfg.get("horizon_pm", 0)) > 0:
             raise NotImplementedError("the cascaded point-mass tail (cascaded_mpc.py:181-277) is SURVEY 8(f) row 3")
-        if cfg.get("obstacles", False):
-            raise NotImplementedError("obstacle barrier terms are SURVEY 8(f) row 4")
         self.car, self.config, self.track = car, cfg, track
         self.dynamic = _is_dynamic(car)
         self.B, self.N = int(batch), int(cfg["horizon"])
         self.mpc_dt = float(cfg["mpc_dt"])
         self.dt = float(car.dt)
         if self.dynamic:
-            params = make_params(dyn_car=car.config, dyn_mpc=cfg, tyre=getattr(car, "tyre", "fiala"))
+            params = make_params(dyn_car=car.config, dyn_mpc=cfg, tyre=getattr(car, "tyre", "fiala"),
+                                 obstacles=obstacle_list(track, cfg))
             model, dtype = _abi.VC_MODEL_DYNAMIC, _abi.VC_F32
         else:
-            params = make_params(kin_car=car.config, kin_mpc=cfg)
+            # the kinematic controller's real-time-iteration trust region (controllers/
+            # kinematic_mpc.py RTI_TRUST) unless the config's qp block sets its own
+            from .controllers.kinematic_mpc import RTI_TRUST
+            qp = dict(RTI_TRUST)
+            qp.update(cfg.get("qp") or {})
+            kcfg = dict(cfg)
+            kcfg["qp"] = qp
+            params = make_params(kin_car=car.config, kin_mpc=kcfg, obstacles=obstacle_list(track, cfg))
             model, dtype = _abi.VC_MODEL_KINEMATIC, _abi.VC_F64
         self.ctx = Context(model=model, N=self.N, max_batch=self.B, dtype=dtype, device=device, params=params)
         self.ctx.set_track(track)

@@ -71,6 +71,14 @@ class Context:
         """Run on an external HIP stream (e.g. ``torch.cuda.current_stream().cuda_stream``)."""
         self._check(self.lib.vc_set_stream(self._h, C.c_void_p(stream_handle or 0)))
 
+    def set_obstacles(self, obstacles, margin_min: float = 0.0):
+        """``vc_set_obstacles``: replace the obstacle list [(s, ey, radius), ...] the
+        barrier terms use (Track._construct_obstacles, track.py:131-138); [] = off."""
+        rows = np.asarray([tuple(r) for r in (obstacles or [])], np.float64).reshape(-1, 3)
+        cols = [np.ascontiguousarray(rows[:, i]) for i in range(3)]
+        self._check(self.lib.vc_set_obstacles(self._h, len(rows), *[C.c_void_p(c.ctypes.data) for c in cols],
+                                              float(margin_min)))
+
     def synchronize(self):
         self._check(self.lib.vc_synchronize(self._h))
 
