@@ -250,3 +250,56 @@ def dyn_transition(x, u, kappa, dt, p, tyre="fiala"):
 def dyn_spatial_transition(x, u, kappa, ds, p, tyre="fiala"):
     """``DynamicCar.spatial_transition`` = RK4(spatial ODE, ds) -- dynamic_car.py:188-191."""
     return rk4_step(lambda x_, u_, k_: dyn_spatial_ode(x_, u_, k_, p, tyre), x, u, kappa, ds)
+
+
+# ----------------------------------------------------------------------------
+# dynamic point mass  (models/dynamic_point_mass.py:26-103), the cascaded tail
+# state [V, s, ey, epsi, t] (:147-161), action [Fx, Fy] (:115-126); same car config
+# as the dynamic bicycle (simulation/racing.py:44-46 builds it from carconfig)
+# ----------------------------------------------------------------------------
+PM_NX, PM_NU = 5, 2
+
+
+def pm_temporal_ode(x, u, kappa, p):
+    """dynamic_point_mass.py:76-88 (Fb = 0)."""
+    V, s, ey, epsi, t = np.moveaxis(x, -1, 0)
+    Fx, Fy = u[..., 0], u[..., 1]
+    kappa = np.asarray(kappa)
+    Fd = p["Frr"] + p["Cd"] * V ** 2
+    V_dot = (Fx - Fd) / p["m"]
+    s_dot = (V * np.cos(epsi)) / (1 - kappa * ey)
+    ey_dot = V * np.sin(epsi)
+    epsi_dot = Fy / (p["m"] * V) - kappa * s_dot
+    return np.stack([V_dot, s_dot, ey_dot, epsi_dot, np.ones_like(V)], axis=-1)
+
+
+def pm_spatial_ode(x, u, kappa, p):
+    """dynamic_point_mass.py:90-100: temporal / s_dot, s' = 1."""
+    fd = pm_temporal_ode(x, u, kappa, p)
+    s_dot = fd[..., 1]
+    fp = fd / s_dot[..., None]
+    fp[..., 1] = 1.0
+    fp[..., 4] = 1.0 / s_dot
+    return fp
+
+
+def pm_spatial_transition(x, u, kappa, ds, p):
+    """``DynamicPointMass.spatial_transition`` = Euler(spatial ODE, ds) (:98-100)."""
+    return euler_step(lambda x_, u_, k_: pm_spatial_ode(x_, u_, k_, p), x, u, kappa, ds)
+
+
+def st_to_pm(x):
+    """Switching constraints of the cascaded MPC (cascaded_mpc.py:256-277): the point
+    mass starts at V = |(Ux, Uy)|, s, ey, epsi + atan(Uy / Ux), t of the last
+    single-track state."""
+    Ux, Uy, s, ey, epsi, t = x[..., 0], x[..., 1], x[..., 4], x[..., 5], x[..., 6], x[..., 7]
+    return np.stack([(Ux ** 2 + Uy ** 2) ** 0.5, s, ey, np.arctan(Uy / Ux) + epsi, t], axis=-1)
+
+
+def dyn_lateral_forces(x, u, p, tyre="fiala"):
+    """``DynamicCar.Fy_f`` / ``Fy_r`` (dynamic_car.py:120-142): (Fy_f, Fy_r)."""
+    F = dyn_forces(x, u, p)
+    if tyre == "fiala":
+        return (fiala_lateral_force(F["alpha_f"], p["Caf"], F["Fymax_f"], p["eps"]),
+                fiala_lateral_force(F["alpha_r"], p["Car"], F["Fymax_r"], p["eps"]))
+    return linear_lateral_force(F["alpha_f"], p["Caf"]), linear_lateral_force(F["alpha_r"], p["Car"])

@@ -58,3 +58,24 @@ def dyn_rollout_np(x0, ubar, kappa, ds, p, tyre="linear"):
             k4 = _ode(x + h * k3, u, kk, p, tyre)
             X[:, k + 1] = x + h / 6 * (k1 + 2 * k2 + 2 * k3 + k4)
     return X
+
+
+def pm_rollout_np(xs_last, u_pm, kappa, ds, p):
+    """Point-mass spatial Euler rollout from the switch state of the last single-track
+    state (cascaded_mpc.py:256-277), P[B, M, 5] = (V, s, ey, epsi, t)."""
+    B, M = u_pm.shape[:2]
+    P = np.empty((B, M, 5))
+    Ux, Uy = xs_last[:, 0], xs_last[:, 1]
+    with np.errstate(all="ignore"):
+        P[:, 0] = np.stack([np.hypot(Ux, Uy), xs_last[:, 4], xs_last[:, 5], np.arctan(Uy / Ux) + xs_last[:, 6],
+                            xs_last[:, 7]], 1)
+        for m in range(M - 1):
+            V, s, ey, ep, t = P[:, m].T
+            Fx, Fy = u_pm[:, m].T
+            k = kappa[:, m]
+            sdot = V * np.cos(ep) / (1 - k * ey)
+            f = np.stack([(Fx - p["Frr"] - p["Cd"] * V ** 2) / p["m"], sdot, V * np.sin(ep),
+                          Fy / (p["m"] * V) - k * sdot, np.ones_like(V)], 1) / sdot[:, None]
+            f[:, 1] = 1.0
+            P[:, m + 1] = P[:, m] + ds[:, m:m + 1] * f
+    return P

@@ -127,6 +127,45 @@ def dynamic_batch(B: int, N: int = 40, seed: int = 31, mpc_dt: float = 0.03, tyr
     return {k: np.ascontiguousarray(np.concatenate(v)[:B].astype(np.float32)) for k, v in out.items()}
 
 
+def cascaded_batch(B: int, N: int = 20, M: int = 40, ds_pm: float = 3.0, seed: int = 31, mpc_dt: float = 0.03,
+                   tyre: str = "fiala", car_cfg=None):
+    """Cascaded NMPC workload (single-track N + point-mass M stages), float64, seeded:
+    the single-track part is dynamic_batch's (x0, kappa, ds, ubar over N stages); the
+    point-mass stages get ds = ds_pm, piecewise-constant curvature ~ U(0, 0.047) over
+    4 segments, Fx = the drag at Ux0 + U(-300, 300) N and Fy = m Ux0^2 kappa (the
+    steady-state cornering force) + U(-300, 300) N.  Problems whose warm-start
+    rollout leaves the model's domain (V < 5, |ey| > 4, |epsi| > 0.6) are re-drawn."""
+    from .config import load_config
+    from .host_models import dyn_params, dyn_rollout_np, pm_rollout_np
+    p = dyn_params(car_cfg if car_cfg is not None else load_config("dynamic_car"))
+    rng = np.random.default_rng(seed + 1)
+    out = {k: [] for k in ("x0", "kappa", "ds", "ubar")}
+    have, draw = 0, 0
+    while have < B:
+        m_ = max(2 * (B - have), 16)
+        d = dynamic_batch(m_, N=N, seed=seed + 1000 * draw, mpc_dt=mpc_dt, tyre=tyre, car_cfg=car_cfg)
+        draw += 1
+        d = {k: v.astype(np.float64) for k, v in d.items()}
+        seg = rng.uniform(0, 0.047, (m_, 4))
+        kp = np.repeat(seg, -(-M // 4), axis=1)[:, :M]
+        ux = d["x0"][:, :1]
+        Fx = p["Frr"] + p["Cd"] * ux ** 2 + rng.uniform(-300, 300, (m_, M))
+        Fy = p["m"] * ux ** 2 * kp + rng.uniform(-300, 300, (m_, M))
+        u_pm = np.stack([Fx, Fy], -1)
+        ds_p = np.full((m_, M), ds_pm)
+        X = dyn_rollout_np(d["x0"], d["ubar"], d["kappa"], d["ds"], p, tyre)
+        P = pm_rollout_np(X[:, -1], u_pm, kp, ds_p, p)
+        with np.errstate(invalid="ignore"):
+            ok = np.isfinite(P).all(axis=(1, 2)) & (P[..., 0] > 5).all(1) & (np.abs(P[..., 2]) < 4).all(1)
+            ok &= (np.abs(P[..., 3]) < 0.6).all(1)
+        parts = dict(x0=d["x0"], kappa=np.concatenate([d["kappa"], kp], 1), ds=np.concatenate([d["ds"], ds_p], 1),
+                     ubar=np.concatenate([d["ubar"], u_pm], 1))
+        for k, v in parts.items():
+            out[k].append(v[ok])
+        have += int(ok.sum())
+    return {k: np.ascontiguousarray(np.concatenate(v)[:B]) for k, v in out.items()}
+
+
 # ---- C5: closed-loop Monte-Carlo on a track --------------------------------------------
 C5_MPC_DT = 0.045   # N = 40 stages x 0.045 s = the reference's 1.8 s preview (singletrack.yaml: 60 x 0.03 s)
 
