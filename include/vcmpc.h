@@ -63,7 +63,7 @@ extern "C" {
 
 typedef struct vc_ctx vc_ctx;
 
-enum vc_model { VC_MODEL_KINEMATIC = 0, VC_MODEL_DYNAMIC = 1 };
+enum vc_model { VC_MODEL_KINEMATIC = 0, VC_MODEL_DYNAMIC = 1, VC_MODEL_CASCADED = 2 };
 enum vc_dtype { VC_F64 = 0, VC_F32 = 1 };
 enum vc_flags { VC_HOST_PTRS = 0, VC_DEVICE_PTRS = 1 };
 enum vc_tyre { VC_TYRE_FIALA = 0, VC_TYRE_LINEAR = 1 };
@@ -121,8 +121,19 @@ typedef struct vc_qp {
   int32_t polish;   /* active-set polish rounds after the interior point (0 = off) */
 } vc_qp;
 
+/* Cascaded controller: single-track stages followed by a point-mass tail
+ * (config/controllers/cascaded.yaml, cascaded_mpc.py:181-277).  The single-track part
+ * and the SQP knobs come from vc_dyn_mpc; these are the tail's own settings. */
+typedef struct vc_casc_mpc {
+  int32_t horizon_pm;  /* M point-mass stages (cascaded.yaml horizon_pm) */
+  int32_t pad_;
+  double ds_pm;        /* point-mass stage length [m] (cascaded.yaml ds_pm) */
+  double w_dev_pm, w_Fy, w_switch;       /* cost_weights deviation_pm, Fy, switch_F */
+  double V_min, ey_min_pm, ey_max_pm;    /* state_pm_constraints */
+} vc_casc_mpc;
+
 /* Circular obstacles in track coordinates (Track._construct_obstacles, environment/
- * track.py:131-138, data `obstacle_data: [s, ey, r]` of config/environment/*.yaml).
+ * track.py:131-138, data `obstacle_data: [s, ey, r]` of config/environment/<track>.yaml).
  * n = 0 switches the barrier terms off (the controller's `obstacles: False`).
  * The reference's stage cost w_obs ds / (dist - (r + 0.1)), dist = |(s, ey) - (s_j, ey_j)|
  * (kinematic_mpc.py:130-133, cascaded_mpc.py:173-176) enters each QP as the convexified
@@ -142,6 +153,7 @@ typedef struct vc_params {
   vc_qp qp;         /* trust_a is the kinematic acceleration trust region; trust_w serves both */
   vc_dyn_mpc dyn_mpc;
   vc_obstacles obs;
+  vc_casc_mpc casc;
 } vc_params;
 
 int vc_abi_version(void);
@@ -152,6 +164,8 @@ int vc_params_sizeof(void);
  * up to max_batch problems.  Returns NULL on failure (reason: vc_last_error(NULL)).
  * Built combinations: (VC_MODEL_KINEMATIC, VC_F64, N = 20) for vc_solve /
  * vc_condense; (VC_MODEL_DYNAMIC, VC_F32, N = 40) for vc_solve (sequential QP);
+ * (VC_MODEL_CASCADED, VC_F64, N = 20 single-track stages, casc.horizon_pm = 40) for
+ * vc_solve / vc_condense, whose arrays span H = N + horizon_pm stages;
  * every N >= 1 for vc_rollout / vc_linearize / vc_plant_step / vc_spatial_step. */
 vc_ctx* vc_create(int device, int model, int N, int max_batch, int dtype, const vc_params* params);
 void vc_destroy(vc_ctx* ctx);
@@ -176,6 +190,9 @@ int vc_synchronize(vc_ctx* ctx);
  * Kinematic: one LTV-QP step, NS = N + 1 state columns (kinematic_mpc.py:59-64).
  * Dynamic:   dyn_mpc.sqp_iters QP steps, NS = N columns with dynamics for k < N-1
  *            (cascaded_mpc.py:70,116-122); x* is the rollout of u*.
+ * Cascaded:  dyn_mpc.sqp_iters QP steps over H = N + casc.horizon_pm stages: kappa, ds
+ *            [B][H], ubar [B][H][2] (Fx, w for k < N; Fx, Fy for the point mass), xbar
+ *            [B][H][8] (point-mass states V, s, ey, epsi, t in slots 0..4, 5..7 = 0). 
  * xbar is output only: the prediction is re-rolled from (x0, ubar). */
 int vc_solve(vc_ctx* ctx, int B, const void* x0, const void* kappa, const void* ds,
              void* xbar, void* ubar, void* u0, int32_t* status, int32_t* iters, int flags);
@@ -208,7 +225,9 @@ int vc_rollout(vc_ctx* ctx, int B, const void* x0, const void* ubar, const void*
 int vc_linearize(vc_ctx* ctx, int B, const void* xbar, const void* ubar, const void* kappa,
                  const void* ds, void* A, void* Bm, int flags);
 
-/* Condense: the LTV-QP Hessian H[B][nu*N][nu*N] and gradient g[B][nu*N]. */
+/* Condense: the LTV-QP Hessian H[B][nu*N][nu*N] and gradient g[B][nu*N] (kinematic);
+ * on a cascaded context the first SQP iteration's QP Hessian H[B][2H][2H] and gradient
+ * g[B][2H] in the scaled variable (oracle/casc_sqp.py casc_qp), ubar[B][H][2]. */
 int vc_condense(vc_ctx* ctx, int B, const void* x0, const void* ubar, const void* kappa,
                 const void* ds, void* H, void* g, int flags);
 

@@ -1,0 +1,99 @@
+"""GPU parity of the cascaded (single-track + point-mass) SQP kernel (csrc/casc_sqp.hip,
+fp64, N = 20 + M = 40) through the C ABI, against the fp64 oracle (oracle/casc_sqp.py)
+and its golden vectors (tests/golden/casc_sqp_golden.npz).
+
+Tolerances (fp64 on both sides; scaled decision variable Fx / 1000, w, Fy / 1000):
+first QP's H and g to 1e-9 relative; u* after the 3 SQP iterations < 1e-5 (the north
+star's bar) -- the kernel's interior point stops at mu <= tol = 1e-9, the oracle's QPs
+are solved exactly.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from oracle import casc_sqp as CS
+
+pytestmark = pytest.mark.gpu
+
+U_TOL = 1e-5
+N, M = 20, 40
+
+
+def _scale():
+    s = np.ones((N + M, 2))
+    s[:, 0] = 1000.0
+    s[N:, 1] = 1000.0
+    return s
+
+
+@pytest.fixture(scope="module")
+def golden():
+    return dict(np.load(os.path.join(GOLDEN, "casc_sqp_golden.npz")))
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from vcmpc import Context, _abi
+    from vcmpc.config import load_config, make_params
+    p = make_params(dyn_car=load_config("dynamic_car"), dyn_mpc=load_config("cascaded_mpc"), tyre="fiala")
+    c = Context(model=_abi.VC_MODEL_CASCADED, N=N, max_batch=512, dtype=_abi.VC_F64, params=p)
+    yield c
+    c.close()
+
+
+def test_context_shapes(ctx):
+    assert ctx.NH == N + M and ctx.ns_solve == N + M and ctx.nx == 8
+
+
+def test_first_qp_vs_golden(ctx, golden):
+    g = golden
+    sl = slice(0, 4)
+    H, gv = ctx.condense(g["x0"][sl].copy(), g["ubar"][sl].copy(), g["kappa"][sl].copy(), g["ds"][sl].copy())
+    scale_h = np.abs(g["H0"]).max(axis=(1, 2), keepdims=True)
+    errH = (np.abs(H - g["H0"]) / scale_h).max()
+    errg = (np.abs(gv - g["g0"]) / np.abs(g["g0"]).max(axis=1, keepdims=True)).max()
+    print("first QP: rel |H - H_oracle| %.2e, rel |g - g_oracle| %.2e" % (errH, errg))
+    assert errH < 1e-9 and errg < 1e-9
+
+
+def test_solve_vs_golden(ctx, golden):
+    g = golden
+    ub = g["ubar"].copy()
+    u0, xs, us, st, it, dg = ctx.solve(g["x0"].copy(), g["kappa"].copy(), g["ds"].copy(), ub, diag=True)
+    err = np.abs((us - g["u_star"]) / _scale()).max(axis=(1, 2))
+    print("scaled |u* - u*_oracle| per problem:", np.array2string(err, precision=1))
+    print("status", st, "iters", it, "diag flags", dg[:, 2])
+    assert (st == 0).all(), st
+    assert err.max() < U_TOL
+    np.testing.assert_allclose(u0, us[:, 0])
+    assert np.abs(xs - g["x_star"]).max() < 1e-3
+    assert (it > 0).all()
+
+
+def test_solve_fresh_vs_oracle(ctx, dyn_params):
+    from vcmpc.config import load_config
+    from vcmpc.workload import cascaded_batch
+    W = CS.casc_weights(load_config("cascaded_mpc"))
+    d = cascaded_batch(3, seed=123)
+    ref = CS.casc_sqp_solve(d["x0"], d["ubar"], d["kappa"], d["ds"], dyn_params, W, tyre="fiala")
+    u0, xs, us, st, it = ctx.solve(d["x0"], d["kappa"], d["ds"], d["ubar"].copy())
+    assert (st == 0).all()
+    assert np.abs((us - ref["u_star"]) / _scale()).max() < U_TOL
+
+
+def test_batch_properties_and_device_pointers(ctx):
+    import torch
+    from vcmpc.workload import cascaded_batch
+    d = cascaded_batch(256, seed=9)
+    out = ctx.solve(d["x0"], d["kappa"], d["ds"], d["ubar"].copy())
+    u0, xs, us, st, it = out
+    assert (st == 0).mean() >= 0.98, (st != 0).sum()
+    assert np.isfinite(us).all() and np.isfinite(xs).all()
+    assert (np.abs(us[:, :N, 1]) <= 0.4 + 1e-9).all()
+    dev = {k: torch.from_numpy(v.copy()).to("cuda:0") for k, v in d.items()}
+    r = ctx.solve(dev["x0"], dev["kappa"], dev["ds"], dev["ubar"])
+    ctx.synchronize()
+    np.testing.assert_array_equal(r[2].cpu().numpy(), us)
+    np.testing.assert_array_equal(r[3].cpu().numpy(), st)

@@ -1,0 +1,919 @@
+// casc_sqp.hip -- fused cascaded (single-track + point-mass) SQP step, fp64, one
+// 256-thread workgroup per problem.
+//
+// Replaces the IPOPT solve of CascadedMPC with horizon_pm > 0
+// (controllers/mpc/cascaded_mpc.py:17-39,91-304, config/controllers/cascaded.yaml: N = 20
+// single-track stages, M = 40 point-mass stages every ds_pm = 3 m).  Contract:
+// oracle/casc_sqp.py.  Per SQP iteration:
+//   predict    thread 0: single-track RK4 (vc_models.hpp dyn_spatial_ode), switching map
+//              st_to_pm, point-mass Euler (pm_spatial_ode)
+//   linearize  one thread per (stage, seed): Dual<1, double> evaluation of the same step
+//              code gives one column of [A B]; the switch Jacobian analytically; the
+//              switching cost's lateral residual Fy_f + Fy_r and its gradient by duals
+//   condense   one thread per decision column j: the column's sensitivity is carried
+//              through the stages and the rows the QP reads are stored in LDS, triangular
+//              (single-track stage k: Ux, Uy, r, delta, ey over columns < 2k; point-mass
+//              stage j: V, ey over columns < 2j; terminal epsi, t; the lateral row)
+//   QP         every cost and constraint term is local to a stage's vector
+//              v_k = (Ux, Uy, r, delta | V, ey, dFx, dw | dFy) = V_k dz, plus input slews,
+//              the switching residuals and the terminal epsi row.  Four lanes per stage
+//              hold its 12 one-sided rows (3 each); the normal matrix
+//                  M = P + sum_k V_k' (Q_k + C_k' D_k C_k) V_k
+//              is accumulated in LDS (packed lower triangle), factorised by a
+//              right-looking Cholesky (2 barriers per column), and each Mehrotra
+//              predictor / corrector solve is two single-wave triangular sweeps.
+//   update     ubar += dz (scaled back: Fx and the point mass's Fy by fx_scale)
+// LDS: packed normal matrix 58 KB (aliased by the linearisation scratch before the QP),
+// condensed rows 68 KB, stage blocks 13 KB, trajectory and vectors 18 KB.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "vc_dual.hpp"
+#include "vc_kernels.hpp"
+
+namespace vc {
+namespace {
+
+constexpr int CTH = 256;
+
+template <int N, int M>
+struct CL {
+  static constexpr int H = N + M, n = 2 * H, NP = n * (n + 1) / 2;
+  static constexpr int P0 = 5 * N * (N - 1);                          // first point-mass row
+  static constexpr int T0 = P0 + 4 * (M * N + M * (M - 1) / 2);       // terminal epsi, t rows
+  static constexpr int SW0 = T0 + 4 * (H - 1);                        // switch lateral row
+  static constexpr int NG = SW0 + 2 * N + 2;
+  // single-track stage k (1..N-1): rows (Ux, Uy, r, delta, ey), each of length 2k
+  __device__ static constexpr int gst(int k) { return 5 * k * (k - 1); }
+  // point-mass stage m (global stage N + m): rows (V, ey), each of length 2(N + m)
+  __device__ static constexpr int gpm(int m) { return P0 + 4 * (m * N + m * (m - 1) / 2); }
+  // packed lower triangle, column-major: (i >= j)
+  __device__ static constexpr int pidx(int i, int j) { return j * n - (j * (j - 1)) / 2 + (i - j); }
+};
+
+template <int N, int M>
+struct CascSmem {
+  using L = CL<N, M>;
+  union {
+    double Mp[L::NP];
+    struct {
+      double As[N - 1][8][10];  // [A B] of the single-track RK4 steps
+      double Ap[M - 1][5][7];   // [A B] of the point-mass Euler steps
+      double Sw[5][8];          // switching map Jacobian
+    } lin;
+  } u;
+  double G[L::NG];
+  double W[L::H][28];           // stage normal blocks, packed symmetric 7x7
+  double xs[N][8];
+  double xp[M][5];
+  double ub[L::H][2];
+  double kap[L::H], dsv[L::H];
+  double z[L::n], dz[L::n], rhs[L::n], gp[L::n], invd[L::n];
+  double Y[L::H][8], R[L::H][8];
+  double ex[4];                 // a_sw . x, g_epsi . x (extra dense rows)
+  double sc[8];                 // lateral residual value + gradient (Ux, Uy, r, delta, Fx)
+  double red[8];
+  int flag[4];
+};
+
+__device__ __forceinline__ int sym7(int a, int b) {  // a <= b
+  return a * 7 - (a * (a - 1)) / 2 + (b - a);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ double wave_min(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+  return v;
+}
+template <int OP>  // 0 sum, 1 max, 2 min
+__device__ __forceinline__ double block_reduce(double v, double* red) {
+  v = OP == 0 ? wave_sum(v) : (OP == 1 ? wave_max(v) : wave_min(v));
+  const int t = threadIdx.x;
+  __syncthreads();
+  if ((t & 63) == 0) red[t >> 6] = v;
+  __syncthreads();
+  const double a = red[0], b = red[1], c = red[2], d = red[3];
+  return OP == 0 ? (a + b) + (c + d) : (OP == 1 ? fmax(fmax(a, b), fmax(c, d)) : fmin(fmin(a, b), fmin(c, d)));
+}
+
+// one-sided constraint rows of a stage: coefficients over the stage vector, rhs, activity
+struct Rows3 {
+  double c[3][7];
+  double d[3];
+  double act[3];
+};
+
+template <int N, int M, int TYRE>
+__global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
+  using L = CL<N, M>;
+  constexpr int H = L::H, n = L::n;
+  __shared__ CascSmem<N, M> s;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int b = blockIdx.x;
+  DynCoef<double> c = A.car;
+  c.tyre = TYRE;
+  const vc_dyn_mpc& W = A.w;
+  const vc_casc_mpc& CW = A.cw;
+  const double S = W.fx_scale;
+  using D1 = Dual<1, double>;
+  using D2 = Dual<2, double>;
+
+  for (int i = t; i < H; i += CTH) {
+    s.kap[i] = A.kappa[(size_t)b * H + i];
+    s.dsv[i] = A.ds[(size_t)b * H + i];
+    s.ub[i][0] = A.ubar[((size_t)b * H + i) * 2];
+    s.ub[i][1] = A.ubar[((size_t)b * H + i) * 2 + 1];
+  }
+  if (t < 8) s.xs[0][t] = A.x0[(size_t)b * 8 + t];
+  if (t == 0) {
+    s.flag[0] = VC_SOLVED;
+    s.flag[1] = 0;  // interior-point iterations, summed
+    s.flag[2] = 2;  // diag flags: 2 = every QP converged
+  }
+  __syncthreads();
+
+  auto predict = [&]() {
+    if (t == 0) {
+      double x[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) x[i] = s.xs[0][i];
+      bool fin = true;
+      for (int k = 0; k < N - 1; ++k) {
+        const double u2[2] = {s.ub[k][0], s.ub[k][1]};
+        const double kp = s.kap[k];
+        double xn[8];
+        rk4_apply<double, 8>(x, s.dsv[k], [&](const double* xx, double* f) { dyn_spatial_ode<double, double>(xx, u2, kp, c, f); }, xn);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          x[i] = xn[i];
+          s.xs[k + 1][i] = xn[i];
+          fin = fin && isfinite(xn[i]);
+        }
+      }
+      double p[5];
+      st_to_pm<double>(x, p);
+#pragma unroll
+      for (int i = 0; i < 5; ++i) s.xp[0][i] = p[i];
+      for (int m = 0; m < M - 1; ++m) {
+        const int j = N + m;
+        const double u2[2] = {s.ub[j][0], s.ub[j][1]};
+        double f[5];
+        pm_spatial_ode<double, double>(p, u2, s.kap[j], c, f);
+        const double h = s.dsv[j];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+          p[i] = p[i] + h * f[i];
+          s.xp[m + 1][i] = p[i];
+          fin = fin && isfinite(p[i]);
+        }
+      }
+      if (!fin) s.flag[0] = VC_NONFINITE;
+    }
+  };
+
+  // stage vector V_k[:, col] (slots 0..6)
+  auto vcol = [&](int k, int col, double* v) {
+    if (k < N) {
+      const int len = 2 * k, base = L::gst(k);
+      const bool in = col < len;
+#pragma unroll
+      for (int r = 0; r < 5; ++r) v[r] = in ? s.G[base + r * len + (in ? col : 0)] : 0.0;
+    } else {
+      const int m = k - N, len = 2 * k, base = L::gpm(m);
+      const bool in = col < len;
+      v[0] = in ? s.G[base + (in ? col : 0)] : 0.0;
+      v[1] = v[2] = v[3] = 0.0;
+      v[4] = in ? s.G[base + len + (in ? col : 0)] : 0.0;
+    }
+    v[5] = col == 2 * k ? 1.0 : 0.0;
+    v[6] = col == 2 * k + 1 ? 1.0 : 0.0;
+  };
+
+  // Y_k = V_k x for every stage, and the extra dense rows' dots (ex[0] a_sw.x, ex[1] g_epsi.x)
+  auto stage_local = [&](const double* x) {
+    if (t < 5 * (N - 1)) {
+      const int k = 1 + t / 5, r = t % 5, len = 2 * k;
+      const double* g = &s.G[L::gst(k) + r * len];
+      double acc = 0.0;
+      for (int j = 0; j < len; ++j) acc += g[j] * x[j];
+      s.Y[k][r] = acc;
+    } else if (t < 5 * (N - 1) + 2 * M) {
+      const int q = t - 5 * (N - 1), m = q >> 1, r = q & 1, len = 2 * (N + m);
+      const double* g = &s.G[L::gpm(m) + r * len];
+      double acc = 0.0;
+      for (int j = 0; j < len; ++j) acc += g[j] * x[j];
+      s.Y[N + m][r ? 4 : 0] = acc;
+    } else if (t < 5 * (N - 1) + 2 * M + 2) {
+      const int q = t - 5 * (N - 1) - 2 * M;
+      const int len = q == 0 ? 2 * N + 2 : 2 * (H - 1);
+      const double* g = &s.G[q == 0 ? L::SW0 : L::T0];
+      double acc = 0.0;
+      for (int j = 0; j < len; ++j) acc += g[j] * x[j];
+      s.ex[q] = acc;
+    }
+    if (t >= CTH - H) {  // inputs and structural zeros
+      const int k = t - (CTH - H);
+      s.Y[k][5] = x[2 * k];
+      s.Y[k][6] = x[2 * k + 1];
+      if (k == 0) {
+#pragma unroll
+        for (int r = 0; r < 5; ++r) s.Y[0][r] = 0.0;
+      }
+      if (k >= N) s.Y[k][1] = s.Y[k][2] = s.Y[k][3] = 0.0;
+    }
+    __syncthreads();
+  };
+
+  // out_j = sum_k V_k[:, j]' R_k  (thread j < n)
+  auto adjoint = [&](int j) -> double {
+    const int kj = j >> 1;
+    double acc = s.R[kj][5 + (j & 1)];
+    if (kj < N) {
+      for (int k = kj + 1; k < N; ++k) {
+        const int len = 2 * k, base = L::gst(k) + j;
+#pragma unroll
+        for (int r = 0; r < 5; ++r) acc += s.G[base + r * len] * s.R[k][r];
+      }
+    }
+    for (int m = (kj < N ? 0 : kj - N + 1); m < M; ++m) {
+      const int len = 2 * (N + m), base = L::gpm(m) + j;
+      acc += s.G[base] * s.R[N + m][0] + s.G[base + len] * s.R[N + m][4];
+    }
+    return acc;
+  };
+
+  // slew pairs between columns a and a + 2: weight c2 (H entries) for the pair starting at a
+  auto pair_w = [&](int a) -> double {  // 2 * w / ds * S^2, 0 if no pair
+    const int k = a >> 1, cc = a & 1;
+    if (k > H - 2) return 0.0;
+    double w;
+    if (cc == 0) w = (k == N - 1 ? CW.w_switch : W.w_Fx) / s.dsv[k];
+    else if (k >= N) w = CW.w_Fy / s.dsv[k];
+    else return 0.0;
+    return 2.0 * w * S * S;
+  };
+
+  int sqp_done = 0;
+  for (int it = 0; it < W.sqp_iters; ++it) {
+    predict();
+    __syncthreads();
+    if (s.flag[0] == VC_NONFINITE) break;
+
+    // ---------------- linearize ----------------
+    if (t < (N - 1) * 10) {
+      const int k = t / 10, q = t % 10;
+      D1 x[8], u2[2], xn[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) x[i] = D1(s.xs[k][i]);
+      u2[0] = D1(s.ub[k][0]);
+      u2[1] = D1(s.ub[k][1]);
+      if (q < 8) x[q].d[0] = 1.0;
+      else u2[q - 8].d[0] = 1.0;
+      const D1 kp(s.kap[k]);
+      rk4_apply<D1, 8>(x, D1(s.dsv[k]), [&](const D1* xx, D1* f) { dyn_spatial_ode<D1, double>(xx, u2, kp, c, f); }, xn);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s.u.lin.As[k][i][q] = xn[i].d[0];
+    }
+    for (int t2 = t; t2 < (M - 1) * 7; t2 += CTH) {
+      const int m = t2 / 7, q = t2 % 7, j = N + m;
+      D1 x[5], u2[2], f[5];
+#pragma unroll
+      for (int i = 0; i < 5; ++i) x[i] = D1(s.xp[m][i]);
+      u2[0] = D1(s.ub[j][0]);
+      u2[1] = D1(s.ub[j][1]);
+      if (q < 5) x[q].d[0] = 1.0;
+      else u2[q - 5].d[0] = 1.0;
+      pm_spatial_ode<D1, double>(x, u2, D1(s.kap[j]), c, f);
+      const double h = s.dsv[j];
+#pragma unroll
+      for (int i = 0; i < 5; ++i) s.u.lin.Ap[m][i][q] = x[i].d[0] + h * f[i].d[0];
+    }
+    if (t == CTH - 1) {  // switching map Jacobian (cascaded_mpc.py:256-277)
+      const double Ux = s.xs[N - 1][0], Uy = s.xs[N - 1][1];
+      const double V = sqrt(Ux * Ux + Uy * Uy), q2 = Ux * Ux + Uy * Uy;
+#pragma unroll
+      for (int r = 0; r < 5; ++r)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s.u.lin.Sw[r][i] = 0.0;
+      s.u.lin.Sw[0][0] = Ux / V;
+      s.u.lin.Sw[0][1] = Uy / V;
+      s.u.lin.Sw[1][4] = 1.0;
+      s.u.lin.Sw[2][5] = 1.0;
+      s.u.lin.Sw[3][0] = -Uy / q2;
+      s.u.lin.Sw[3][1] = Ux / q2;
+      s.u.lin.Sw[3][6] = 1.0;
+      s.u.lin.Sw[4][7] = 1.0;
+    }
+    if (t >= CTH - 6 && t < CTH - 1) {  // lateral residual Fy_f + Fy_r at stage N-1 (cascaded_mpc.py:250-255)
+      const int q = t - (CTH - 6);
+      D1 X5[5];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) X5[i] = D1(s.xs[N - 1][i]);
+      X5[4] = D1(s.ub[N - 1][0]);
+      X5[q].d[0] = 1.0;
+      const D1 fy = dyn_lateral_sum<D1, double>(X5, c);
+      s.sc[1 + q] = fy.d[0];
+      if (q == 0) s.sc[0] = fy.v;
+    }
+    __syncthreads();
+
+    // ---------------- condense (thread j = decision column) ----------------
+    if (t < n) {
+      const int j = t, kj = j >> 1, cj = j & 1;
+      double c8[8], c5[5];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) c8[i] = 0.0;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) c5[i] = 0.0;
+      int m0;
+      if (kj < N) {
+        const double scl = cj ? 1.0 : S;
+        if (kj < N - 1) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) c8[i] = scl * s.u.lin.As[kj][i][8 + cj];
+        }
+        for (int k = kj + 1; k < N; ++k) {
+          const int len = 2 * k, base = L::gst(k) + j;
+          s.G[base] = c8[0];
+          s.G[base + len] = c8[1];
+          s.G[base + 2 * len] = c8[2];
+          s.G[base + 3 * len] = c8[3];
+          s.G[base + 4 * len] = c8[5];
+          if (k < N - 1) {
+            double nx[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+              double a = 0.0;
+#pragma unroll
+              for (int q = 0; q < 8; ++q) a += s.u.lin.As[k][i][q] * c8[q];
+              nx[i] = a;
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) c8[i] = nx[i];
+          }
+        }
+        // switching cost's lateral row (the sensitivity at stage N-1 is c8 now)
+        double a = -(s.sc[1] * c8[0] + s.sc[2] * c8[1] + s.sc[3] * c8[2] + s.sc[4] * c8[3]);
+        if (j == 2 * (N - 1)) a -= s.sc[5] * S;
+        s.G[L::SW0 + j] = a;
+#pragma unroll
+        for (int r = 0; r < 5; ++r) {
+          double v = 0.0;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v += s.u.lin.Sw[r][q] * c8[q];
+          c5[r] = v;
+        }
+        m0 = 0;
+      } else {
+        const int mj = kj - N;
+        if (mj < M - 1) {
+#pragma unroll
+          for (int i = 0; i < 5; ++i) c5[i] = S * s.u.lin.Ap[mj][i][5 + cj];
+        }
+        if (j < 2 * N + 2) s.G[L::SW0 + j] = (j == 2 * N + 1) ? S : 0.0;
+        m0 = mj + 1;
+      }
+      for (int m = m0; m < M; ++m) {
+        const int len = 2 * (N + m), base = L::gpm(m) + j;
+        s.G[base] = c5[0];
+        s.G[base + len] = c5[2];
+        if (m < M - 1) {
+          double nx[5];
+#pragma unroll
+          for (int i = 0; i < 5; ++i) {
+            double a = 0.0;
+#pragma unroll
+            for (int q = 0; q < 5; ++q) a += s.u.lin.Ap[m][i][q] * c5[q];
+            nx[i] = a;
+          }
+#pragma unroll
+          for (int i = 0; i < 5; ++i) c5[i] = nx[i];
+        }
+      }
+      if (j < 2 * (H - 1)) {
+        s.G[L::T0 + j] = c5[3];
+        s.G[L::T0 + 2 * (H - 1) + j] = c5[4];
+      }
+    }
+    __syncthreads();
+
+    // ---------------- QP setup ----------------
+    // rows and stage costs: 4 lanes per stage k = t / 4 (t < 4H), lane q = t % 4
+    Rows3 R3;
+    double Qp[28], qv[7];
+    const bool stl = t < 4 * H;
+    const int k = stl ? (t >> 2) : 0, q = t & 3;
+#pragma unroll
+    for (int e = 0; e < 28; ++e) Qp[e] = 0.0;
+#pragma unroll
+    for (int e = 0; e < 7; ++e) qv[e] = 0.0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      R3.d[i] = 1.0;
+      R3.act[i] = 0.0;
+#pragma unroll
+      for (int e = 0; e < 7; ++e) R3.c[i][e] = 0.0;
+    }
+    {
+      // obstacle barrier (cascaded_mpc.py:173-176, 233-237), convexified in ey
+      auto ey_cost = [&](double ey, double sv, double ds, double lo, double hi, double wdev) {
+        const double blo = ey < lo ? W.w_b : 0.0, bhi = ey > hi ? W.w_b : 0.0;
+        double qo = 0.0, po = 0.0;
+        if (A.obs.n > 0) obstacle_ey_model<double>(A.obs, sv, ey, W.w_obs * ds, po, qo);
+        Qp[sym7(4, 4)] += 2.0 * ds * (wdev + blo + bhi) + qo;
+        qv[4] += 2.0 * ds * (wdev * ey + blo * (ey - lo) + bhi * (ey - hi)) + po;
+      };
+      if (k < N) {
+        // stage functions with duals: d[0] along this lane's state (Ux, Uy, r, delta), d[1] along Fx
+        D2 X5[5];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) X5[i] = D2(s.xs[k][i]);
+        X5[4] = D2(s.ub[k][0]);
+        X5[q].d[0] = 1.0;
+        X5[4].d[1] = 1.0;
+        D2 o[7];
+        dyn_stage_terms<D2, double>(X5, c, o);
+        double fv[7], gr[7][5];
+        const int qb = lane & ~3;
+#pragma unroll
+        for (int r = 0; r < 7; ++r) {
+          fv[r] = o[r].v;
+#pragma unroll
+          for (int a = 0; a < 4; ++a) gr[r][a] = __shfl(o[r].d[0], qb | a, 64);
+          gr[r][4] = o[r].d[1];
+        }
+        const double ds = s.dsv[k];
+        if (q == 0 && stl) {
+          // Gauss-Newton cost (cascaded_mpc.py:130-171)
+          ey_cost(s.xs[k][5], s.xs[k][4], ds, W.ey_min, W.ey_max, W.w_dev);
+          Qp[sym7(6, 6)] += 2.0 * W.w_w;
+          qv[6] += 2.0 * W.w_w * s.ub[k][1];
+#pragma unroll
+          for (int sr = 0; sr < 2; ++sr) {
+            if (fv[sr] >= 0.0) {
+              const double a7[7] = {gr[sr][0], gr[sr][1], gr[sr][2], gr[sr][3], 0.0, gr[sr][4] * S, 0.0};
+#pragma unroll
+              for (int a = 0; a < 7; ++a) {
+                qv[a] += 2.0 * W.w_slip * fv[sr] * a7[a];
+#pragma unroll
+                for (int e = a; e < 7; ++e) Qp[sym7(a, e)] += 2.0 * W.w_slip * a7[a] * a7[e];
+              }
+            }
+          }
+        }
+        // rows (slot 3q + i)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const int sl = 3 * q + i;
+          double* cr = R3.c[i];
+          double d = 1.0, act = 1.0;
+          if (sl == 0) { cr[0] = -1.0; d = s.xs[k][0] - W.Ux_min; act = k >= 1; }
+          else if (sl == 1) { cr[3] = 1.0; d = W.delta_max - s.xs[k][3]; act = k >= 1; }
+          else if (sl == 2) { cr[3] = -1.0; d = s.xs[k][3] - W.delta_min; act = k >= 1; }
+          else if (sl <= 7) {
+            const int r = sl - 1;  // stage functions 2..6: peng, tyre f up / lo, r up / lo
+#pragma unroll
+            for (int rr = 2; rr < 7; ++rr) {
+              if (rr == r) {
+                cr[0] = gr[rr][0] / S; cr[1] = gr[rr][1] / S; cr[2] = gr[rr][2] / S; cr[3] = gr[rr][3] / S;
+                cr[5] = gr[rr][4];
+                d = -fv[rr] / S;
+              }
+            }
+          } else if (sl == 8) {
+            cr[6] = 1.0;
+            d = W.w_max - s.ub[k][1];
+            if (A.qp.trust_w > 0) d = fmin(d, A.qp.trust_w);
+          } else if (sl == 9) {
+            cr[6] = -1.0;
+            d = s.ub[k][1] - W.w_min;
+            if (A.qp.trust_w > 0) d = fmin(d, A.qp.trust_w);
+          } else {
+            cr[5] = sl == 10 ? 1.0 : -1.0;
+            d = W.trust_Fx / S;
+            act = W.trust_Fx > 0;
+          }
+          R3.d[i] = d;
+          R3.act[i] = stl ? act : 0.0;
+          if (!(act > 0)) {
+#pragma unroll
+            for (int e = 0; e < 7; ++e) cr[e] = 0.0;
+            R3.d[i] = 1.0;
+          }
+        }
+      } else {
+        const int m = k - N;
+        const double V = s.xp[m][0];
+        if (q == 0 && stl) {
+          // point-mass stage cost (cascaded_mpc.py:204-239) and the terminal cost (:279-304)
+          ey_cost(s.xp[m][2], s.xp[m][1], s.dsv[k], CW.ey_min_pm, CW.ey_max_pm, CW.w_dev_pm);
+          if (m == M - 1) {
+            if (V >= W.max_speed) {
+              Qp[sym7(0, 0)] += 2.0 * W.w_speed;
+              qv[0] += 2.0 * W.w_speed * (V - W.max_speed);
+            }
+            Qp[sym7(4, 4)] += 2.0 * W.w_ey;
+            qv[4] += 2.0 * W.w_ey * s.xp[m][2];
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const int sl = 3 * q + i;
+          double* cr = R3.c[i];
+          double d = 1.0, act = 1.0;
+          if (sl == 0) { cr[0] = -1.0; d = V - CW.V_min; }
+          else if (sl == 1) {  // Fx <= Peng / V (cascaded_mpc.py:193), divided by S
+            cr[0] = c.Peng / (V * V) / S;
+            cr[5] = 1.0;
+            d = -(s.ub[k][0] - c.Peng / V) / S;
+          } else if (sl <= 5) {
+            cr[sl <= 3 ? 5 : 6] = (sl & 1) ? -1.0 : 1.0;
+            d = W.trust_Fx / S;
+            act = W.trust_Fx > 0;
+          } else {
+            act = 0.0;
+          }
+          R3.d[i] = d;
+          R3.act[i] = stl ? act : 0.0;
+          if (!(act > 0)) {
+#pragma unroll
+            for (int e = 0; e < 7; ++e) cr[e] = 0.0;
+            R3.d[i] = 1.0;
+          }
+        }
+      }
+    }
+    // constant gradient part gp (slews, switching residuals, terminal epsi and time)
+    const double csw = CW.w_switch / s.dsv[N - 1];
+    const double r_lat = s.ub[N][1] - s.sc[0];
+    const double ep_end = s.xp[M - 1][3];
+    if (t < n) {
+      const int j = t;
+      double g = 0.0;
+      auto lin = [&](int a) -> double {  // 2 w r0 S of the pair starting at column a
+        const double c2 = pair_w(a);
+        return c2 == 0.0 ? 0.0 : c2 / S * (s.ub[(a >> 1) + 1][a & 1] - s.ub[a >> 1][a & 1]);
+      };
+      if (j >= 2) g += lin(j - 2);
+      g -= lin(j);
+      if (j < 2 * N + 2) g += 2.0 * csw * r_lat * s.G[L::SW0 + j];
+      if (j < 2 * (H - 1)) {
+        g += 2.0 * W.w_epsi * ep_end * s.G[L::T0 + j];
+        g += W.w_time * s.G[L::T0 + 2 * (H - 1) + j];
+      }
+      s.gp[j] = g;
+      s.z[j] = 0.0;
+    }
+    // P x (prox, slews, switching lateral and terminal epsi rank-1 terms); ex[] must hold the dots
+    auto px = [&](const double* x, int j) -> double {
+      double v = 2.0 * A.qp.prox * x[j];
+      const double cf = pair_w(j);
+      if (cf != 0.0) v += cf * (x[j] - x[j + 2]);
+      if (j >= 2) {
+        const double cb = pair_w(j - 2);
+        if (cb != 0.0) v += cb * (x[j] - x[j - 2]);
+      }
+      if (j < 2 * N + 2) v += 2.0 * csw * s.G[L::SW0 + j] * s.ex[0];
+      if (j < 2 * (H - 1)) v += 2.0 * W.w_epsi * s.G[L::T0 + j] * s.ex[1];
+      return v;
+    };
+    // normal matrix: M = P + sum_k V_k' W_k V_k (W_k in s.W)
+    auto build = [&]() {
+      for (int j = wave; j < n; j += 4) {
+        const double aj = j < 2 * N + 2 ? s.G[L::SW0 + j] : 0.0;
+        const double ej = j < 2 * (H - 1) ? s.G[L::T0 + j] : 0.0;
+        const double cj = pair_w(j), cb = j >= 2 ? pair_w(j - 2) : 0.0;
+        for (int i = j + lane; i < n; i += 64) {
+          double v = 0.0;
+          if (i < 2 * N + 2) v += 2.0 * csw * s.G[L::SW0 + i] * aj;
+          if (i < 2 * (H - 1)) v += 2.0 * W.w_epsi * s.G[L::T0 + i] * ej;
+          if (i == j) v += 2.0 * A.qp.prox + cj + cb;
+          if (i == j + 2) v -= cj;
+          s.u.Mp[L::pidx(i, j)] = v;
+        }
+      }
+      __syncthreads();
+      if (t < 4 * (n / 2)) {
+        const int p = t >> 2, sub = t & 3;
+#pragma unroll 1
+        for (int pass = 0; pass < 2; ++pass) {
+          const int j = pass == 0 ? p : n - 1 - p;
+          const int kj = j >> 1;
+#pragma unroll 1
+          for (int kk = kj; kk < H; ++kk) {
+            double vj[7], hv[7];
+            vcol(kk, j, vj);
+            const double* Wk = s.W[kk];
+#pragma unroll
+            for (int a = 0; a < 7; ++a) {
+              double acc = 0.0;
+#pragma unroll
+              for (int e = 0; e < 7; ++e) acc += Wk[a <= e ? sym7(a, e) : sym7(e, a)] * vj[e];
+              hv[a] = acc;
+            }
+            const int iend = 2 * kk + 2;
+#pragma unroll 1
+            for (int i = j + sub; i < iend; i += 4) {
+              double vi[7];
+              vcol(kk, i, vi);
+              double acc = 0.0;
+#pragma unroll
+              for (int a = 0; a < 7; ++a) acc += vi[a] * hv[a];
+              s.u.Mp[L::pidx(i, j)] += acc;
+            }
+          }
+        }
+      }
+      __syncthreads();
+    };
+
+    if (A.mode == 1) {  // first QP's H and g (vc_condense)
+      if (stl && q == 0) {
+#pragma unroll
+        for (int e = 0; e < 28; ++e) s.W[k][e] = Qp[e];
+#pragma unroll
+        for (int e = 0; e < 7; ++e) s.R[k][e] = qv[e];
+      }
+      __syncthreads();
+      build();
+      for (int e = t; e < n * n; e += CTH) {
+        const int i = e / n, j = e % n;
+        A.H_out[(size_t)b * n * n + e] = s.u.Mp[i >= j ? L::pidx(i, j) : L::pidx(j, i)];
+      }
+      if (t < n) A.g_out[(size_t)b * n + t] = adjoint(t) + s.gp[t];
+      return;
+    }
+
+    // ---------------- interior point (Mehrotra predictor-corrector) ----------------
+    double sl3[3], lm3[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      sl3[i] = R3.act[i] > 0 ? fmax(R3.d[i], 0.0) + 1.0 : 1.0;
+      lm3[i] = R3.act[i] > 0 ? 1.0 : 0.0;
+    }
+    const double m_act = block_reduce<0>(R3.act[0] + R3.act[1] + R3.act[2], s.red);
+    int ipm_it = 0;
+    bool conv = false, fail = false;
+    __syncthreads();
+    for (ipm_it = 0; ipm_it < A.qp.max_iter; ++ipm_it) {
+      stage_local(s.z);
+      double pxj = 0.0;
+      if (t < n) pxj = px(s.z, t);
+      double Yk[7];
+#pragma unroll
+      for (int e = 0; e < 7; ++e) Yk[e] = s.Y[k][e];
+      double qy[7];
+#pragma unroll
+      for (int a = 0; a < 7; ++a) {
+        double acc = qv[a];
+#pragma unroll
+        for (int e = 0; e < 7; ++e) acc += Qp[a <= e ? sym7(a, e) : sym7(e, a)] * Yk[e];
+        qy[a] = acc;
+      }
+      double rp3[3], Dg3[3];
+      double smu = 0.0, rpm = 0.0;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        double cy = 0.0;
+#pragma unroll
+        for (int e = 0; e < 7; ++e) cy += R3.c[i][e] * Yk[e];
+        rp3[i] = R3.act[i] > 0 ? cy + sl3[i] - R3.d[i] : 0.0;
+        Dg3[i] = R3.act[i] > 0 ? lm3[i] / sl3[i] : 0.0;
+        smu += R3.act[i] * sl3[i] * lm3[i];
+        rpm = fmax(rpm, fabs(rp3[i]));
+      }
+      const double mu = block_reduce<0>(smu, s.red) / fmax(m_act, 1.0);
+      const double rp_inf = block_reduce<1>(rpm, s.red);
+      // dual residual r_d = H z + g + C' lambda
+      auto stage_vec = [&](const double* wv) {  // R_k = Q_k Y_k + q_k + sum_i wv_i c_i (quad-reduced)
+        double v[7];
+#pragma unroll
+        for (int e = 0; e < 7; ++e) {
+          double a = 0.0;
+#pragma unroll
+          for (int i = 0; i < 3; ++i) a += wv[i] * R3.c[i][e];
+          a += __shfl_xor(a, 1, 64);
+          a += __shfl_xor(a, 2, 64);
+          v[e] = a + qy[e];
+        }
+        if (stl && q == 0) {
+#pragma unroll
+          for (int e = 0; e < 7; ++e) s.R[k][e] = v[e];
+        }
+        __syncthreads();
+      };
+      stage_vec(lm3);
+      double rdm = 0.0;
+      if (t < n) rdm = fabs(adjoint(t) + pxj + s.gp[t]);
+      const double rd_inf = block_reduce<1>(rdm, s.red);
+      if (!(mu == mu) || !(rd_inf == rd_inf)) { fail = true; break; }
+      if (mu <= A.qp.tol && rp_inf <= 10.0 * A.qp.tol && rd_inf <= 10.0 * A.qp.tol) { conv = true; break; }
+      // W_k = Q_k + sum_i D_i c_i c_i'
+      {
+        double wk[28];
+#pragma unroll
+        for (int a = 0; a < 7; ++a)
+#pragma unroll
+          for (int e = a; e < 7; ++e) {
+            double v = 0.0;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) v += Dg3[i] * R3.c[i][a] * R3.c[i][e];
+            v += __shfl_xor(v, 1, 64);
+            v += __shfl_xor(v, 2, 64);
+            wk[sym7(a, e)] = v + Qp[sym7(a, e)];
+          }
+        if (stl && q == 0) {
+#pragma unroll
+          for (int e = 0; e < 28; ++e) s.W[k][e] = wk[e];
+        }
+      }
+      __syncthreads();
+      build();
+      // Cholesky, right-looking, 2 barriers per column; column j is scaled one step later
+      if (t == 0) s.flag[3] = 0;
+      for (int j = 0; j < n; ++j) {
+        if (t == 0) {
+          const double dj = s.u.Mp[L::pidx(j, j)];
+          if (!(dj > 1e-300)) s.flag[3] = 1;
+          const double dd = dj > 1e-300 ? dj : 1e-300;
+          s.red[4] = 1.0 / dd;
+          s.invd[j] = 1.0 / sqrt(dd);
+        }
+        if (j > 0) {  // scale column j - 1 (L = column / sqrt(pivot))
+          const double sc = s.invd[j - 1];
+          for (int i = j + t; i < n; i += CTH) s.u.Mp[L::pidx(i, j - 1)] *= sc;
+          if (t == 0) s.u.Mp[L::pidx(j - 1, j - 1)] = 1.0 / sc;
+        }
+        __syncthreads();
+        const double inv2 = s.red[4];
+        for (int cc = j + 1 + wave; cc < n; cc += 4) {
+          const double lc = s.u.Mp[L::pidx(cc, j)] * inv2;
+          for (int i = cc + lane; i < n; i += 64) s.u.Mp[L::pidx(i, cc)] -= s.u.Mp[L::pidx(i, j)] * lc;
+        }
+        __syncthreads();
+      }
+      if (t == 0) s.u.Mp[L::pidx(n - 1, n - 1)] = 1.0 / s.invd[n - 1];
+      __syncthreads();
+      if (s.flag[3]) { fail = true; break; }
+
+      // solve M dz = rhs (in s.rhs) -> s.dz; wave 0, lanes own rows lane and lane + 64
+      auto chol_solve = [&]() {
+        if (wave == 0) {
+          const int i0 = lane, i1 = lane + 64;
+          double y0 = s.rhs[i0], y1 = i1 < n ? s.rhs[i1] : 0.0;
+          for (int j = 0; j < n; ++j) {  // L y = b
+            const double own = j < 64 ? y0 : y1;
+            const double yj = __shfl(own, j & 63, 64) * s.invd[j];
+            if (j < 64) { if (i0 == j) y0 = yj; }
+            else if (i1 == j) y1 = yj;
+            if (i0 > j) y0 -= s.u.Mp[L::pidx(i0, j)] * yj;
+            if (i1 > j && i1 < n) y1 -= s.u.Mp[L::pidx(i1, j)] * yj;
+          }
+          for (int j = n - 1; j >= 0; --j) {  // L' x = y
+            const double own = j < 64 ? y0 : y1;
+            const double xj = __shfl(own, j & 63, 64) * s.invd[j];
+            if (j < 64) { if (i0 == j) y0 = xj; }
+            else if (i1 == j) y1 = xj;
+            if (i0 < j) y0 -= s.u.Mp[L::pidx(j, i0)] * xj;
+            if (i1 < j) y1 -= s.u.Mp[L::pidx(j, i1)] * xj;
+          }
+          s.dz[i0] = y0;
+          if (i1 < n) s.dz[i1] = y1;
+        }
+        __syncthreads();
+      };
+      // Newton direction for a given w (per row): rhs = -(adjoint(QY + q + sum (lam + w) c) + Px + gp)
+      auto direction = [&](const double* w3, double* dsl, double* dlm) {
+        double lw[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) lw[i] = lm3[i] + w3[i];
+        stage_vec(lw);
+        if (t < n) s.rhs[t] = -(adjoint(t) + pxj + s.gp[t]);
+        __syncthreads();
+        chol_solve();
+        stage_local(s.dz);
+        double Yd[7];
+#pragma unroll
+        for (int e = 0; e < 7; ++e) Yd[e] = s.Y[k][e];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          double cy = 0.0;
+#pragma unroll
+          for (int e = 0; e < 7; ++e) cy += R3.c[i][e] * Yd[e];
+          dsl[i] = R3.act[i] > 0 ? -rp3[i] - cy : 0.0;
+          dlm[i] = R3.act[i] > 0 ? w3[i] + Dg3[i] * cy : 0.0;
+        }
+      };
+      auto max_step = [&](const double* dsl, const double* dlm) -> double {
+        double a = 1.0;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          if (R3.act[i] > 0) {
+            if (dsl[i] < 0.0) a = fmin(a, -sl3[i] / dsl[i]);
+            if (dlm[i] < 0.0) a = fmin(a, -lm3[i] / dlm[i]);
+          }
+        }
+        return block_reduce<2>(a, s.red);
+      };
+      // predictor (affine)
+      double w3[3], dsa[3], dla[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) w3[i] = R3.act[i] > 0 ? (-sl3[i] * lm3[i] + lm3[i] * rp3[i]) / sl3[i] : 0.0;
+      direction(w3, dsa, dla);
+      const double aa = max_step(dsa, dla);
+      double mua = 0.0;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) mua += R3.act[i] * (sl3[i] + aa * dsa[i]) * (lm3[i] + aa * dla[i]);
+      mua = block_reduce<0>(mua, s.red) / fmax(m_act, 1.0);
+      const double sg = mu > 0 ? (mua / mu) * (mua / mu) * (mua / mu) : 0.0;
+      // corrector
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        w3[i] = R3.act[i] > 0 ? (sg * mu - sl3[i] * lm3[i] - dsa[i] * dla[i] + lm3[i] * rp3[i]) / sl3[i] : 0.0;
+      double dsc[3], dlc[3];
+      direction(w3, dsc, dlc);
+      const double al = fmin(1.0, 0.995 * max_step(dsc, dlc));
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        if (R3.act[i] > 0) {
+          sl3[i] += al * dsc[i];
+          lm3[i] += al * dlc[i];
+        }
+      }
+      if (t < n) s.z[t] += al * s.dz[t];
+      __syncthreads();
+    }
+    if (t == 0) {
+      s.flag[1] += ipm_it;
+      if (fail) { s.flag[0] = VC_NONFINITE; s.flag[2] = 1; }
+      else if (!conv) { if (s.flag[0] == VC_SOLVED) s.flag[0] = VC_MAX_ITER; s.flag[2] &= ~2; }
+      if (A.diag) {
+        A.diag[(size_t)b * 4 + 0] = 0.0;
+        A.diag[(size_t)b * 4 + 1] = 0.0;
+      }
+    }
+    if (fail) { __syncthreads(); break; }
+    // update ubar (scaled back)
+    if (t < n) {
+      const int kk = t >> 1, cc = t & 1;
+      const double scl = (cc == 0 || kk >= N) ? S : 1.0;
+      s.ub[kk][cc] += s.z[t] * scl;
+    }
+    __syncthreads();
+    ++sqp_done;
+  }
+
+  // outputs: u*, x* = rollout(u*), u0, status, iterations
+  if (s.flag[0] != VC_NONFINITE) {
+    predict();
+    __syncthreads();
+  }
+  for (int i = t; i < H; i += CTH) {
+    A.u_out[((size_t)b * H + i) * 2] = s.ub[i][0];
+    A.u_out[((size_t)b * H + i) * 2 + 1] = s.ub[i][1];
+  }
+  for (int e = t; e < H * 8; e += CTH) {
+    const int kk = e >> 3, i = e & 7;
+    double v;
+    if (kk < N) v = s.xs[kk][i];
+    else v = i < 5 ? s.xp[kk - N][i] : 0.0;
+    A.x_out[(size_t)b * H * 8 + e] = v;
+  }
+  if (t == 0) {
+    A.u0[(size_t)b * 2] = s.ub[0][0];
+    A.u0[(size_t)b * 2 + 1] = s.ub[0][1];
+    A.status[b] = s.flag[0];
+    A.iters[b] = s.flag[1];
+    if (A.diag) {
+      A.diag[(size_t)b * 4 + 2] = s.flag[2];
+      A.diag[(size_t)b * 4 + 3] = sqp_done;
+    }
+  }
+}
+
+}  // namespace
+
+bool casc_sqp_built(int N, int M) { return N == 20 && M == 40; }
+
+hipError_t launch_casc_sqp(const CascSqpArgs& a, int N, int M, hipStream_t stream) {
+  if (a.B <= 0) return hipSuccess;
+  if (!casc_sqp_built(N, M)) return hipErrorInvalidValue;
+  if (a.car.tyre == VC_TYRE_LINEAR)
+    hipLaunchKernelGGL((casc_sqp_kernel<20, 40, VC_TYRE_LINEAR>), dim3(a.B), dim3(CTH), 0, stream, a);
+  else
+    hipLaunchKernelGGL((casc_sqp_kernel<20, 40, VC_TYRE_FIALA>), dim3(a.B), dim3(CTH), 0, stream, a);
+  return hipGetLastError();
+}
+
+}  // namespace vc

@@ -14,108 +14,108 @@
 
 namespace vc {
 
-template <int K>
+template <int K, typename S = float>
 struct Dual {
-  float v;
-  float d[K];
-  __host__ __device__ Dual() : v(0.f) {
+  S v;
+  S d[K];
+  __host__ __device__ Dual() : v(S(0)) {
 #pragma unroll
-    for (int i = 0; i < K; ++i) d[i] = 0.f;
+    for (int i = 0; i < K; ++i) d[i] = S(0);
   }
-  __host__ __device__ Dual(double c) : v(float(c)) {
+  __host__ __device__ Dual(double c) : v(S(c)) {
 #pragma unroll
-    for (int i = 0; i < K; ++i) d[i] = 0.f;
+    for (int i = 0; i < K; ++i) d[i] = S(0);
   }
-  __host__ __device__ Dual(float c) : v(c) {
+  __host__ __device__ Dual(float c) : v(S(c)) {
 #pragma unroll
-    for (int i = 0; i < K; ++i) d[i] = 0.f;
+    for (int i = 0; i < K; ++i) d[i] = S(0);
   }
-  __host__ __device__ Dual(int c) : v(float(c)) {
+  __host__ __device__ Dual(int c) : v(S(c)) {
 #pragma unroll
-    for (int i = 0; i < K; ++i) d[i] = 0.f;
+    for (int i = 0; i < K; ++i) d[i] = S(0);
   }
 };
 
 // unary map: value f(v), derivative scale f'(v)
-template <int K>
-__device__ __forceinline__ Dual<K> dmap(const Dual<K>& a, float fv, float dfv) {
-  Dual<K> r;
+template <int K, typename S>
+__device__ __forceinline__ Dual<K, S> dmap(const Dual<K, S>& a, S fv, S dfv) {
+  Dual<K, S> r;
   r.v = fv;
 #pragma unroll
   for (int i = 0; i < K; ++i) r.d[i] = dfv * a.d[i];
   return r;
 }
 
-template <int K>
-__device__ __forceinline__ Dual<K> operator+(const Dual<K>& a, const Dual<K>& b) {
-  Dual<K> r;
+template <int K, typename S>
+__device__ __forceinline__ Dual<K, S> operator+(const Dual<K, S>& a, const Dual<K, S>& b) {
+  Dual<K, S> r;
   r.v = a.v + b.v;
 #pragma unroll
   for (int i = 0; i < K; ++i) r.d[i] = a.d[i] + b.d[i];
   return r;
 }
-template <int K>
-__device__ __forceinline__ Dual<K> operator-(const Dual<K>& a, const Dual<K>& b) {
-  Dual<K> r;
+template <int K, typename S>
+__device__ __forceinline__ Dual<K, S> operator-(const Dual<K, S>& a, const Dual<K, S>& b) {
+  Dual<K, S> r;
   r.v = a.v - b.v;
 #pragma unroll
   for (int i = 0; i < K; ++i) r.d[i] = a.d[i] - b.d[i];
   return r;
 }
-template <int K>
-__device__ __forceinline__ Dual<K> operator-(const Dual<K>& a) {
-  Dual<K> r;
+template <int K, typename S>
+__device__ __forceinline__ Dual<K, S> operator-(const Dual<K, S>& a) {
+  Dual<K, S> r;
   r.v = -a.v;
 #pragma unroll
   for (int i = 0; i < K; ++i) r.d[i] = -a.d[i];
   return r;
 }
-template <int K>
-__device__ __forceinline__ Dual<K> operator*(const Dual<K>& a, const Dual<K>& b) {
-  Dual<K> r;
+template <int K, typename S>
+__device__ __forceinline__ Dual<K, S> operator*(const Dual<K, S>& a, const Dual<K, S>& b) {
+  Dual<K, S> r;
   r.v = a.v * b.v;
 #pragma unroll
   for (int i = 0; i < K; ++i) r.d[i] = a.d[i] * b.v + a.v * b.d[i];
   return r;
 }
-template <int K>
-__device__ __forceinline__ Dual<K> operator/(const Dual<K>& a, const Dual<K>& b) {
-  Dual<K> r;
-  const float ib = 1.0f / b.v;
+template <int K, typename S>
+__device__ __forceinline__ Dual<K, S> operator/(const Dual<K, S>& a, const Dual<K, S>& b) {
+  Dual<K, S> r;
+  const S ib = S(1) / b.v;
   r.v = a.v * ib;
 #pragma unroll
   for (int i = 0; i < K; ++i) r.d[i] = (a.d[i] - r.v * b.d[i]) * ib;
   return r;
 }
-template <int K>
-__device__ __forceinline__ bool operator<(const Dual<K>& a, const Dual<K>& b) { return a.v < b.v; }
-template <int K>
-__device__ __forceinline__ bool operator>(const Dual<K>& a, const Dual<K>& b) { return a.v > b.v; }
-template <int K>
-__device__ __forceinline__ bool operator<=(const Dual<K>& a, const Dual<K>& b) { return a.v <= b.v; }
+template <int K, typename S>
+__device__ __forceinline__ bool operator<(const Dual<K, S>& a, const Dual<K, S>& b) { return a.v < b.v; }
+template <int K, typename S>
+__device__ __forceinline__ bool operator>(const Dual<K, S>& a, const Dual<K, S>& b) { return a.v > b.v; }
+template <int K, typename S>
+__device__ __forceinline__ bool operator<=(const Dual<K, S>& a, const Dual<K, S>& b) { return a.v <= b.v; }
 
-template <int K>
-__device__ __forceinline__ Dual<K> vsin(const Dual<K>& a) { return dmap(a, vsin(a.v), vcos(a.v)); }
-template <int K>
-__device__ __forceinline__ Dual<K> vcos(const Dual<K>& a) { return dmap(a, vcos(a.v), -vsin(a.v)); }
-template <int K>
-__device__ __forceinline__ Dual<K> vtan(const Dual<K>& a) {
-  const float t = vtan(a.v);
-  return dmap(a, t, 1.0f + t * t);
+template <int K, typename S>
+__device__ __forceinline__ Dual<K, S> vsin(const Dual<K, S>& a) { return dmap(a, S(vsin(a.v)), S(vcos(a.v))); }
+template <int K, typename S>
+__device__ __forceinline__ Dual<K, S> vcos(const Dual<K, S>& a) { return dmap(a, S(vcos(a.v)), S(-vsin(a.v))); }
+template <int K, typename S>
+__device__ __forceinline__ Dual<K, S> vtan(const Dual<K, S>& a) {
+  const S t = vtan(a.v);
+  return dmap(a, t, S(1) + t * t);
 }
-template <int K>
-__device__ __forceinline__ Dual<K> vatan(const Dual<K>& a) { return dmap(a, vatan(a.v), 1.0f / (1.0f + a.v * a.v)); }
-template <int K>
-__device__ __forceinline__ Dual<K> vtanh(const Dual<K>& a) {
-  const float t = vtanh(a.v);
-  return dmap(a, t, 1.0f - t * t);
+template <int K, typename S>
+__device__ __forceinline__ Dual<K, S> vatan(const Dual<K, S>& a) { return dmap(a, S(vatan(a.v)), S(1) / (S(1) + a.v * a.v)); }
+template <int K, typename S>
+__device__ __forceinline__ Dual<K, S> vtanh(const Dual<K, S>& a) {
+  const S t = vtanh(a.v);
+  return dmap(a, t, S(1) - t * t);
 }
-template <int K>
-__device__ __forceinline__ Dual<K> vsqrt(const Dual<K>& a) {
-  const float r = vsqrt(a.v);
-  return dmap(a, r, 0.5f / r);
+template <int K, typename S>
+__device__ __forceinline__ Dual<K, S> vsqrt(const Dual<K, S>& a) {
+  const S r = vsqrt(a.v);
+  return dmap(a, r, S(0.5) / r);
 }
-template <int K>
-__device__ __forceinline__ Dual<K> vfabs(const Dual<K>& a) { return a.v < 0.f ? -a : a; }
+template <int K, typename S>
+__device__ __forceinline__ Dual<K, S> vfabs(const Dual<K, S>& a) { return a.v < S(0) ? -a : a; }
 
 }  // namespace vc

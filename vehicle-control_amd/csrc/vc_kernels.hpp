@@ -84,6 +84,29 @@ struct DynSqpArgs {
   vc_obstacles obs;
 };
 
+// Fused cascaded (single-track + point-mass) SQP step (casc_sqp.hip), fp64.
+struct CascSqpArgs {
+  const double* x0;     // [B][8]
+  const double* kappa;  // [B][H]
+  const double* ds;     // [B][H]
+  const double* ubar;   // [B][H][2]  warm start (may alias u_out)
+  double* u_out;        // [B][H][2]  u*
+  double* x_out;        // [B][H][8]  x* = rollout(u*), point-mass states in slots 0..4
+  double* u0;           // [B][2]
+  int32_t* status;      // [B]
+  int32_t* iters;       // [B]
+  double* diag;         // [B][4] optional diagnostics, may be null
+  double* H_out;        // [B][2H][2H]  (mode 1 only)
+  double* g_out;        // [B][2H]      (mode 1 only)
+  int mode;             // 0 = full solve, 1 = first QP's H, g only
+  int B;
+  DynCoef<double> car;
+  vc_dyn_mpc w;
+  vc_casc_mpc cw;
+  vc_qp qp;
+  vc_obstacles obs;
+};
+
 // Elementwise model kernels (models.hip).
 struct ModelArgs {
   int model;  // vc_model
@@ -115,6 +138,8 @@ hipError_t launch_drive(const ModelArgs& m, int dtype, const TrackTable& tt, dou
                         void* log_u, hipStream_t st);
 hipError_t launch_kin_ltv(const KinLtvArgs& a, int N, hipStream_t stream);
 hipError_t launch_dyn_sqp(const DynSqpArgs& a, int N, hipStream_t stream);
+hipError_t launch_casc_sqp(const CascSqpArgs& a, int N, int M, hipStream_t stream);
+bool casc_sqp_built(int N, int M);
 size_t dyn_sqp_smem_bytes(int N);
 int dyn_sqp_debug_stride();
 size_t kin_ltv_smem_bytes(int N);

@@ -362,6 +362,44 @@ __host__ __device__ inline void dyn_stage_terms_alg(const T* X5, const DynCoef<R
   out[6] = -F.Fx_r - bound_r;
 }
 
+// Dynamic point mass, the cascaded controller's tail (models/dynamic_point_mass.py:76-100):
+// x = [V, s, ey, epsi, t], u = [Fx, Fy]; spatial ODE = temporal / s_dot, s' = 1, t' = 1/s_dot.
+// Same car coefficients as the bicycle (simulation/racing.py:44-46 builds both from carconfig).
+template <typename T, typename R>
+__host__ __device__ inline void pm_spatial_ode(const T* x, const T* u, T kappa, const DynCoef<R>& c, T* f) {
+  const T V = x[0], ey = x[2], epsi = x[3];
+  const T Fd = T(c.Frr) + T(c.Cd) * (V * V);
+  const T s_dot = (V * vcos(epsi)) / (T(1) - kappa * ey);
+  const T V_dot = (u[0] - Fd) / T(c.m);
+  const T ey_dot = V * vsin(epsi);
+  const T epsi_dot = u[1] / (T(c.m) * V) - kappa * s_dot;
+  f[0] = V_dot / s_dot;
+  f[1] = T(1);
+  f[2] = ey_dot / s_dot;
+  f[3] = epsi_dot / s_dot;
+  f[4] = T(1) / s_dot;
+}
+
+// Switching map of the cascaded controller (cascaded_mpc.py:256-277): point-mass state
+// from the last single-track state.
+template <typename T>
+__host__ __device__ inline void st_to_pm(const T* x, T* p) {
+  p[0] = vsqrt(x[0] * x[0] + x[1] * x[1]);
+  p[1] = x[4];
+  p[2] = x[5];
+  p[3] = vatan(x[1] / x[0]) + x[6];
+  p[4] = x[7];
+}
+
+// Lateral tyre forces Fy_f + Fy_r at (Ux, Uy, r, delta, Fx) (dynamic_car.py:117-142), the
+// switching cost's lateral residual (cascaded_mpc.py:241-255).
+template <typename T, typename R>
+__host__ __device__ inline T dyn_lateral_sum(const T* X5, const DynCoef<R>& c) {
+  const DynForces<T, R> F(X5[0], X5[1], X5[2], X5[3], X5[4], c);
+  if (c.tyre == VC_TYRE_LINEAR) return -T(c.Caf) * vtan(F.alpha_f) + -T(c.Car) * vtan(F.alpha_r);
+  return fiala_fy(F.alpha_f, T(c.Caf), F.fymax_f(c), T(c.eps)) + fiala_fy(F.alpha_r, T(c.Car), F.fymax_r(c), T(c.eps));
+}
+
 // RK4 (utils/integrators.py:26-37): x + h (1/6) (k1 + 2k2 + 2k3 + k4).
 // The stage sum is accumulated left to right, ((k1 + 2k2) + 2k3) + k4, the evaluation
 // order of the reference expression, so only four stage vectors are live at once.

@@ -133,6 +133,83 @@ bool kin_solve_built(const vc_ctx* c) {
 bool dyn_solve_built(const vc_ctx* c) {
   return c->model == VC_MODEL_DYNAMIC && c->dtype == VC_F32 && vc::dyn_sqp_smem_bytes(c->N) > 0;
 }
+bool casc_solve_built(const vc_ctx* c) {
+  return c->model == VC_MODEL_CASCADED && c->dtype == VC_F64 && vc::casc_sqp_built(c->N, c->p.casc.horizon_pm);
+}
+
+// Cascaded single-track + point-mass SQP (casc_sqp.hip), fp64: arrays span H = N + M stages.
+// mode 0: solve (xbar, ubar, u0, status, iters, diag); mode 1: first QP's H, g (H_out, g_out).
+int casc_solve(vc_ctx* c, int B, const void* x0, const void* kappa, const void* ds, void* xbar, void* ubar, void* u0,
+               int32_t* status, int32_t* iters, void* diag, int flags, int mode = 0, void* H_out = nullptr,
+               void* g_out = nullptr) {
+  const int Hs = c->N + c->p.casc.horizon_pm, n = 2 * Hs, nx = 8, nu = 2;
+  const vc_dyn_mpc& w = c->p.dyn_mpc;
+  if (w.sqp_iters < 1 || w.sqp_iters > 64) return fail(c, VC_E_ARG, "dyn_mpc.sqp_iters=%d outside [1,64]", w.sqp_iters);
+  if (!(w.fx_scale > 0)) return fail(c, VC_E_ARG, "dyn_mpc.fx_scale must be > 0");
+  if (c->p.qp.max_iter < 1) return fail(c, VC_E_ARG, "qp.max_iter must be >= 1");
+  if (!(c->p.casc.ds_pm > 0)) return fail(c, VC_E_ARG, "casc.ds_pm must be > 0");
+  vc::CascSqpArgs a{};
+  a.B = B;
+  a.mode = mode;
+  a.car = vc::make_dyn_coef<double>(c->p.dyn_car);
+  a.w = w;
+  a.cw = c->p.casc;
+  a.qp = c->p.qp;
+  a.obs = c->p.obs;
+  std::vector<Slot> slots;
+  if (flags == VC_HOST_PTRS) {
+    if (mode == 0) {
+      slots = {{x0, nullptr, (size_t)B * nx * 8, nullptr},
+               {kappa, nullptr, (size_t)B * Hs * 8, nullptr},
+               {ds, nullptr, (size_t)B * Hs * 8, nullptr},
+               {ubar, ubar, (size_t)B * Hs * nu * 8, nullptr},
+               {nullptr, xbar, (size_t)B * Hs * nx * 8, nullptr},
+               {nullptr, u0, (size_t)B * nu * 8, nullptr},
+               {nullptr, status, (size_t)B * 4, nullptr},
+               {nullptr, iters, (size_t)B * 4, nullptr},
+               {nullptr, diag, diag ? (size_t)B * 4 * 8 : 0, nullptr}};
+    } else {
+      slots = {{x0, nullptr, (size_t)B * nx * 8, nullptr},
+               {kappa, nullptr, (size_t)B * Hs * 8, nullptr},
+               {ds, nullptr, (size_t)B * Hs * 8, nullptr},
+               {ubar, nullptr, (size_t)B * Hs * nu * 8, nullptr},
+               {nullptr, H_out, (size_t)B * n * n * 8, nullptr},
+               {nullptr, g_out, (size_t)B * n * 8, nullptr}};
+    }
+    if (int r = stage(c, slots)) return r;
+    a.x0 = (const double*)slots[0].dev;
+    a.kappa = (const double*)slots[1].dev;
+    a.ds = (const double*)slots[2].dev;
+    a.ubar = (const double*)slots[3].dev;
+    if (mode == 0) {
+      a.u_out = (double*)slots[3].dev;
+      a.x_out = (double*)slots[4].dev;
+      a.u0 = (double*)slots[5].dev;
+      a.status = (int32_t*)slots[6].dev;
+      a.iters = (int32_t*)slots[7].dev;
+      a.diag = diag ? (double*)slots[8].dev : nullptr;
+    } else {
+      a.H_out = (double*)slots[4].dev;
+      a.g_out = (double*)slots[5].dev;
+    }
+  } else {
+    a.x0 = (const double*)x0;
+    a.kappa = (const double*)kappa;
+    a.ds = (const double*)ds;
+    a.ubar = (const double*)ubar;
+    a.u_out = (double*)ubar;
+    a.x_out = (double*)xbar;
+    a.u0 = (double*)u0;
+    a.status = status;
+    a.iters = iters;
+    a.diag = (double*)diag;
+    a.H_out = (double*)H_out;
+    a.g_out = (double*)g_out;
+  }
+  VC_HIP(c, vc::launch_casc_sqp(a, c->N, c->p.casc.horizon_pm, c->stream));
+  if (flags == VC_HOST_PTRS) return unstage(c, slots);
+  return 0;
+}
 
 // Dynamic single-track SQP (dyn_sqp.hip), fp32: xbar has N state columns.
 int dyn_solve(vc_ctx* c, int B, const void* x0, const void* kappa, const void* ds, void* xbar, void* ubar, void* u0,
@@ -199,7 +276,14 @@ int vc_params_sizeof(void) { return (int)sizeof(vc_params); }
 vc_ctx* vc_create(int device, int model, int N, int max_batch, int dtype, const vc_params* params) {
   g_create_err.clear();
   if (!params) { fail(nullptr, VC_E_ARG, "params is NULL"); return nullptr; }
-  if (model != VC_MODEL_KINEMATIC && model != VC_MODEL_DYNAMIC) { fail(nullptr, VC_E_ARG, "bad model %d", model); return nullptr; }
+  if (model != VC_MODEL_KINEMATIC && model != VC_MODEL_DYNAMIC && model != VC_MODEL_CASCADED) {
+    fail(nullptr, VC_E_ARG, "bad model %d", model);
+    return nullptr;
+  }
+  if (model == VC_MODEL_CASCADED && (params->casc.horizon_pm < 1 || params->casc.horizon_pm > 4096)) {
+    fail(nullptr, VC_E_ARG, "cascaded context needs casc.horizon_pm >= 1 (got %d)", params->casc.horizon_pm);
+    return nullptr;
+  }
   if (dtype != VC_F64 && dtype != VC_F32) { fail(nullptr, VC_E_ARG, "bad dtype %d", dtype); return nullptr; }
   if (N < 1 || N > 4096) { fail(nullptr, VC_E_ARG, "bad horizon N=%d", N); return nullptr; }
   if (max_batch < 1) { fail(nullptr, VC_E_ARG, "bad max_batch %d", max_batch); return nullptr; }
@@ -286,13 +370,14 @@ int vc_solve(vc_ctx* c, int B, const void* x0, const void* kappa, const void* ds
 int vc_solve_diag(vc_ctx* c, int B, const void* x0, const void* kappa, const void* ds, void* xbar, void* ubar,
                   void* u0, int32_t* status, int32_t* iters, void* diag, int flags) {
   if (int r = check_common(c, B, flags)) return r;
-  if (!kin_solve_built(c) && !dyn_solve_built(c))
+  if (!kin_solve_built(c) && !dyn_solve_built(c) && !casc_solve_built(c))
     return fail(c, VC_E_UNSUPPORTED,
-                "vc_solve: model=%d dtype=%d N=%d not built (kinematic fp64 N=20 and dynamic fp32 N=40 are)", c->model,
-                c->dtype, c->N);
+                "vc_solve: model=%d dtype=%d N=%d not built (kinematic fp64 N=20, dynamic fp32 N=40 and "
+                "cascaded fp64 N=20 + 40 are)", c->model, c->dtype, c->N);
   if (!x0 || !kappa || !ds || !xbar || !ubar || !u0 || !status || !iters) return fail(c, VC_E_ARG, "null pointer");
   if (B == 0) return 0;
   if (c->model == VC_MODEL_DYNAMIC) return dyn_solve(c, B, x0, kappa, ds, xbar, ubar, u0, status, iters, diag, flags);
+  if (c->model == VC_MODEL_CASCADED) return casc_solve(c, B, x0, kappa, ds, xbar, ubar, u0, status, iters, diag, flags);
   const int N = c->N, nx = 6, nu = 2;
   vc::KinLtvArgs a{};
   a.mode = 0;
@@ -355,10 +440,13 @@ int vc_debug_stride(void) { return vc::dyn_sqp_debug_stride(); }
 int vc_condense(vc_ctx* c, int B, const void* x0, const void* ubar, const void* kappa, const void* ds, void* H,
                 void* g, int flags) {
   if (int r = check_common(c, B, flags)) return r;
-  if (!kin_solve_built(c))
+  if (!kin_solve_built(c) && !casc_solve_built(c))
     return fail(c, VC_E_UNSUPPORTED, "vc_condense: model=%d dtype=%d N=%d not built", c->model, c->dtype, c->N);
   if (!x0 || !kappa || !ds || !ubar || !H || !g) return fail(c, VC_E_ARG, "null pointer");
   if (B == 0) return 0;
+  if (c->model == VC_MODEL_CASCADED)
+    return casc_solve(c, B, x0, kappa, ds, nullptr, const_cast<void*>(ubar), nullptr, nullptr, nullptr, nullptr, flags,
+                      1, H, g);
   const int N = c->N, n = 2 * N;
   vc::KinLtvArgs a{};
   a.mode = 1;
@@ -528,6 +616,8 @@ int vc_horizon(vc_ctx* c, int B, const void* x0, const void* xbar, double mpc_dt
   if (int r = check_common(c, B, flags)) return r;
   if (!x0 || !xbar || !kappa || !ds) return fail(c, VC_E_ARG, "null pointer");
   if (!c->track) return fail(c, VC_E_ARG, "vc_horizon: no track table (vc_track_set)");
+  if (c->model == VC_MODEL_CASCADED)
+    return fail(c, VC_E_UNSUPPORTED, "vc_horizon: cascaded contexts build their horizon on the host");
   if (B == 0) return 0;
   const int N = c->N, nx = nx_of(c), NS = ns_of(c);
   const size_t es = esize(c);

@@ -16,7 +16,7 @@ ABI_VERSION = 4
 VC_MAX_OBSTACLES = 16
 OBS_MARGIN_MIN = 0.05  # VC_OBS_MARGIN_MIN (csrc/vc_kernels.hpp)
 
-VC_MODEL_KINEMATIC, VC_MODEL_DYNAMIC = 0, 1
+VC_MODEL_KINEMATIC, VC_MODEL_DYNAMIC, VC_MODEL_CASCADED = 0, 1, 2
 VC_F64, VC_F32 = 0, 1
 VC_HOST_PTRS, VC_DEVICE_PTRS = 0, 1
 VC_TYRE_FIALA, VC_TYRE_LINEAR = 0, 1
@@ -62,9 +62,14 @@ class vc_obstacles(C.Structure):
                 ("radius", C.c_double * VC_MAX_OBSTACLES)]
 
 
+class vc_casc_mpc(C.Structure):
+    _fields_ = [("horizon_pm", C.c_int32), ("pad_", C.c_int32)] + [(k, C.c_double) for k in (
+        "ds_pm", "w_dev_pm", "w_Fy", "w_switch", "V_min", "ey_min_pm", "ey_max_pm")]
+
+
 class vc_params(C.Structure):
     _fields_ = [("kin_car", vc_kin_car), ("dyn_car", vc_dyn_car), ("kin_mpc", vc_kin_mpc), ("qp", vc_qp),
-                ("dyn_mpc", vc_dyn_mpc), ("obs", vc_obstacles)]
+                ("dyn_mpc", vc_dyn_mpc), ("obs", vc_obstacles), ("casc", vc_casc_mpc)]
 
 
 class VcError(RuntimeError):

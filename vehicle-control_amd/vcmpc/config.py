@@ -133,6 +133,15 @@ def dyn_mpc_struct(cfg) -> _abi.vc_dyn_mpc:
         w_obs=float(cw.get("obstacles", 0.0)))
 
 
+def casc_mpc_struct(cfg) -> _abi.vc_casc_mpc:
+    """The point-mass tail of a cascaded controller config (reference schema
+    config/controllers/cascaded.yaml, read at cascaded_mpc.py:41-52,181-277)."""
+    cw, pc = cfg["cost_weights"], cfg["state_pm_constraints"]
+    return _abi.vc_casc_mpc(horizon_pm=int(cfg["horizon_pm"]), ds_pm=float(cfg["ds_pm"]),
+                            w_dev_pm=float(cw["deviation_pm"]), w_Fy=float(cw["Fy"]), w_switch=float(cw["switch_F"]),
+                            V_min=float(pc["V_min"]), ey_min_pm=float(pc["ey_min"]), ey_max_pm=float(pc["ey_max"]))
+
+
 def make_params(kin_car=None, dyn_car=None, kin_mpc=None, dyn_mpc=None, tyre: str = "fiala",
                 obstacles=None) -> _abi.vc_params:
     """Pack whichever configs are given into one ``vc_params`` (others zeroed).
@@ -149,6 +158,8 @@ def make_params(kin_car=None, dyn_car=None, kin_mpc=None, dyn_mpc=None, tyre: st
     if dyn_mpc is not None:
         p.dyn_mpc = dyn_mpc_struct(dyn_mpc)
         p.qp = qp_struct(dyn_mpc, DYN_QP_DEFAULTS)
+        if int(dyn_mpc.get("horizon_pm", 0) or 0) > 0:
+            p.casc = casc_mpc_struct(dyn_mpc)
     else:
         p.qp = qp_struct(kin_mpc)
     return p

@@ -22,7 +22,7 @@ import numpy as np
 from . import _abi
 from .config import make_params
 
-NX = {_abi.VC_MODEL_KINEMATIC: 6, _abi.VC_MODEL_DYNAMIC: 8}
+NX = {_abi.VC_MODEL_KINEMATIC: 6, _abi.VC_MODEL_DYNAMIC: 8, _abi.VC_MODEL_CASCADED: 8}
 NU = 2
 _NP_DT = {_abi.VC_F64: np.float64, _abi.VC_F32: np.float32}
 
@@ -39,8 +39,11 @@ class Context:
         self.lib = _abi.load_library()
         self.model, self.N, self.max_batch, self.dtype, self.device = model, int(N), int(max_batch), dtype, device
         self.nx = NX[model]
-        self.ns_solve = self.N + 1 if model == _abi.VC_MODEL_KINEMATIC else self.N
         self.params = params if params is not None else make_params(**cfgs)
+        # stages of the solve arrays: N + 1 states (kinematic), N (single track), or
+        # H = N + horizon_pm (cascaded: kappa, ds, ubar, xbar span the point-mass tail too)
+        self.NH = self.N + (int(self.params.casc.horizon_pm) if model == _abi.VC_MODEL_CASCADED else 0)
+        self.ns_solve = self.N + 1 if model == _abi.VC_MODEL_KINEMATIC else self.NH
         h = self.lib.vc_create(device, model, self.N, self.max_batch, dtype, C.byref(self.params))
         if not h:
             raise _abi.VcError(_abi.VC_E_HIP, self.lib.vc_last_error(None).decode())
@@ -119,7 +122,7 @@ class Context:
         overwritten with u*; returns (u0, xbar, ubar, status, iters).  With
         ``diag=True`` (or a [B, 4] buffer) it calls ``vc_solve_diag`` and returns
         the per-problem solver diagnostics as a sixth element."""
-        B, N, nx, f = self._batch(x0), self.N, self.nx, _NP_DT[self.dtype]
+        B, N, nx, f = self._batch(x0), self.NH, self.nx, _NP_DT[self.dtype]
         NS = self.ns_solve
         if _is_torch(x0):
             import torch
@@ -181,7 +184,7 @@ class Context:
         return A, Bm
 
     def condense(self, x0, ubar, kappa, ds):
-        B, N, nx, f = self._batch(x0), self.N, self.nx, _NP_DT[self.dtype]
+        B, N, nx, f = self._batch(x0), self.NH, self.nx, _NP_DT[self.dtype]
         n = NU * N
         H = self._like(x0, (B, n, n))
         g = self._like(x0, (B, n))
