@@ -12,7 +12,10 @@ The same line carries, under "c3", BASELINE config 3 -- B = 4096 dynamic-bicycle
 (vc_solve on a dynamic context, csrc/dyn_sqp.hip) -- measured the same way; it is a
 secondary workload, not `value`.  Under "c5": BASELINE config 5 -- the closed-loop
 Monte-Carlo, 8192 vehicles x 500 steps on ippodromo (horizon -> NMPC solve -> fp64
-plant, all on the device, vc_simulate), vehicles sharded over the ranks.
+plant, all on the device, vc_simulate), vehicles sharded over the ranks.  Under
+"cascaded": the reference's cascaded NMPC (20 single-track + 40 point-mass stages,
+config/controllers/cascaded.yaml), B = 4096 per GPU, fp64
+(csrc/casc_sqp.hip).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--c3-batch B3]
                     [--c5-vehicles V] [--c5-steps S] [--no-c3] [--no-c5] [--no-cpu-baseline]
@@ -102,6 +105,8 @@ def parse():
     ap.add_argument("--c5-vehicles", type=int, default=C5_VEHICLES, help="C5 vehicles in total (config 5: 8192)")
     ap.add_argument("--c5-steps", type=int, default=C5_STEPS, help="C5 closed-loop steps (config 5: 500)")
     ap.add_argument("--no-c5", action="store_true", help="skip the secondary C5 closed-loop measurement")
+    ap.add_argument("--casc-batch", type=int, default=4096, help="cascaded NMPC problems per GPU")
+    ap.add_argument("--no-casc", action="store_true", help="skip the cascaded (point-mass tail) measurement")
     return ap.parse_args()
 
 
@@ -212,6 +217,103 @@ def run_c3(args, dev, stream, rank, dist, steps):
            "solver": {"solved_frac": float((st == 0).mean()), "pdip_iters_mean": float(it.mean()),
                       "pdip_iters_max": int(it.max())}}
     return out, data
+
+
+# ---- cascaded NMPC: N = 20 single-track + M = 40 point-mass stages, fp64 ----
+CA_N, CA_M = 20, 40
+CA_H, CA_n = CA_N + CA_M, 2 * (CA_N + CA_M)
+# compulsory bytes: in x0 + kappa + ds + ubar, out u* + x* (H columns) + u0 (fp64) + status + iters
+CA_BYTES_PER_SOLVE = (8 + 2 * CA_H + 2 * CA_H) * 8 + (2 * CA_H + 8 * CA_H + 2) * 8 + 8
+# algorithmic fp64 FLOPs per interior-point iteration: the stage-block normal matrix
+# sum_k V_k' W_k V_k (7 basis rows, columns < 2k + 2: W V then the lower half of V' (W V)),
+# n^3/3 Cholesky, 2 x 2 triangular solves, 6 forward/adjoint passes over the condensed rows;
+# per SQP iteration the rollout + dual-number Jacobians and the condensing
+CA_G_NNZ = 5 * sum(2 * k for k in range(1, CA_N)) + 2 * sum(2 * (CA_N + m) for m in range(CA_M))
+CA_FLOP_ITER = (sum(2 * (2 * k + 2) * 7 * 7 + (2 * k + 2) ** 2 * 7 for k in range(CA_H))
+                + CA_n ** 3 // 3 + 4 * CA_n * CA_n + 6 * 2 * CA_G_NNZ)
+CA_FLOP_SQP = (CA_N - 1) * 10 * 4 * 400 + (CA_M - 1) * 7 * 60 + CA_n * (CA_N * 8 * 8 + CA_M * 5 * 5) * 2
+
+
+def run_casc(args, dev, stream, rank, dist, steps):
+    """Cascaded NMPC (horizon_pm = 40) on this rank, B problems per GPU, fp64."""
+    import numpy as np
+    import torch
+
+    from vcmpc import Context, _abi
+    from vcmpc.config import load_config, make_params
+    from vcmpc.workload import cascaded_batch
+
+    B = args.casc_batch
+    data = cascaded_batch(B, seed=args.seed + 15485863 * rank)
+    t = {k: torch.from_numpy(v).to(dev) for k, v in data.items()}
+    ubar0 = t["ubar"].clone()
+    params = make_params(dyn_car=load_config("dynamic_car"), dyn_mpc=load_config("cascaded_mpc"), tyre="fiala")
+    ctx = Context(model=_abi.VC_MODEL_CASCADED, N=CA_N, max_batch=B, dtype=_abi.VC_F64, device=dev.index,
+                  params=params)
+    ctx.set_stream(stream.cuda_stream)
+    xbar = torch.empty((B, CA_H, 8), dtype=torch.float64, device=dev)
+    u0 = torch.empty((B, 2), dtype=torch.float64, device=dev)
+    status = torch.empty((B,), dtype=torch.int32, device=dev)
+    iters = torch.empty((B,), dtype=torch.int32, device=dev)
+
+    def step(ev=None):
+        t["ubar"].copy_(ubar0)
+        if ev is not None:
+            ev[0].record(stream)
+        ctx.solve(t["x0"], t["kappa"], t["ds"], t["ubar"], xbar, u0, status, iters)
+        if ev is not None:
+            ev[1].record(stream)
+
+    step()
+    torch.cuda.synchronize(dev)
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(events[i])
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    st, it = status.cpu().numpy(), iters.cpu().numpy()
+    solves, elapsed_max, kern_ms_max = dist.aggregate(float(B * steps), elapsed, kern_ms, dev)
+    ctx.close()
+    flops = 3 * CA_FLOP_SQP + float(it.mean()) * CA_FLOP_ITER
+    out = {"metric": "MPC solves/sec (batched, N=20 single-track + 40 point-mass stages, 3 SQP iterations)",
+           "value": solves / elapsed_max, "unit": "solves/s", "steps": steps,
+           "ms_per_step": elapsed_max / steps * 1e3, "dtype": "f64",
+           "config": {"workload": f"cascaded NMPC (config/controllers/cascaded.yaml), B={B} per GPU, "
+                                  f"H={CA_N}+{CA_M}, fp64, Fiala tyre", "batch_per_gpu": B, "horizon": CA_H},
+           "roofline": {"bound": "mfma", "kernel": "casc_sqp_kernel<20, 40, fiala>", "kernel_ms": kern_ms,
+                        "flops_per_solve": flops, "achieved": flops * B / (kern_ms / 1e3) / 1e12,
+                        "peak": FP64_VALU_PEAK, "unit": "TFLOP/s",
+                        "frac": flops * B / (kern_ms / 1e3) / 1e12 / FP64_VALU_PEAK,
+                        "hbm": {"bytes_per_solve": CA_BYTES_PER_SOLVE,
+                                "achieved": CA_BYTES_PER_SOLVE * B / (kern_ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
+                                "unit": "GB/s"}},
+           "solver": {"solved_frac": float((st == 0).mean()), "pdip_iters_mean": float(it.mean()),
+                      "pdip_iters_max": int(it.max())}}
+    return out, data
+
+
+def cpu_baseline_casc(data, sample):
+    """The fp64 numpy oracle of the cascaded SQP contract (oracle/casc_sqp.py), one thread."""
+    from threadpoolctl import threadpool_limits
+
+    from oracle import casc_sqp as CS
+    from oracle import models as M
+    from vcmpc.config import load_config
+    W = CS.casc_weights(load_config("cascaded_mpc"))
+    p = M.dyn_params_from_config(load_config("dynamic_car"))
+    d = {k: v[:sample] for k, v in data.items()}
+    with threadpool_limits(limits=1):
+        t0 = time.perf_counter()
+        CS.casc_sqp_solve(d["x0"], d["ubar"], d["kappa"], d["ds"], p, W, "fiala")
+        dt = time.perf_counter() - t0
+    return {"value": len(d["x0"]) / dt, "unit": "solves/s", "cores": 1, "kind": "port",
+            "sample": f"{len(d['x0'])} problems of the cascaded workload, one oracle pass (3 SQP iterations of "
+                      f"complex-step linearisation + exact QP, numpy fp64, 1 thread) in {dt:.2f} s"}
 
 
 C5_VEHICLES, C5_STEPS = 8192, 500
@@ -378,6 +480,12 @@ def main():
             c3, c3_data = run_c3(args, dev, stream, rank, dist, max(3, args.steps // 4))
         except Exception as e:  # the headline line must still print
             c3 = {"error": f"{type(e).__name__}: {e}"}
+    ca = ca_data = None
+    if not args.no_casc:
+        try:
+            ca, ca_data = run_casc(args, dev, stream, rank, dist, max(2, args.steps // 8))
+        except Exception as e:
+            ca = {"error": f"{type(e).__name__}: {e}"}
     c5 = c5_aux = None
     if not args.no_c5:
         try:
@@ -425,12 +533,16 @@ def main():
             out["cpu_baseline"] = cpu_baseline(data, min(args.cpu_sample, B))
             if c3_data is not None and "error" not in c3:
                 c3["cpu_baseline"] = cpu_baseline_c3(c3_data, 8)
+            if ca_data is not None and "error" not in ca:
+                ca["cpu_baseline"] = cpu_baseline_casc(ca_data, 4)
             if c5_aux and "error" not in c5:
                 from oracle.track import load_track
                 otrack = load_track(os.path.join(ROOT, "vehicle-control_amd", "config", "tracks", "ippodromo.yaml"))
                 c5["cpu_baseline"] = cpu_baseline_c5(c5_aux[0], otrack)
         if c3 is not None:
             out["c3"] = c3
+        if ca is not None:
+            out["cascaded"] = ca
         if c5 is not None:
             out["c5"] = c5
         print(json.dumps(out), flush=True)

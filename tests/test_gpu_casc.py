@@ -97,3 +97,49 @@ def test_batch_properties_and_device_pointers(ctx):
     ctx.synchronize()
     np.testing.assert_array_equal(r[2].cpu().numpy(), us)
     np.testing.assert_array_equal(r[3].cpu().numpy(), st)
+
+
+def test_cascaded_controller_closed_loop_on_ippodromo():
+    """CascadedMPC(car, point_mass, cascaded config) -> command -> car.drive, the reference's
+    racing loop (simulation/racing.py:416-423) with the point-mass tail, on ippodromo."""
+    from vcmpc.config import load_config
+    from vcmpc.controllers import CascadedMPC, CascadedTailMPC
+    from vcmpc.environment import Track
+    from vcmpc.models import DynamicCar, DynamicPointMass
+    np.random.seed(31)
+    tr = Track.load("ippodromo")
+    car = DynamicCar(load_config("dynamic_car"), tr, tyre="fiala")
+    pm = DynamicPointMass(load_config("dynamic_car"), tr)
+    car.state = car.create_state(Ux=8.0, s=1.0)
+    mpc = CascadedMPC(car, pm, load_config("cascaded_mpc"))
+    assert isinstance(mpc, CascadedTailMPC) and isinstance(mpc, CascadedMPC)
+    solved, ey_max = 0, 0.0
+    for _ in range(200):
+        a = mpc.command(car.state)
+        solved += int(mpc.status[0] == 0)
+        car.drive(a)
+        ey_max = max(ey_max, abs(car.state.ey))
+        assert np.isfinite(car.state.values).all()
+    print("cascaded closed loop: solved %d/200, s %.1f m, Ux %.1f m/s, max |ey| %.2f m"
+          % (solved, car.state.s, car.state.Ux, ey_max))
+    assert mpc.state_prediction.shape == (8, N + M) and mpc.action_prediction.shape == (2, N + M)
+    assert mpc.get_state_prediction().shape == (N + M, 3)
+    assert solved >= 190
+    assert ey_max < tr.width / 2
+    assert car.state.s > 100.0
+
+
+def test_host_horizon_params_match_oracle():
+    from vcmpc.controllers.cascaded_mpc import casc_horizon_params
+    from vcmpc.environment import Track
+    tr = Track.load("ippodromo")
+    rng = np.random.default_rng(0)
+    s0 = rng.uniform(0, 300, 3)
+    ux = rng.uniform(5, 20, (3, N + M))
+    ds, kap = casc_horizon_params(s0, ux, 0.03, N, M, 3.0, tr.k)
+    for b in range(3):
+        x = np.zeros(8); x[4] = s0[b]
+        pred = np.zeros((8, N + M)); pred[0] = ux[b]
+        d2, k2 = CS.casc_horizon_params(x, pred, 0.03, N, M, 3.0, tr.k)
+        np.testing.assert_allclose(ds[b], d2, rtol=0, atol=1e-15)
+        np.testing.assert_allclose(kap[b], k2, rtol=0, atol=1e-15)

@@ -13,8 +13,9 @@ and ``get_state_prediction`` (:340-352).
 What changes is the solve (cascaded_mpc.py:308, IPOPT + HSL MA27 on the NLP): a fixed
 number of sequential-QP iterations in one fused fp32 gfx950 kernel (csrc/dyn_sqp.hip;
 contract: oracle/dyn_sqp.py).  ``BatchedSingleTrackMPC`` is the same controller for B
-vehicles at once.  The cascaded point-mass tail (``horizon_pm > 0``,
-cascaded_mpc.py:181-277) is SURVEY 8(f) row 3 and raises; obstacle barrier terms
+vehicles at once.  With ``horizon_pm > 0`` (the cascaded point-mass tail,
+cascaded_mpc.py:181-277) ``CascadedMPC`` / ``BatchedCascadedMPC`` run the fp64 cascaded
+SQP (csrc/casc_sqp.hip, contract oracle/casc_sqp.py); obstacle barrier terms
 (`obstacles: True`, cascaded_mpc.py:173-176) enter each QP as in DESIGN.md 2c.
 """
 from __future__ import annotations
@@ -47,7 +48,7 @@ class BatchedSingleTrackMPC(Controller):
     def __init__(self, car, config, batch: int, device: int = 0, seed: int | None = 31):
         super().__init__()
         if int(config.get("horizon_pm", 0)) > 0:
-            raise NotImplementedError("the cascaded point-mass tail (cascaded_mpc.py:181-277) is SURVEY 8(f) row 3")
+            raise ValueError("horizon_pm > 0: use BatchedCascadedMPC (the point-mass tail, cascaded_mpc.py:181-277)")
         self.config = config
         self.car = car
         self.N = int(config["horizon"])
@@ -93,9 +94,101 @@ class BatchedSingleTrackMPC(Controller):
         return u0.astype(np.float64)
 
 
+def casc_horizon_params(s0, ux_pred, mpc_dt, N, M, ds_pm, k_of_s):
+    """``_init_horizon`` with a point-mass tail (cascaded_mpc.py:316-338), batched.
+
+    s0[B], ux_pred[B, >= N] (the *unshifted* previous Ux prediction) -> ds[B, H], kappa[B, H]:
+    single-track ds = mpc_dt * Ux_pred[:N], curvature at s0 + cumsum(ds) - ds[0]; point mass
+    ds = ds_pm, curvature at cumsum(ds_pm) - ds[N-1] + s_traj[N-1] (:331-338)."""
+    ds = mpc_dt * np.asarray(ux_pred, np.float64)[:, :N]
+    s_traj = np.cumsum(ds, axis=1) - ds[:, :1] + np.asarray(s0, np.float64)[:, None]
+    ds_p = np.full((ds.shape[0], M), float(ds_pm))
+    s_pm = np.cumsum(ds_p, axis=1) - ds[:, -1:] + s_traj[:, -1:]
+    s_all = np.concatenate([s_traj, s_pm], axis=1)
+    kappa = np.asarray(k_of_s(s_all), np.float64).reshape(s_all.shape)
+    return np.ascontiguousarray(np.concatenate([ds, ds_p], axis=1)), np.ascontiguousarray(kappa)
+
+
+class BatchedCascadedMPC(Controller):
+    """B independent cascaded NMPCs (single track N + point mass M = horizon_pm stages)
+    solved in one launch (csrc/casc_sqp.hip, fp64; contract oracle/casc_sqp.py)."""
+
+    def __init__(self, car, config, batch: int, device: int = 0, seed: int | None = 31):
+        Controller.__init__(self)
+        self.config = config
+        self.car = car
+        self.N = int(config["horizon"])
+        self.M = int(config["horizon_pm"])
+        self.H = self.N + self.M
+        self.dt = float(config["mpc_dt"])
+        self.ds_pm = float(config["ds_pm"])
+        self.ns, self.na = len(car.state), len(car.input)
+        self.B = int(batch)
+        self.ctx = Context(model=_abi.VC_MODEL_CASCADED, N=self.N, max_batch=self.B, dtype=_abi.VC_F64,
+                           device=device,
+                           params=make_params(dyn_car=car.config, dyn_mpc=config, tyre=getattr(car, "tyre", "fiala"),
+                                              obstacles=obstacle_list(car, config)))
+        # warm starts: cascaded_mpc.py:72-76 (ones over H columns, Ux + 3 on the single-track part)
+        rng = np.random.RandomState(seed) if seed is not None else np.random
+        self.state_prediction = np.ones((self.B, self.ns, self.H))
+        self.state_prediction[:, IUX, :self.N] += 3
+        self.action_prediction = np.ones((self.B, self.na, self.H)) + rng.random_sample((self.B, self.na, self.H))
+        self.status = np.zeros(self.B, np.int32)
+        self.iters = np.zeros(self.B, np.int32)
+        self._fresh = np.ones(self.B, bool)  # no solution yet: the tail gets the neutral guess
+
+    def _neutral(self, x0, kappa):
+        """Neutral warm start [B, H, 2]: single track Fx = w = 0; point mass Fx = the drag at
+        the current speed and Fy = m V^2 kappa (steady cornering along the centre line).
+        The condensed SQP rolls the point mass out from its inputs, so the reference's first
+        guess 1 + U[0, 1) N (cascaded_mpc.py:74-76; harmless for IPOPT's multiple shooting)
+        would turn the 120 m tail off the track in every corner."""
+        car = self.car.config
+        m, Frr, Cd = float(car["car"]["m"]), float(car["env"]["Frr"]), float(car["env"]["Cd"])
+        V = np.maximum(np.hypot(x0[:, 0], x0[:, 1]), 3.0)[:, None]
+        u = np.zeros((x0.shape[0], self.H, self.na))
+        u[:, self.N:, 0] = Frr + Cd * V ** 2
+        u[:, self.N:, 1] = m * V ** 2 * kappa[:, self.N:]
+        return u
+
+    def command(self, states):
+        """states[B, 8] -> actions[B, 2] (Fx, w of the first stage).
+
+        Warm start: the previous (8, H) / (2, H) predictions, unshifted
+        (cascaded_mpc.py:320-321), w projected onto its box, the point-mass tail of a
+        vehicle without a previous solution from :meth:`_neutral`; a problem that does not
+        come back VC_SOLVED is re-solved once from the neutral warm start."""
+        x0 = np.ascontiguousarray(np.asarray(states, np.float64).reshape(self.B, self.ns))
+        ds, kappa = casc_horizon_params(x0[:, IS], self.state_prediction[:, IUX, :], self.dt, self.N, self.M,
+                                        self.ds_pm, self.car.track.k)
+        ubar = np.ascontiguousarray(np.swapaxes(self.action_prediction, 1, 2), dtype=np.float64)
+        if self._fresh.any():
+            ubar[self._fresh, self.N:] = self._neutral(x0, kappa)[self._fresh, self.N:]
+        ic = self.config["input_constraints"]
+        np.clip(ubar[:, :self.N, IW], ic["w_min"], ic["w_max"], out=ubar[:, :self.N, IW])
+        u0, xbar, ustar, status, iters = self.ctx.solve(x0, kappa, ds, ubar)
+        bad = status != 0
+        if bad.any():
+            idx = np.nonzero(bad)[0]
+            r = self.ctx.solve(np.ascontiguousarray(x0[idx]), np.ascontiguousarray(kappa[idx]),
+                               np.ascontiguousarray(ds[idx]), np.ascontiguousarray(self._neutral(x0, kappa)[idx]))
+            u0[idx], xbar[idx], ustar[idx], status[idx], iters[idx] = r
+        self._fresh = status != 0
+        self.action_prediction = np.swapaxes(ustar, 1, 2).copy()
+        self.state_prediction = np.swapaxes(xbar, 1, 2).copy()
+        self.status, self.iters = status, iters
+        return u0
+
+
 class CascadedMPC(BatchedSingleTrackMPC):
-    """Single-vehicle drop-in for ``CascadedMPC(car, point_mass, config)`` (cascaded_mpc.py:16-39)
-    with ``horizon_pm: 0``."""
+    """Single-vehicle drop-in for ``CascadedMPC(car, point_mass, config)`` (cascaded_mpc.py:16-39).
+    ``horizon_pm: 0`` runs the single-track SQP (csrc/dyn_sqp.hip, fp32); ``horizon_pm > 0``
+    returns a :class:`CascadedTailMPC` (point-mass tail, csrc/casc_sqp.hip, fp64)."""
+
+    def __new__(cls, car, point_mass, config, device: int = 0):
+        if cls is CascadedMPC and int(config.get("horizon_pm", 0) or 0) > 0:
+            return object.__new__(CascadedTailMPC)
+        return object.__new__(cls)
 
     def __init__(self, car, point_mass, config, device: int = 0):
         self.point_mass = point_mass
@@ -119,3 +212,35 @@ class CascadedMPC(BatchedSingleTrackMPC):
     def get_state_prediction(self):
         """Global (x, y, psi) of the N predicted states -- cascaded_mpc.py:340-352 (M = 0)."""
         return np.array([self.car.rel2glob(self.state_prediction[:, i]) for i in range(self.N)]).squeeze()
+
+
+class CascadedTailMPC(BatchedCascadedMPC, CascadedMPC):
+    """``CascadedMPC(car, point_mass, config)`` with ``horizon_pm > 0`` (the reference's
+    cascaded controller, config/controllers/cascaded.yaml) for one vehicle."""
+
+    def __init__(self, car, point_mass, config, device: int = 0):
+        self.point_mass = point_mass
+        BatchedCascadedMPC.__init__(self, car, config, batch=1, device=device, seed=None)
+        self.state_prediction = self.state_prediction[0]
+        self.action_prediction = np.ones((self.na, self.H)) + np.random.random((self.na, self.H))
+
+    def command(self, state):
+        sp, ap = self.state_prediction, self.action_prediction
+        self.state_prediction, self.action_prediction = sp[None], ap[None]
+        try:
+            u0 = BatchedCascadedMPC.command(self, state.values.reshape(1, -1))
+        except Exception:
+            self.state_prediction, self.action_prediction = sp, ap
+            raise
+        self.state_prediction = self.state_prediction[0]
+        self.action_prediction = self.action_prediction[0]
+        return self.car.create_action(*u0[0])
+
+    def get_state_prediction(self):
+        """cascaded_mpc.py:340-352: the car's N predicted states and the point mass's M,
+        as global (x, y, psi) (point-mass columns hold V, s, ey, epsi, t in rows 0..4)."""
+        sp = self.state_prediction
+        car = [self.car.rel2glob(sp[:, i]) for i in range(self.N)]
+        tr = self.car.track
+        pm = [tr.rel2glob(sp[1, j], sp[2, j], sp[3, j]) for j in range(self.N, self.H)]
+        return np.array(car + pm, dtype=np.float64).squeeze()
