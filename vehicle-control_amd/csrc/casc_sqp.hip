@@ -114,6 +114,365 @@ struct Rows3 {
   double act[3];
 };
 
+
+// normal matrix (see the kernel's comment at its call); out of line so its register tiles do not
+// compete with the interior point's live row state
+// normal matrix: M = P + sum_k V_k' W_k V_k (W_k in s.W), one pass, no read-modify-write.
+// Thread-owned 4x4 register tiles of the lower triangle (465 tiles; thread t takes tile t
+// and its mirror 464 - t so heavy and light tiles pair up).  Entry (i, j), i >= j, sums
+// the stages k >= i / 2; past the tile's first two stages every column is below 2k, so
+// only the condensed rows enter (5 for a single-track stage, 2 for a point-mass stage).
+template <int N, int M>
+__device__ __forceinline__ void casc_build(CascSmem<N, M>& s, double csw, double w_epsi, double prox, double w_Fx,
+                                        double w_Fy, double w_switch, double S) {
+  using L = CL<N, M>;
+  constexpr int H = L::H, n = L::n;
+  const int t = threadIdx.x;
+  auto pair_w = [&](int a) -> double {
+    const int k = a >> 1, cc = a & 1;
+    if (k > H - 2) return 0.0;
+    double w;
+    if (cc == 0) w = (k == N - 1 ? w_switch : w_Fx) / s.dsv[k];
+    else if (k >= N) w = w_Fy / s.dsv[k];
+    else return 0.0;
+    return 2.0 * w * S * S;
+  };
+  auto vcol = [&](int k, int col, double* v) {
+    if (k < N) {
+      const int len = 2 * k, base = L::gst(k);
+      const bool in = col < len;
+#pragma unroll
+      for (int r = 0; r < 5; ++r) v[r] = in ? s.G[base + r * len + (in ? col : 0)] : 0.0;
+    } else {
+      const int m = k - N, len = 2 * k, base = L::gpm(m);
+      const bool in = col < len;
+      v[0] = in ? s.G[base + (in ? col : 0)] : 0.0;
+      v[1] = v[2] = v[3] = 0.0;
+      v[4] = in ? s.G[base + len + (in ? col : 0)] : 0.0;
+    }
+    v[5] = col == 2 * k ? 1.0 : 0.0;
+    v[6] = col == 2 * k + 1 ? 1.0 : 0.0;
+  };
+      constexpr int NT = n / 4, NTILES = NT * (NT + 1) / 2;
+#pragma unroll 1
+      for (int pass = 0; pass < 2; ++pass) {
+        const int tile = pass == 0 ? t : NTILES - 1 - t;
+        if (tile >= NTILES || (pass == 1 && tile < CTH)) continue;
+        int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
+        while ((I + 1) * (I + 2) / 2 <= tile) ++I;
+        while (I * (I + 1) / 2 > tile) --I;
+        const int J = tile - I * (I + 1) / 2;
+        const int i0 = 4 * I, j0 = 4 * J;
+        double acc[4][4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int cc = 0; cc < 4; ++cc) {
+            const int i = i0 + r, j = j0 + cc;
+            double v = 0.0;
+            if (i < 2 * N + 2 && j < 2 * N + 2) v += 2.0 * csw * s.G[L::SW0 + i] * s.G[L::SW0 + j];
+            if (i < 2 * (H - 1) && j < 2 * (H - 1)) v += 2.0 * w_epsi * s.G[L::T0 + i] * s.G[L::T0 + j];
+            if (i == j) v += 2.0 * prox + pair_w(j) + (j >= 2 ? pair_w(j - 2) : 0.0);
+            if (i == j + 2) v -= pair_w(j);
+            acc[r][cc] = v;
+          }
+        // the tile's first two stages: general stage vectors (unit input slots); one column
+        // at a time to keep the register footprint small (these are 2 of up to 60 stages)
+#pragma unroll 1
+        for (int kk = 2 * I; kk < 2 * I + 2 && kk < H; ++kk) {
+          const double* Wf = s.W[kk];
+#pragma unroll 1
+          for (int cc = 0; cc < 4; ++cc) {
+            double vj[7], hv[7];
+            vcol(kk, j0 + cc, vj);
+#pragma unroll
+            for (int a = 0; a < 7; ++a) {
+              double x = 0.0;
+#pragma unroll
+              for (int e = 0; e < 7; ++e) x += Wf[a <= e ? sym7(a, e) : sym7(e, a)] * vj[e];
+              hv[a] = x;
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              double vi[7];
+              vcol(kk, i0 + r, vi);
+              double x = 0.0;
+#pragma unroll
+              for (int a = 0; a < 7; ++a) x += vi[a] * hv[a];
+#pragma unroll
+              for (int c2 = 0; c2 < 4; ++c2) acc[r][c2] += (c2 == cc) ? x : 0.0;
+            }
+          }
+        }
+        // single-track bulk stages: 5 condensed rows
+#pragma unroll 1
+        for (int kk = 2 * I + 2; kk < N; ++kk) {
+          const int len = 2 * kk;
+          const double* g = &s.G[L::gst(kk)];
+          double Wg[5][5];
+#pragma unroll
+          for (int a = 0; a < 5; ++a)
+#pragma unroll
+            for (int e = 0; e < 5; ++e) Wg[a][e] = s.W[kk][a <= e ? sym7(a, e) : sym7(e, a)];
+          double hv[4][5];
+#pragma unroll
+          for (int cc = 0; cc < 4; ++cc) {
+            double vj[5];
+#pragma unroll
+            for (int a = 0; a < 5; ++a) vj[a] = g[a * len + j0 + cc];
+#pragma unroll
+            for (int a = 0; a < 5; ++a) {
+              double x = 0.0;
+#pragma unroll
+              for (int e = 0; e < 5; ++e) x += Wg[a][e] * vj[e];
+              hv[cc][a] = x;
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            double vi[5];
+#pragma unroll
+            for (int a = 0; a < 5; ++a) vi[a] = g[a * len + i0 + r];
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) {
+              double x = 0.0;
+#pragma unroll
+              for (int a = 0; a < 5; ++a) x += vi[a] * hv[cc][a];
+              acc[r][cc] += x;
+            }
+          }
+        }
+        // point-mass bulk stages: rows V (slot 0) and ey (slot 4)
+#pragma unroll 1
+        for (int kk = (2 * I + 2 > N ? 2 * I + 2 : N); kk < H; ++kk) {
+          const int len = 2 * kk;
+          const double* g = &s.G[L::gpm(kk - N)];
+          const double w00 = s.W[kk][sym7(0, 0)], w04 = s.W[kk][sym7(0, 4)], w44 = s.W[kk][sym7(4, 4)];
+          double h0[4], h4[4];
+#pragma unroll
+          for (int cc = 0; cc < 4; ++cc) {
+            const double a = g[j0 + cc], e = g[len + j0 + cc];
+            h0[cc] = w00 * a + w04 * e;
+            h4[cc] = w04 * a + w44 * e;
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const double a = g[i0 + r], e = g[len + i0 + r];
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) acc[r][cc] += a * h0[cc] + e * h4[cc];
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int cc = 0; cc < 4; ++cc)
+            if (i0 + r >= j0 + cc) s.u.Mp[L::pidx(i0 + r, j0 + cc)] = acc[r][cc];
+      }
+      __syncthreads();
+}
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+
+// Blocked right-looking Cholesky of the packed normal matrix, in place (L in the lower
+// triangle, 1 / L_jj in s.invd), 8-column blocks, 3 barriers per block:
+//   A  wave 0 factors the 8x8 diagonal block in registers (lane p owns column p);
+//   B  one thread per row below the block solves its 8 panel entries against L_D;
+//   C  4x4 register tiles of the trailing triangle take the rank-8 update.
+// s.flag[3] = 1 on a non-positive pivot.
+template <int N, int M>
+__device__ __forceinline__ void casc_cholesky(CascSmem<N, M>& s) {
+  using L = CL<N, M>;
+  constexpr int n = L::n, NB = 8;
+  static_assert(n % NB == 0, "block size");
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  if (t == 0) s.flag[3] = 0;
+#pragma unroll 1
+  for (int j0 = 0; j0 < n; j0 += NB) {
+    // A: diagonal block
+    if (wave == 0) {
+      const int p = lane < NB ? lane : 0;
+      double a[NB];
+#pragma unroll
+      for (int r = 0; r < NB; ++r) a[r] = (r >= p) ? s.u.Mp[L::pidx(j0 + r, j0 + p)] : 0.0;
+      bool bad = false;
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        const double d = readlane_d(a[q], q);
+        bad = bad || !(d > 1e-300);
+        const double l = sqrt(d > 1e-300 ? d : 1e-300), il = 1.0 / l;
+        if (p == q) {
+#pragma unroll
+          for (int r = 0; r < NB; ++r) a[r] = r == q ? l : (r > q ? a[r] * il : a[r]);
+        }
+        double lq[NB];  // column q of L (rows > q), read from lane q after its scaling
+#pragma unroll
+        for (int r = q + 1; r < NB; ++r) lq[r] = readlane_d(a[r], q);
+        // lanes p > q: a[r] -= L[r][q] L[p][q] for r >= p
+#pragma unroll
+        for (int r = q + 1; r < NB; ++r) {
+          const double lrq = lq[r];
+          double lp = 0.0;
+#pragma unroll
+          for (int c = q + 1; c < NB; ++c) lp = (p == c) ? lq[c] : lp;
+          if (p > q && r >= p) a[r] -= lrq * lp;
+        }
+        if (lane == 0) s.invd[j0 + q] = il;
+      }
+      if (lane < NB) {
+#pragma unroll
+        for (int r = 0; r < NB; ++r)
+          if (r >= p) s.u.Mp[L::pidx(j0 + r, j0 + p)] = a[r];
+      }
+      if (lane == 0 && bad) s.flag[3] = 1;
+    }
+    __syncthreads();
+    // B: panel rows i >= j0 + NB
+    {
+      const int i = j0 + NB + t;
+      if (i < n) {
+        double x[NB];
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+          double v = s.u.Mp[L::pidx(i, j0 + q)];
+#pragma unroll
+          for (int r = 0; r < q; ++r) v -= x[r] * s.u.Mp[L::pidx(j0 + q, j0 + r)];
+          x[q] = v * s.invd[j0 + q];
+        }
+#pragma unroll
+        for (int q = 0; q < NB; ++q) s.u.Mp[L::pidx(i, j0 + q)] = x[q];
+      }
+    }
+    __syncthreads();
+    // C: trailing update of rows / columns >= j0 + NB, 4x4 tiles
+    {
+      const int b0 = j0 + NB, nt = (n - b0) / 4, ntiles = nt * (nt + 1) / 2;
+#pragma unroll 1
+      for (int tile = t; tile < ntiles; tile += CTH) {
+        int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
+        while ((I + 1) * (I + 2) / 2 <= tile) ++I;
+        while (I * (I + 1) / 2 > tile) --I;
+        const int Jt = tile - I * (I + 1) / 2;
+        const int i0 = b0 + 4 * I, c0 = b0 + 4 * Jt;
+        double acc[4][4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) acc[r][c] = 0.0;
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+          double li[4], lc[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) li[r] = s.u.Mp[L::pidx(i0 + r, j0 + q)];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) lc[c] = s.u.Mp[L::pidx(c0 + c, j0 + q)];
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[r][c] += li[r] * lc[c];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            if (i0 + r >= c0 + c) s.u.Mp[L::pidx(i0 + r, c0 + c)] -= acc[r][c];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Solve M x = s.rhs with the factor of casc_cholesky -> s.dz.  Wave 0, lanes own rows lane
+// and lane + 64; each step's factor column is loaded one step ahead (off the dependency
+// chain), the pivot value is broadcast with v_readlane.
+template <int N, int M>
+__device__ __forceinline__ void casc_tri_solve(CascSmem<N, M>& s) {
+  using L = CL<N, M>;
+  constexpr int n = L::n;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  if (wave == 0) {
+    // branch-free: every lane loads every step (a clamped, valid address) and selects, so
+    // the next column's loads stay in flight across the dependency chain
+    const int i0 = lane, i1 = lane + 64 < n ? lane + 64 : n - 1;
+    const bool has1 = lane + 64 < n;
+    double y0 = s.rhs[i0], y1 = has1 ? s.rhs[i1] : 0.0;
+    const double d0 = s.invd[i0], d1 = s.invd[i1];
+    auto lowc = [&](int i, int j) -> double {  // L[i][j] for i > j, else 0
+      const double v = s.u.Mp[L::pidx(i > j ? i : j, j)];
+      return i > j ? v : 0.0;
+    };
+    // L y = b
+    double l0 = lowc(i0, 0), l1 = has1 ? lowc(i1, 0) : 0.0;
+#pragma unroll 2
+    for (int j = 0; j < n; ++j) {
+      const int jn = j + 1 < n ? j + 1 : j;
+      const double n0 = lowc(i0, jn), n1 = has1 ? lowc(i1, jn) : 0.0;
+      double yj;
+      if (j < 64) {
+        y0 = (i0 == j) ? y0 * d0 : y0;
+        yj = readlane_d(y0, j);
+      } else {
+        y1 = (lane + 64 == j) ? y1 * d1 : y1;
+        yj = readlane_d(y1, j - 64);
+      }
+      y0 -= l0 * yj;
+      y1 -= l1 * yj;
+      l0 = n0;
+      l1 = n1;
+    }
+    // L' x = y: column i of row j is L[j][i] (j > i)
+    auto uppc = [&](int j, int i) -> double {  // L[j][i] for j > i, else 0
+      const double v = s.u.Mp[L::pidx(j, i < j ? i : j)];
+      return i < j ? v : 0.0;
+    };
+    l0 = uppc(n - 1, i0);
+    l1 = has1 ? uppc(n - 1, i1) : 0.0;
+#pragma unroll 2
+    for (int j = n - 1; j >= 0; --j) {
+      const int jn = j > 0 ? j - 1 : 0;
+      const double n0 = uppc(jn, i0), n1 = has1 ? uppc(jn, i1) : 0.0;
+      double xj;
+      if (j < 64) {
+        y0 = (i0 == j) ? y0 * d0 : y0;
+        xj = readlane_d(y0, j);
+      } else {
+        y1 = (lane + 64 == j) ? y1 * d1 : y1;
+        xj = readlane_d(y1, j - 64);
+      }
+      y0 -= l0 * xj;
+      y1 -= l1 * xj;
+      l0 = n0;
+      l1 = n1;
+    }
+    s.dz[i0] = y0;
+    if (has1) s.dz[i1] = y1;
+  }
+  __syncthreads();
+}
+
+// Section timing (debug builds only, -DVC_TIMING, `make timing`): thread 0's s_memtime stamps,
+// accumulated per section and written to diag[b][4 + slot] (scripts/casc_phase_timing.py).
+enum { CT_PRED = 0, CT_LIN, CT_COND, CT_SETUP, CT_LOCAL, CT_RD, CT_WASM, CT_BUILD, CT_CHOL, CT_SOLVE, CT_DIR,
+       CT_UPD, CT_TOTAL, CT_NSLOT };
+#ifdef VC_TIMING
+#define CT_STAMP(var)                                \
+  __builtin_amdgcn_sched_barrier(0);                 \
+  const uint64_t var = __builtin_amdgcn_s_memtime(); \
+  __builtin_amdgcn_sched_barrier(0);
+#define CT_ACC(slot, t0)                               \
+  {                                                    \
+    __builtin_amdgcn_sched_barrier(0);                 \
+    tacc[slot] += __builtin_amdgcn_s_memtime() - (t0); \
+    __builtin_amdgcn_sched_barrier(0);                 \
+  }
+#else
+#define CT_STAMP(var)
+#define CT_ACC(slot, t0)
+#endif
+
 template <int N, int M, int TYRE>
 __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
   using L = CL<N, M>;
@@ -136,6 +495,10 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
     s.ub[i][1] = A.ubar[((size_t)b * H + i) * 2 + 1];
   }
   if (t < 8) s.xs[0][t] = A.x0[(size_t)b * 8 + t];
+#ifdef VC_TIMING
+  uint64_t tacc[CT_NSLOT] = {};
+  const uint64_t t_start = __builtin_amdgcn_s_memtime();
+#endif
   if (t == 0) {
     s.flag[0] = VC_SOLVED;
     s.flag[1] = 0;  // interior-point iterations, summed
@@ -266,8 +629,11 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
 
   int sqp_done = 0;
   for (int it = 0; it < W.sqp_iters; ++it) {
+    CT_STAMP(t_p0)
     predict();
     __syncthreads();
+    CT_ACC(CT_PRED, t_p0)
+    CT_STAMP(t_l0)
     if (s.flag[0] == VC_NONFINITE) break;
 
     // ---------------- linearize ----------------
@@ -278,8 +644,10 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
       for (int i = 0; i < 8; ++i) x[i] = D1(s.xs[k][i]);
       u2[0] = D1(s.ub[k][0]);
       u2[1] = D1(s.ub[k][1]);
-      if (q < 8) x[q].d[0] = 1.0;
-      else u2[q - 8].d[0] = 1.0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) x[i].d[0] = (i == q) ? 1.0 : 0.0;
+      u2[0].d[0] = (q == 8) ? 1.0 : 0.0;
+      u2[1].d[0] = (q == 9) ? 1.0 : 0.0;
       const D1 kp(s.kap[k]);
       rk4_apply<D1, 8>(x, D1(s.dsv[k]), [&](const D1* xx, D1* f) { dyn_spatial_ode<D1, double>(xx, u2, kp, c, f); }, xn);
 #pragma unroll
@@ -292,8 +660,10 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
       for (int i = 0; i < 5; ++i) x[i] = D1(s.xp[m][i]);
       u2[0] = D1(s.ub[j][0]);
       u2[1] = D1(s.ub[j][1]);
-      if (q < 5) x[q].d[0] = 1.0;
-      else u2[q - 5].d[0] = 1.0;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) x[i].d[0] = (i == q) ? 1.0 : 0.0;
+      u2[0].d[0] = (q == 5) ? 1.0 : 0.0;
+      u2[1].d[0] = (q == 6) ? 1.0 : 0.0;
       pm_spatial_ode<D1, double>(x, u2, D1(s.kap[j]), c, f);
       const double h = s.dsv[j];
 #pragma unroll
@@ -321,12 +691,15 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) X5[i] = D1(s.xs[N - 1][i]);
       X5[4] = D1(s.ub[N - 1][0]);
-      X5[q].d[0] = 1.0;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) X5[i].d[0] = (i == q) ? 1.0 : 0.0;
       const D1 fy = dyn_lateral_sum<D1, double>(X5, c);
       s.sc[1 + q] = fy.d[0];
       if (q == 0) s.sc[0] = fy.v;
     }
     __syncthreads();
+    CT_ACC(CT_LIN, t_l0)
+    CT_STAMP(t_c0)
 
     // ---------------- condense (thread j = decision column) ----------------
     if (t < n) {
@@ -407,6 +780,8 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
       }
     }
     __syncthreads();
+    CT_ACC(CT_COND, t_c0)
+    CT_STAMP(t_s0)
 
     // ---------------- QP setup ----------------
     // rows and stage costs: 4 lanes per stage k = t / 4 (t < 4H), lane q = t % 4
@@ -440,7 +815,8 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) X5[i] = D2(s.xs[k][i]);
         X5[4] = D2(s.ub[k][0]);
-        X5[q].d[0] = 1.0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) X5[i].d[0] = (i == q) ? 1.0 : 0.0;
         X5[4].d[1] = 1.0;
         D2 o[7];
         dyn_stage_terms<D2, double>(X5, c, o);
@@ -554,6 +930,16 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
         }
       }
     }
+    // distribute the stage cost Hessian over the quad: lane q keeps packed entries 7q..7q+6
+    double Qd[7];
+    {
+      const int qb = lane & ~3;
+#pragma unroll
+      for (int e = 0; e < 28; ++e) {
+        const double v = __shfl(Qp[e], qb, 64);
+        if (e / 7 == q) Qd[e % 7] = v;
+      }
+    }
     // constant gradient part gp (slews, switching residuals, terminal epsi and time)
     const double csw = CW.w_switch / s.dsv[N - 1];
     const double r_lat = s.ub[N][1] - s.sc[0];
@@ -588,60 +974,12 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
       if (j < 2 * (H - 1)) v += 2.0 * W.w_epsi * s.G[L::T0 + j] * s.ex[1];
       return v;
     };
-    // normal matrix: M = P + sum_k V_k' W_k V_k (W_k in s.W)
-    auto build = [&]() {
-      for (int j = wave; j < n; j += 4) {
-        const double aj = j < 2 * N + 2 ? s.G[L::SW0 + j] : 0.0;
-        const double ej = j < 2 * (H - 1) ? s.G[L::T0 + j] : 0.0;
-        const double cj = pair_w(j), cb = j >= 2 ? pair_w(j - 2) : 0.0;
-        for (int i = j + lane; i < n; i += 64) {
-          double v = 0.0;
-          if (i < 2 * N + 2) v += 2.0 * csw * s.G[L::SW0 + i] * aj;
-          if (i < 2 * (H - 1)) v += 2.0 * W.w_epsi * s.G[L::T0 + i] * ej;
-          if (i == j) v += 2.0 * A.qp.prox + cj + cb;
-          if (i == j + 2) v -= cj;
-          s.u.Mp[L::pidx(i, j)] = v;
-        }
-      }
-      __syncthreads();
-      if (t < 4 * (n / 2)) {
-        const int p = t >> 2, sub = t & 3;
-#pragma unroll 1
-        for (int pass = 0; pass < 2; ++pass) {
-          const int j = pass == 0 ? p : n - 1 - p;
-          const int kj = j >> 1;
-#pragma unroll 1
-          for (int kk = kj; kk < H; ++kk) {
-            double vj[7], hv[7];
-            vcol(kk, j, vj);
-            const double* Wk = s.W[kk];
-#pragma unroll
-            for (int a = 0; a < 7; ++a) {
-              double acc = 0.0;
-#pragma unroll
-              for (int e = 0; e < 7; ++e) acc += Wk[a <= e ? sym7(a, e) : sym7(e, a)] * vj[e];
-              hv[a] = acc;
-            }
-            const int iend = 2 * kk + 2;
-#pragma unroll 1
-            for (int i = j + sub; i < iend; i += 4) {
-              double vi[7];
-              vcol(kk, i, vi);
-              double acc = 0.0;
-#pragma unroll
-              for (int a = 0; a < 7; ++a) acc += vi[a] * hv[a];
-              s.u.Mp[L::pidx(i, j)] += acc;
-            }
-          }
-        }
-      }
-      __syncthreads();
-    };
+    auto build = [&]() { casc_build<N, M>(s, csw, W.w_epsi, A.qp.prox, W.w_Fx, CW.w_Fy, CW.w_switch, S); };
 
     if (A.mode == 1) {  // first QP's H and g (vc_condense)
       if (stl && q == 0) {
 #pragma unroll
-        for (int e = 0; e < 28; ++e) s.W[k][e] = Qp[e];
+        for (int e = 0; e < 28; ++e) s.W[k][e] = __shfl(Qp[e], lane & ~3, 64);
 #pragma unroll
         for (int e = 0; e < 7; ++e) s.R[k][e] = qv[e];
       }
@@ -663,10 +1001,12 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
       lm3[i] = R3.act[i] > 0 ? 1.0 : 0.0;
     }
     const double m_act = block_reduce<0>(R3.act[0] + R3.act[1] + R3.act[2], s.red);
+    CT_ACC(CT_SETUP, t_s0)
     int ipm_it = 0;
     bool conv = false, fail = false;
     __syncthreads();
     for (ipm_it = 0; ipm_it < A.qp.max_iter; ++ipm_it) {
+      CT_STAMP(t_i0)
       stage_local(s.z);
       double pxj = 0.0;
       if (t < n) pxj = px(s.z, t);
@@ -674,12 +1014,26 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
 #pragma unroll
       for (int e = 0; e < 7; ++e) Yk[e] = s.Y[k][e];
       double qy[7];
+      {
+        double pq[7];
 #pragma unroll
-      for (int a = 0; a < 7; ++a) {
-        double acc = qv[a];
+        for (int a = 0; a < 7; ++a) pq[a] = 0.0;
 #pragma unroll
-        for (int e = 0; e < 7; ++e) acc += Qp[a <= e ? sym7(a, e) : sym7(e, a)] * Yk[e];
-        qy[a] = acc;
+        for (int a = 0; a < 7; ++a)
+#pragma unroll
+          for (int e = a; e < 7; ++e) {
+            const int id = sym7(a, e);
+            const double v = (id / 7 == q) ? Qd[id % 7] : 0.0;
+            pq[a] += v * Yk[e];
+            if (e != a) pq[e] += v * Yk[a];
+          }
+#pragma unroll
+        for (int a = 0; a < 7; ++a) {
+          double v = pq[a];
+          v += __shfl_xor(v, 1, 64);
+          v += __shfl_xor(v, 2, 64);
+          qy[a] = v + qv[a];  // qv is nonzero on lane 0 only: stage_vec's quad sum must not add it again
+        }
       }
       double rp3[3], Dg3[3];
       double smu = 0.0, rpm = 0.0;
@@ -713,86 +1067,41 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
         }
         __syncthreads();
       };
+      CT_ACC(CT_LOCAL, t_i0)
+      CT_STAMP(t_r0)
       stage_vec(lm3);
       double rdm = 0.0;
       if (t < n) rdm = fabs(adjoint(t) + pxj + s.gp[t]);
       const double rd_inf = block_reduce<1>(rdm, s.red);
       if (!(mu == mu) || !(rd_inf == rd_inf)) { fail = true; break; }
+      CT_ACC(CT_RD, t_r0)
       if (mu <= A.qp.tol && rp_inf <= 10.0 * A.qp.tol && rd_inf <= 10.0 * A.qp.tol) { conv = true; break; }
+      CT_STAMP(t_w0)
       // W_k = Q_k + sum_i D_i c_i c_i'
-      {
-        double wk[28];
 #pragma unroll
-        for (int a = 0; a < 7; ++a)
+      for (int a = 0; a < 7; ++a)
 #pragma unroll
-          for (int e = a; e < 7; ++e) {
-            double v = 0.0;
+        for (int e = a; e < 7; ++e) {
+          const int id = sym7(a, e);
+          double v = 0.0;
 #pragma unroll
-            for (int i = 0; i < 3; ++i) v += Dg3[i] * R3.c[i][a] * R3.c[i][e];
-            v += __shfl_xor(v, 1, 64);
-            v += __shfl_xor(v, 2, 64);
-            wk[sym7(a, e)] = v + Qp[sym7(a, e)];
-          }
-        if (stl && q == 0) {
-#pragma unroll
-          for (int e = 0; e < 28; ++e) s.W[k][e] = wk[e];
+          for (int i = 0; i < 3; ++i) v += Dg3[i] * R3.c[i][a] * R3.c[i][e];
+          v += __shfl_xor(v, 1, 64);
+          v += __shfl_xor(v, 2, 64);
+          if (stl && id / 7 == q) s.W[k][id] = v + Qd[id % 7];
         }
-      }
       __syncthreads();
+      CT_ACC(CT_WASM, t_w0)
+      CT_STAMP(t_b0)
       build();
-      // Cholesky, right-looking, 2 barriers per column; column j is scaled one step later
-      if (t == 0) s.flag[3] = 0;
-      for (int j = 0; j < n; ++j) {
-        if (t == 0) {
-          const double dj = s.u.Mp[L::pidx(j, j)];
-          if (!(dj > 1e-300)) s.flag[3] = 1;
-          const double dd = dj > 1e-300 ? dj : 1e-300;
-          s.red[4] = 1.0 / dd;
-          s.invd[j] = 1.0 / sqrt(dd);
-        }
-        if (j > 0) {  // scale column j - 1 (L = column / sqrt(pivot))
-          const double sc = s.invd[j - 1];
-          for (int i = j + t; i < n; i += CTH) s.u.Mp[L::pidx(i, j - 1)] *= sc;
-          if (t == 0) s.u.Mp[L::pidx(j - 1, j - 1)] = 1.0 / sc;
-        }
-        __syncthreads();
-        const double inv2 = s.red[4];
-        for (int cc = j + 1 + wave; cc < n; cc += 4) {
-          const double lc = s.u.Mp[L::pidx(cc, j)] * inv2;
-          for (int i = cc + lane; i < n; i += 64) s.u.Mp[L::pidx(i, cc)] -= s.u.Mp[L::pidx(i, j)] * lc;
-        }
-        __syncthreads();
-      }
-      if (t == 0) s.u.Mp[L::pidx(n - 1, n - 1)] = 1.0 / s.invd[n - 1];
-      __syncthreads();
+      CT_ACC(CT_BUILD, t_b0)
+      CT_STAMP(t_h0)
+      casc_cholesky<N, M>(s);
+      CT_ACC(CT_CHOL, t_h0)
       if (s.flag[3]) { fail = true; break; }
 
       // solve M dz = rhs (in s.rhs) -> s.dz; wave 0, lanes own rows lane and lane + 64
-      auto chol_solve = [&]() {
-        if (wave == 0) {
-          const int i0 = lane, i1 = lane + 64;
-          double y0 = s.rhs[i0], y1 = i1 < n ? s.rhs[i1] : 0.0;
-          for (int j = 0; j < n; ++j) {  // L y = b
-            const double own = j < 64 ? y0 : y1;
-            const double yj = __shfl(own, j & 63, 64) * s.invd[j];
-            if (j < 64) { if (i0 == j) y0 = yj; }
-            else if (i1 == j) y1 = yj;
-            if (i0 > j) y0 -= s.u.Mp[L::pidx(i0, j)] * yj;
-            if (i1 > j && i1 < n) y1 -= s.u.Mp[L::pidx(i1, j)] * yj;
-          }
-          for (int j = n - 1; j >= 0; --j) {  // L' x = y
-            const double own = j < 64 ? y0 : y1;
-            const double xj = __shfl(own, j & 63, 64) * s.invd[j];
-            if (j < 64) { if (i0 == j) y0 = xj; }
-            else if (i1 == j) y1 = xj;
-            if (i0 < j) y0 -= s.u.Mp[L::pidx(j, i0)] * xj;
-            if (i1 < j) y1 -= s.u.Mp[L::pidx(j, i1)] * xj;
-          }
-          s.dz[i0] = y0;
-          if (i1 < n) s.dz[i1] = y1;
-        }
-        __syncthreads();
-      };
+      auto chol_solve = [&]() { casc_tri_solve<N, M>(s); };
       // Newton direction for a given w (per row): rhs = -(adjoint(QY + q + sum (lam + w) c) + Px + gp)
       auto direction = [&](const double* w3, double* dsl, double* dlm) {
         double lw[3];
@@ -801,7 +1110,9 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
         stage_vec(lw);
         if (t < n) s.rhs[t] = -(adjoint(t) + pxj + s.gp[t]);
         __syncthreads();
+        CT_STAMP(t_v0)
         chol_solve();
+        CT_ACC(CT_SOLVE, t_v0)
         stage_local(s.dz);
         double Yd[7];
 #pragma unroll
@@ -826,6 +1137,7 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
         }
         return block_reduce<2>(a, s.red);
       };
+      CT_STAMP(t_d0)
       // predictor (affine)
       double w3[3], dsa[3], dla[3];
 #pragma unroll
@@ -853,15 +1165,13 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
       }
       if (t < n) s.z[t] += al * s.dz[t];
       __syncthreads();
+      CT_ACC(CT_DIR, t_d0)
     }
     if (t == 0) {
       s.flag[1] += ipm_it;
       if (fail) { s.flag[0] = VC_NONFINITE; s.flag[2] = 1; }
       else if (!conv) { if (s.flag[0] == VC_SOLVED) s.flag[0] = VC_MAX_ITER; s.flag[2] &= ~2; }
-      if (A.diag) {
-        A.diag[(size_t)b * 4 + 0] = 0.0;
-        A.diag[(size_t)b * 4 + 1] = 0.0;
-      }
+
     }
     if (fail) { __syncthreads(); break; }
     // update ubar (scaled back)
@@ -896,8 +1206,17 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
     A.status[b] = s.flag[0];
     A.iters[b] = s.flag[1];
     if (A.diag) {
-      A.diag[(size_t)b * 4 + 2] = s.flag[2];
-      A.diag[(size_t)b * 4 + 3] = sqp_done;
+#ifdef VC_TIMING
+      constexpr int DS = 4 + CT_NSLOT;
+      tacc[CT_TOTAL] = __builtin_amdgcn_s_memtime() - t_start;
+      for (int i = 0; i < CT_NSLOT; ++i) A.diag[(size_t)b * DS + 4 + i] = double(tacc[i]);
+#else
+      constexpr int DS = 4;
+#endif
+      A.diag[(size_t)b * DS + 0] = 0.0;
+      A.diag[(size_t)b * DS + 1] = 0.0;
+      A.diag[(size_t)b * DS + 2] = s.flag[2];
+      A.diag[(size_t)b * DS + 3] = sqp_done;
     }
   }
 }

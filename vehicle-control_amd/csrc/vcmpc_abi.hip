@@ -19,9 +19,11 @@
 #ifdef VC_TIMING
 #define VC_DIAG_COLS 13      // 4 diagnostics + 9 section-cycle counters (kin_ltv.hip T_*)
 #define VC_DYN_DIAG_COLS 19  // 4 diagnostics + 15 section-cycle counters (dyn_sqp.hip DT_*)
+#define VC_CASC_DIAG_COLS 17 // 4 diagnostics + 13 section-cycle counters (casc_sqp.hip CT_*)
 #else
 #define VC_DIAG_COLS 4
 #define VC_DYN_DIAG_COLS 4
+#define VC_CASC_DIAG_COLS 4
 #endif
 
 struct vc_ctx {
@@ -167,7 +169,7 @@ int casc_solve(vc_ctx* c, int B, const void* x0, const void* kappa, const void* 
                {nullptr, u0, (size_t)B * nu * 8, nullptr},
                {nullptr, status, (size_t)B * 4, nullptr},
                {nullptr, iters, (size_t)B * 4, nullptr},
-               {nullptr, diag, diag ? (size_t)B * 4 * 8 : 0, nullptr}};
+               {nullptr, diag, diag ? (size_t)B * VC_CASC_DIAG_COLS * 8 : 0, nullptr}};
     } else {
       slots = {{x0, nullptr, (size_t)B * nx * 8, nullptr},
                {kappa, nullptr, (size_t)B * Hs * 8, nullptr},

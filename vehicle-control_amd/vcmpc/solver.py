@@ -142,7 +142,8 @@ class Context:
         if diag is not None and diag is not False:
             if diag is True:
                 diag = self._like(x0, (B, 4))
-            ptrs, flags = self._marshal(bufs + [diag], shapes + [(B, 4)], dts + [f])
+            # [B, 4]; timing builds (libvcmpc_timing.so) append section-cycle columns
+            ptrs, flags = self._marshal(bufs + [diag], shapes + [(B, int(diag.shape[1]))], dts + [f])
             self._check(self.lib.vc_solve_diag(self._h, B, *ptrs, flags))
             return u0, xbar, ubar, status, iters, diag
         ptrs, flags = self._marshal(bufs, shapes, dts)
