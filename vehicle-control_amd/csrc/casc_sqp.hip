@@ -385,67 +385,94 @@ __device__ __forceinline__ void casc_cholesky(CascSmem<N, M>& s) {
   }
 }
 
-// Solve M x = s.rhs with the factor of casc_cholesky -> s.dz.  Wave 0, lanes own rows lane
-// and lane + 64; each step's factor column is loaded one step ahead (off the dependency
-// chain), the pivot value is broadcast with v_readlane.
+// Solve M x = s.rhs with the factor of casc_cholesky -> s.dz.  Wave 0 alone (no barriers):
+// lanes own rows lane and lane + 64.  The sweeps run in 8-column blocks whose factor
+// entries sit in registers, and the NEXT block's 16 entries per lane are loaded before the
+// current block's 8 dependent steps, so LDS latency stays off the pivot chain; each pivot
+// is broadcast with v_readlane.  Blocks never straddle the lane / lane + 64 split.
 template <int N, int M>
 __device__ __forceinline__ void casc_tri_solve(CascSmem<N, M>& s) {
   using L = CL<N, M>;
-  constexpr int n = L::n;
+  constexpr int n = L::n, NB = 8;
+  static_assert(n % NB == 0 && 64 % NB == 0 && n > 64 && n <= 128, "tri solve layout");
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   if (wave == 0) {
-    // branch-free: every lane loads every step (a clamped, valid address) and selects, so
-    // the next column's loads stay in flight across the dependency chain
     const int i0 = lane, i1 = lane + 64 < n ? lane + 64 : n - 1;
     const bool has1 = lane + 64 < n;
     double y0 = s.rhs[i0], y1 = has1 ? s.rhs[i1] : 0.0;
     const double d0 = s.invd[i0], d1 = s.invd[i1];
-    auto lowc = [&](int i, int j) -> double {  // L[i][j] for i > j, else 0
-      const double v = s.u.Mp[L::pidx(i > j ? i : j, j)];
-      return i > j ? v : 0.0;
+    // addresses: column j starts at the wave-uniform pidx(j, j); row j of column i (i < j)
+    // is at rb_i + j with the lane constant rb_i = pidx(i, i) - i -- one add per load
+    auto lowc = [&](int i, int j) -> double {  // L[i][j] for i > j, else 0 (clamped address)
+      const int d = i - j;
+      const double v = s.u.Mp[L::pidx(j, j) + (d > 0 ? d : 0)];
+      return d > 0 ? v : 0.0;
     };
-    // L y = b
-    double l0 = lowc(i0, 0), l1 = has1 ? lowc(i1, 0) : 0.0;
-#pragma unroll 2
-    for (int j = 0; j < n; ++j) {
-      const int jn = j + 1 < n ? j + 1 : j;
-      const double n0 = lowc(i0, jn), n1 = has1 ? lowc(i1, jn) : 0.0;
-      double yj;
-      if (j < 64) {
-        y0 = (i0 == j) ? y0 * d0 : y0;
-        yj = readlane_d(y0, j);
+    const int rb0 = L::pidx(i0, i0) - i0, rb1 = L::pidx(i1, i1) - i1;
+    auto uppc0 = [&](int j) -> double {  // L[j][i0] for j > i0, else 0
+      const double v = s.u.Mp[j > i0 ? rb0 + j : 0];
+      return j > i0 ? v : 0.0;
+    };
+    auto uppc1 = [&](int j) -> double {  // L[j][i1] for j > i1, else 0
+      const double v = s.u.Mp[j > i1 ? rb1 + j : 0];
+      return (j > i1 && has1) ? v : 0.0;
+    };
+    double c0[NB], c1[NB], n0[NB], n1[NB];
+    // L y = b: step j scales y_j by 1 / L_jj, then y_i -= L[i][j] y_j for i > j
+#pragma unroll
+    for (int q = 0; q < NB; ++q) { c0[q] = lowc(i0, q); c1[q] = has1 ? lowc(i1, q) : 0.0; }
+#pragma unroll 1
+    for (int j0 = 0; j0 < n; j0 += NB) {
+      const int jn = j0 + NB < n ? j0 + NB : j0;
+#pragma unroll
+      for (int q = 0; q < NB; ++q) { n0[q] = lowc(i0, jn + q); n1[q] = has1 ? lowc(i1, jn + q) : 0.0; }
+      if (j0 < 64) {
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+          y0 = (i0 == j0 + q) ? y0 * d0 : y0;
+          const double yj = readlane_d(y0, j0 + q);
+          y0 -= c0[q] * yj;
+          y1 -= c1[q] * yj;
+        }
       } else {
-        y1 = (lane + 64 == j) ? y1 * d1 : y1;
-        yj = readlane_d(y1, j - 64);
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+          y1 = (i1 == j0 + q && has1) ? y1 * d1 : y1;
+          const double yj = readlane_d(y1, j0 + q - 64);
+          y0 -= c0[q] * yj;
+          y1 -= c1[q] * yj;
+        }
       }
-      y0 -= l0 * yj;
-      y1 -= l1 * yj;
-      l0 = n0;
-      l1 = n1;
+#pragma unroll
+      for (int q = 0; q < NB; ++q) { c0[q] = n0[q]; c1[q] = n1[q]; }
     }
-    // L' x = y: column i of row j is L[j][i] (j > i)
-    auto uppc = [&](int j, int i) -> double {  // L[j][i] for j > i, else 0
-      const double v = s.u.Mp[L::pidx(j, i < j ? i : j)];
-      return i < j ? v : 0.0;
-    };
-    l0 = uppc(n - 1, i0);
-    l1 = has1 ? uppc(n - 1, i1) : 0.0;
-#pragma unroll 2
-    for (int j = n - 1; j >= 0; --j) {
-      const int jn = j > 0 ? j - 1 : 0;
-      const double n0 = uppc(jn, i0), n1 = has1 ? uppc(jn, i1) : 0.0;
-      double xj;
-      if (j < 64) {
-        y0 = (i0 == j) ? y0 * d0 : y0;
-        xj = readlane_d(y0, j);
+    // L' x = y: descending j, x_j = y_j / L_jj, then y_i -= L[j][i] x_j for i < j
+#pragma unroll
+    for (int q = 0; q < NB; ++q) { c0[q] = uppc0(n - 1 - q); c1[q] = uppc1(n - 1 - q); }
+#pragma unroll 1
+    for (int j0 = n - 1; j0 > 0; j0 -= NB) {  // block covers j0, j0 - 1, ..., j0 - NB + 1
+      const int jn = j0 - NB > 0 ? j0 - NB : j0;
+#pragma unroll
+      for (int q = 0; q < NB; ++q) { n0[q] = uppc0(jn - q); n1[q] = uppc1(jn - q); }
+      if (j0 >= 64) {
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+          y1 = (i1 == j0 - q && has1) ? y1 * d1 : y1;
+          const double xj = readlane_d(y1, j0 - q - 64);
+          y0 -= c0[q] * xj;
+          y1 -= c1[q] * xj;
+        }
       } else {
-        y1 = (lane + 64 == j) ? y1 * d1 : y1;
-        xj = readlane_d(y1, j - 64);
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+          y0 = (i0 == j0 - q) ? y0 * d0 : y0;
+          const double xj = readlane_d(y0, j0 - q);
+          y0 -= c0[q] * xj;
+          y1 -= c1[q] * xj;
+        }
       }
-      y0 -= l0 * xj;
-      y1 -= l1 * xj;
-      l0 = n0;
-      l1 = n1;
+#pragma unroll
+      for (int q = 0; q < NB; ++q) { c0[q] = n0[q]; c1[q] = n1[q]; }
     }
     s.dz[i0] = y0;
     if (has1) s.dz[i1] = y1;
@@ -1075,7 +1102,10 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
       const double rd_inf = block_reduce<1>(rdm, s.red);
       if (!(mu == mu) || !(rd_inf == rd_inf)) { fail = true; break; }
       CT_ACC(CT_RD, t_r0)
-      if (mu <= A.qp.tol && rp_inf <= 10.0 * A.qp.tol && rd_inf <= 10.0 * A.qp.tol) { conv = true; break; }
+      // mu carries the accuracy (tol = 1e-13); the residuals only need to be small in the
+      // scaled units (|dz| ~ 1), a 1e-12 absolute dual residual is below fp64 resolution of
+      // adjoint sums of magnitude ~1e3 and left 1 % of problems at max_iter
+      if (mu <= A.qp.tol && rp_inf <= 1e-9 && rd_inf <= 1e-9) { conv = true; break; }
       CT_STAMP(t_w0)
       // W_k = Q_k + sum_i D_i c_i c_i'
 #pragma unroll
