@@ -5,7 +5,8 @@
 // (controllers/mpc/cascaded_mpc.py:17-39,91-304, config/controllers/cascaded.yaml: N = 20
 // single-track stages, M = 40 point-mass stages every ds_pm = 3 m).  Contract:
 // oracle/casc_sqp.py.  Per SQP iteration:
-//   predict    thread 0: single-track RK4 (vc_models.hpp dyn_spatial_ode), switching map
+//   predict    thread 0: single-track RK4 (vc_models.hpp dyn_spatial_ode_alg: the same model
+//              in tan(alpha), no atan / tan), switching map
 //              st_to_pm, point-mass Euler (pm_spatial_ode)
 //   linearize  one thread per (stage, seed): Dual<1, double> evaluation of the same step
 //              code gives one column of [A B]; the switch Jacobian analytically; the
@@ -543,7 +544,7 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
         const double u2[2] = {s.ub[k][0], s.ub[k][1]};
         const double kp = s.kap[k];
         double xn[8];
-        rk4_apply<double, 8>(x, s.dsv[k], [&](const double* xx, double* f) { dyn_spatial_ode<double, double>(xx, u2, kp, c, f); }, xn);
+        rk4_apply<double, 8>(x, s.dsv[k], [&](const double* xx, double* f) { dyn_spatial_ode_alg<double, double>(xx, u2, kp, c, f); }, xn);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           x[i] = xn[i];
@@ -654,14 +655,16 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
     return 2.0 * w * S * S;
   };
 
+  // one predict call site (the final pass is the output rollout x* = rollout(u*)): a second
+  // call site made the compiler outline the rollout, and the call spilled ~400 VGPRs
   int sqp_done = 0;
-  for (int it = 0; it < W.sqp_iters; ++it) {
+  for (int it = 0;; ++it) {
     CT_STAMP(t_p0)
     predict();
     __syncthreads();
     CT_ACC(CT_PRED, t_p0)
     CT_STAMP(t_l0)
-    if (s.flag[0] == VC_NONFINITE) break;
+    if (it == W.sqp_iters || s.flag[0] == VC_NONFINITE) break;
 
     // ---------------- linearize ----------------
     if (t < (N - 1) * 10) {
@@ -1214,11 +1217,7 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
     ++sqp_done;
   }
 
-  // outputs: u*, x* = rollout(u*), u0, status, iterations
-  if (s.flag[0] != VC_NONFINITE) {
-    predict();
-    __syncthreads();
-  }
+  // outputs: u*, x* = rollout(u*) (the loop's last predict), u0, status, iterations
   for (int i = t; i < H; i += CTH) {
     A.u_out[((size_t)b * H + i) * 2] = s.ub[i][0];
     A.u_out[((size_t)b * H + i) * 2 + 1] = s.ub[i][1];

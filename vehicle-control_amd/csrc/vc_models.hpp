@@ -304,7 +304,7 @@ struct DynForcesAlg {
 template <typename T, typename R>
 __host__ __device__ inline T fiala_fy_alg(T ta, R Ca, T Fymax, R tam_k, R fi1, R fi2) {
   const T q = (T(Ca) * ta) / Fymax;
-  const T inside = T(Ca) * ta * (T(-1) + vfabs(q) * T(1.f / 3.f) - q * q * T(1.f / 27.f));
+  const T inside = T(Ca) * ta * (T(-1) + vfabs(q) * T(R(1) / R(3)) - q * q * T(R(1) / R(27)));
   const T sg = ta > T(0) ? T(1) : (ta < T(0) ? T(-1) : T(0));
   const T outside = -T(Ca * fi1) * ta - Fymax * T(fi2) * sg;
   return vfabs(ta) <= Fymax * T(tam_k) ? inside : outside;
