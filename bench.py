@@ -137,6 +137,42 @@ def cpu_baseline(batch, sample):
                       f"numpy fp64, 1 thread) in {dt:.2f} s on {cpu}"}
 
 
+def _oracle_chunk(chunk):
+    """Pool worker: one oracle pass over a chunk of C2 problems, one thread."""
+    from threadpoolctl import threadpool_limits
+
+    from oracle import ltv_qp as Q
+    from vcmpc.config import load_config
+    if chunk is None:  # warm-up: imports only
+        return 0.0
+    W = Q.kin_weights(load_config("kinematic_mpc"))
+    with threadpool_limits(limits=1):
+        Q.kin_ltv_solve(chunk["x0"], chunk["ubar"], chunk["kappa"], chunk["ds"], 2.5, W)
+    return float(len(chunk["x0"]))
+
+
+def cpu_baseline_all_cores(batch, sample, workers=16):
+    """SURVEY 8(d)'s second CPU figure: the same oracle pass with one single-threaded
+    process per core (`workers` processes; 16 = this pool's CPU share per GPU box).
+    Spawned children (fresh interpreters, no forked HIP state); interpreter start-up and
+    imports are excluded by a warm-up map before the timed one."""
+    import multiprocessing as mp
+
+    import numpy as np
+    d = {k: v[:sample] for k, v in batch.items()}
+    n = len(d["x0"])
+    parts = np.array_split(np.arange(n), workers)
+    chunks = [{k: np.ascontiguousarray(v[p]) for k, v in d.items()} for p in parts if len(p)]
+    with mp.get_context("spawn").Pool(len(chunks)) as pool:
+        pool.map(_oracle_chunk, [None] * len(chunks), chunksize=1)
+        t0 = time.perf_counter()
+        done = sum(pool.map(_oracle_chunk, chunks, chunksize=1))
+        dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "solves/s", "cores": len(chunks), "kind": "port",
+            "sample": f"{int(done)} problems of the C2 workload split over {len(chunks)} single-threaded "
+                      f"oracle processes, {dt:.2f} s wall"}
+
+
 def cpu_baseline_c3(data, sample):
     """The fp64 numpy oracle of the SQP contract (oracle/dyn_sqp.py, 3 exact QPs per
     solve), one host thread, on the first `sample` problems of the C3 workload."""
@@ -531,6 +567,10 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(data, min(args.cpu_sample, B))
+            try:
+                out["cpu_baseline_all_cores"] = cpu_baseline_all_cores(data, min(args.cpu_sample, B))
+            except Exception as e:  # reported, never fatal: the GPU numbers stand alone
+                out["cpu_baseline_all_cores"] = {"error": repr(e)}
             if c3_data is not None and "error" not in c3:
                 c3["cpu_baseline"] = cpu_baseline_c3(c3_data, 8)
             if ca_data is not None and "error" not in ca:
