@@ -210,11 +210,11 @@ __device__ __forceinline__ void casc_build(CascSmem<N, M>& s, double csw, double
         for (int kk = 2 * I + 2; kk < N; ++kk) {
           const int len = 2 * kk;
           const double* g = &s.G[L::gst(kk)];
-          double Wg[5][5];
-#pragma unroll
-          for (int a = 0; a < 5; ++a)
-#pragma unroll
-            for (int e = 0; e < 5; ++e) Wg[a][e] = s.W[kk][a <= e ? sym7(a, e) : sym7(e, a)];
+          // W_k entries straight from LDS (one broadcast address for the whole workgroup)
+          // rather than a 25-double register copy: the build runs inside the interior
+          // point, whose per-lane row state is live across it
+          const double* Wk = s.W[kk];
+          auto Wg = [&](int a, int e) -> double { return Wk[a <= e ? sym7(a, e) : sym7(e, a)]; };
           double hv[4][5];
 #pragma unroll
           for (int cc = 0; cc < 4; ++cc) {
@@ -225,7 +225,7 @@ __device__ __forceinline__ void casc_build(CascSmem<N, M>& s, double csw, double
             for (int a = 0; a < 5; ++a) {
               double x = 0.0;
 #pragma unroll
-              for (int e = 0; e < 5; ++e) x += Wg[a][e] * vj[e];
+              for (int e = 0; e < 5; ++e) x += Wg(a, e) * vj[e];
               hv[cc][a] = x;
             }
           }
