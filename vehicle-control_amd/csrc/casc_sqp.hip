@@ -404,44 +404,40 @@ __device__ __forceinline__ void casc_tri_solve(CascSmem<N, M>& s) {
     const double d0 = s.invd[i0], d1 = s.invd[i1];
     // addresses: column j starts at the wave-uniform pidx(j, j); row j of column i (i < j)
     // is at rb_i + j with the lane constant rb_i = pidx(i, i) - i -- one add per load
-    auto lowc = [&](int i, int j) -> double {  // L[i][j] for i > j, else 0 (clamped address)
+    // raw loads at clamped (always valid) addresses, no control flow and no select, so the
+    // next block's 16 loads stay in flight; the structural zeros are applied at the use
+    auto lowc = [&](int i, int j) -> double {  // L[i][j] where i > j
       const int d = i - j;
-      const double v = s.u.Mp[L::pidx(j, j) + (d > 0 ? d : 0)];
-      return d > 0 ? v : 0.0;
+      return s.u.Mp[L::pidx(j, j) + (d > 0 ? d : 0)];
     };
     const int rb0 = L::pidx(i0, i0) - i0, rb1 = L::pidx(i1, i1) - i1;
-    auto uppc0 = [&](int j) -> double {  // L[j][i0] for j > i0, else 0
-      const double v = s.u.Mp[j > i0 ? rb0 + j : 0];
-      return j > i0 ? v : 0.0;
-    };
-    auto uppc1 = [&](int j) -> double {  // L[j][i1] for j > i1, else 0
-      const double v = s.u.Mp[j > i1 ? rb1 + j : 0];
-      return (j > i1 && has1) ? v : 0.0;
-    };
+    auto uppc0 = [&](int j) -> double { return s.u.Mp[j > i0 ? rb0 + j : 0]; };  // L[j][i0] where j > i0
+    auto uppc1 = [&](int j) -> double { return s.u.Mp[j > i1 ? rb1 + j : 0]; };  // L[j][i1] where j > i1
     double c0[NB], c1[NB], n0[NB], n1[NB];
     // L y = b: step j scales y_j by 1 / L_jj, then y_i -= L[i][j] y_j for i > j
 #pragma unroll
-    for (int q = 0; q < NB; ++q) { c0[q] = lowc(i0, q); c1[q] = has1 ? lowc(i1, q) : 0.0; }
+    for (int q = 0; q < NB; ++q) { c0[q] = lowc(i0, q); c1[q] = lowc(i1, q); }
 #pragma unroll 1
     for (int j0 = 0; j0 < n; j0 += NB) {
       const int jn = j0 + NB < n ? j0 + NB : j0;
 #pragma unroll
-      for (int q = 0; q < NB; ++q) { n0[q] = lowc(i0, jn + q); n1[q] = has1 ? lowc(i1, jn + q) : 0.0; }
+      for (int q = 0; q < NB; ++q) { n0[q] = lowc(i0, jn + q); n1[q] = lowc(i1, jn + q); }
       if (j0 < 64) {
 #pragma unroll
         for (int q = 0; q < NB; ++q) {
+          const double l0 = i0 > j0 + q ? c0[q] : 0.0, l1 = i1 > j0 + q ? c1[q] : 0.0;
           y0 = (i0 == j0 + q) ? y0 * d0 : y0;
           const double yj = readlane_d(y0, j0 + q);
-          y0 -= c0[q] * yj;
-          y1 -= c1[q] * yj;
+          y0 -= l0 * yj;
+          y1 -= l1 * yj;
         }
       } else {
 #pragma unroll
         for (int q = 0; q < NB; ++q) {
+          const double l1 = i1 > j0 + q ? c1[q] : 0.0;  // rows i0 < 64 <= j: nothing
           y1 = (i1 == j0 + q && has1) ? y1 * d1 : y1;
           const double yj = readlane_d(y1, j0 + q - 64);
-          y0 -= c0[q] * yj;
-          y1 -= c1[q] * yj;
+          y1 -= l1 * yj;
         }
       }
 #pragma unroll
@@ -458,18 +454,19 @@ __device__ __forceinline__ void casc_tri_solve(CascSmem<N, M>& s) {
       if (j0 >= 64) {
 #pragma unroll
         for (int q = 0; q < NB; ++q) {
+          const double l0 = c0[q], l1 = j0 - q > i1 ? c1[q] : 0.0;  // rows i0 < 64 <= j: all
           y1 = (i1 == j0 - q && has1) ? y1 * d1 : y1;
           const double xj = readlane_d(y1, j0 - q - 64);
-          y0 -= c0[q] * xj;
-          y1 -= c1[q] * xj;
+          y0 -= l0 * xj;
+          y1 -= l1 * xj;
         }
       } else {
 #pragma unroll
         for (int q = 0; q < NB; ++q) {
+          const double l0 = j0 - q > i0 ? c0[q] : 0.0;  // rows i1 >= 64 > j: nothing
           y0 = (i0 == j0 - q) ? y0 * d0 : y0;
           const double xj = readlane_d(y0, j0 - q);
-          y0 -= c0[q] * xj;
-          y1 -= c1[q] * xj;
+          y0 -= l0 * xj;
         }
       }
 #pragma unroll
