@@ -298,7 +298,9 @@ __device__ __forceinline__ void casc_cholesky(CascSmem<N, M>& s) {
       const int p = lane < NB ? lane : 0;
       double a[NB];
 #pragma unroll
-      for (int r = 0; r < NB; ++r) a[r] = (r >= p) ? s.u.Mp[L::pidx(j0 + r, j0 + p)] : 0.0;
+      for (int r = 0; r < NB; ++r) a[r] = s.u.Mp[L::pidx(j0 + (r >= p ? r : p), j0 + p)];  // no branch
+#pragma unroll
+      for (int r = 0; r < NB; ++r) a[r] = r >= p ? a[r] : 0.0;
       bool bad = false;
 #pragma unroll
       for (int q = 0; q < NB; ++q) {
