@@ -306,7 +306,13 @@ __device__ __forceinline__ void casc_cholesky(CascSmem<N, M>& s) {
       for (int q = 0; q < NB; ++q) {
         const double d = readlane_d(a[q], q);
         bad = bad || !(d > 1e-300);
-        const double l = sqrt(d > 1e-300 ? d : 1e-300), il = 1.0 / l;
+        // 1 / sqrt(d): v_rsq_f64 + two Newton steps (full fp64 accuracy; a much shorter
+        // dependent chain than IEEE sqrt then IEEE divide, on every block's serial path)
+        const double dd = d > 1e-300 ? d : 1e-300;
+        double il = __builtin_amdgcn_rsq(dd);
+        il = il * (1.5 - 0.5 * dd * il * il);
+        il = il * (1.5 - 0.5 * dd * il * il);
+        const double l = dd * il;
         if (p == q) {
 #pragma unroll
           for (int r = 0; r < NB; ++r) a[r] = r == q ? l : (r > q ? a[r] * il : a[r]);
