@@ -159,7 +159,7 @@ __device__ __forceinline__ void casc_build(CascSmem<N, M>& s, double csw, double
       for (int pass = 0; pass < 2; ++pass) {
         const int tile = pass == 0 ? t : NTILES - 1 - t;
         if (tile >= NTILES || (pass == 1 && tile < CTH)) continue;
-        int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
+        int I = (int)((sqrtf(8.f * tile + 1.f) - 1.f) * 0.5f);  // fp32 guess, fixed up below
         while ((I + 1) * (I + 2) / 2 <= tile) ++I;
         while (I * (I + 1) / 2 > tile) --I;
         const int J = tile - I * (I + 1) / 2;
@@ -361,7 +361,7 @@ __device__ __forceinline__ void casc_cholesky(CascSmem<N, M>& s) {
       const int b0 = j0 + NB, nt = (n - b0) / 4, ntiles = nt * (nt + 1) / 2;
 #pragma unroll 1
       for (int tile = t; tile < ntiles; tile += CTH) {
-        int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
+        int I = (int)((sqrtf(8.f * tile + 1.f) - 1.f) * 0.5f);  // fp32 guess, fixed up below
         while ((I + 1) * (I + 2) / 2 <= tile) ++I;
         while (I * (I + 1) / 2 > tile) --I;
         const int Jt = tile - I * (I + 1) / 2;
