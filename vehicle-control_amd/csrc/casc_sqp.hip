@@ -20,9 +20,10 @@
 //              the switching residuals and the terminal epsi row.  Four lanes per stage
 //              hold its 12 one-sided rows (3 each); the normal matrix
 //                  M = P + sum_k V_k' (Q_k + C_k' D_k C_k) V_k
-//              is accumulated in LDS (packed lower triangle), factorised by a
-//              right-looking Cholesky (2 barriers per column), and each Mehrotra
-//              predictor / corrector solve is two single-wave triangular sweeps.
+//              is built in LDS (packed lower triangle) from 4x4 register tiles,
+//              factorised by a blocked right-looking Cholesky (8-column blocks, 3
+//              barriers per block), and each Mehrotra predictor / corrector solve is
+//              two single-wave triangular sweeps in register-prefetched 8-column blocks.
 //   update     ubar += dz (scaled back: Fx and the point mass's Fy by fx_scale)
 // LDS: packed normal matrix 58 KB (aliased by the linearisation scratch before the QP),
 // condensed rows 68 KB, stage blocks 13 KB, trajectory and vectors 18 KB.
