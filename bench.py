@@ -107,6 +107,12 @@ def parse():
     ap.add_argument("--no-c5", action="store_true", help="skip the secondary C5 closed-loop measurement")
     ap.add_argument("--casc-batch", type=int, default=4096, help="cascaded NMPC problems per GPU")
     ap.add_argument("--no-casc", action="store_true", help="skip the cascaded (point-mass tail) measurement")
+    ap.add_argument("--c4-total", type=int, default=C4_TOTAL,
+                    help="C4 problems in total, split into contiguous shards over the ranks (config 4: 65536)")
+    ap.add_argument("--no-c4", action="store_true", help="skip the C4 sharded measurement")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU work: each rank only takes its C2/C4/C5 shards and runs the counter "
+                         "collective over gloo (tests the launcher and the rank logic on a CPU host)")
     return ap.parse_args()
 
 
@@ -321,7 +327,7 @@ def run_casc(args, dev, stream, rank, dist, steps):
            "ms_per_step": elapsed_max / steps * 1e3, "dtype": "f64",
            "config": {"workload": f"cascaded NMPC (config/controllers/cascaded.yaml), B={B} per GPU, "
                                   f"H={CA_N}+{CA_M}, fp64, Fiala tyre", "batch_per_gpu": B, "horizon": CA_H},
-           "roofline": {"bound": "mfma", "kernel": "casc_sqp_kernel<20, 40, fiala>", "kernel_ms": kern_ms,
+           "roofline": {"bound": "fp64-valu", "kernel": "casc_sqp_kernel<20, 40, fiala>", "kernel_ms": kern_ms,
                         "flops_per_solve": flops, "achieved": flops * B / (kern_ms / 1e3) / 1e12,
                         "peak": FP64_VALU_PEAK, "unit": "TFLOP/s",
                         "frac": flops * B / (kern_ms / 1e3) / 1e12 / FP64_VALU_PEAK,
@@ -353,6 +359,103 @@ def cpu_baseline_casc(data, sample):
 
 
 C5_VEHICLES, C5_STEPS = 8192, 500
+C4_TOTAL = 65536
+C4_CHUNK = 8192   # the C4 problem set is generated in 8192-problem chunks (seed + chunk index),
+                  # so every world size solves the same 65536 problems
+
+
+def c4_shard(total, rank, world, seed):
+    """This rank's contiguous C4 shard [lo, hi) of `total` kinematic problems."""
+    import numpy as np
+
+    from vcmpc.workload import kinematic_batch, shard
+    lo, hi = shard(total, rank, world)
+    parts = []
+    for c in range(lo // C4_CHUNK, -(-hi // C4_CHUNK)):
+        a, b = c * C4_CHUNK, min((c + 1) * C4_CHUNK, total)
+        d = kinematic_batch(b - a, N=N_HORIZON, seed=seed + 1000003 * (c + 1))
+        parts.append({k: v[max(lo, a) - a:min(hi, b) - a] for k, v in d.items()})
+    return lo, hi, {k: np.ascontiguousarray(np.concatenate([p[k] for p in parts])) for k in parts[0]}
+
+
+def run_c4(args, dev, stream, rank, world, dist, steps):
+    """BASELINE config 4: 65536 kinematic LTV-MPC problems (N = 20, fp64) in total, one
+    contiguous shard per rank (8192 per GPU at 8 GPUs), no data-path collective; `value`
+    = all problems / the slowest rank's time (strong scaling over the fixed 65536)."""
+    import numpy as np
+    import torch
+
+    from vcmpc import Context, _abi
+    from vcmpc.config import load_config
+    lo, hi, data = c4_shard(args.c4_total, rank, world, args.seed)
+    B = hi - lo
+    t = {k: torch.from_numpy(v).to(dev) for k, v in data.items()}
+    ubar0 = t["ubar"].clone()
+    ctx = Context(model=_abi.VC_MODEL_KINEMATIC, N=N_HORIZON, max_batch=B, device=dev.index,
+                  kin_car=load_config("kinematic_car"), kin_mpc=load_config("kinematic_mpc"))
+    ctx.set_stream(stream.cuda_stream)
+    xbar = torch.empty((B, N_HORIZON + 1, NX), dtype=torch.float64, device=dev)
+    u0 = torch.empty((B, NU), dtype=torch.float64, device=dev)
+    status = torch.empty((B,), dtype=torch.int32, device=dev)
+    iters = torch.empty((B,), dtype=torch.int32, device=dev)
+
+    def step(ev=None):
+        t["ubar"].copy_(ubar0)
+        if ev is not None:
+            ev[0].record(stream)
+        ctx.solve(t["x0"], t["kappa"], t["ds"], t["ubar"], xbar, u0, status, iters)
+        if ev is not None:
+            ev[1].record(stream)
+
+    step()
+    torch.cuda.synchronize(dev)
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(events[i])
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    st, it = status.cpu().numpy(), iters.cpu().numpy()
+    solves, elapsed_max, kern_ms_max = dist.aggregate(float(B * steps), elapsed, kern_ms, dev)
+    solved, _, _ = dist.aggregate(float((st == 0).sum()), 0.0, 0.0, dev)
+    ctx.close()
+    return {"metric": "MPC solves/sec (batched, N=20), C4 problem set sharded over the ranks",
+            "value": solves / elapsed_max, "unit": "solves/s", "steps": steps,
+            "ms_per_step": elapsed_max / steps * 1e3, "kernel_ms_max": kern_ms_max, "dtype": "f64",
+            "scaling": "strong",
+            "config": {"workload": f"C4 kinematic-bicycle LTV-MPC, {args.c4_total} problems in total, N={N_HORIZON}, "
+                                   f"fp64, contiguous shards", "total_batch": args.c4_total,
+                       "batch_per_gpu_rank0": B, "parallelism": f"dp{world} (contiguous shards, no collective "
+                                                                f"on the data path)"},
+            "solver": {"solved_frac": solved / args.c4_total, "iters_mean_rank0": float(it.mean()),
+                       "iters_max_rank0": int(it.max())}}
+
+
+def dry_run(args):
+    """--dry-run: the multi-rank control flow without a GPU -- gloo process group from the
+    launcher's environment, every rank's C2 batch / C4 and C5 shards, the counter
+    collective, and rank 0's JSON line (tests/test_dist.py drives it through `launch`)."""
+    from vcmpc import dist
+    from vcmpc.workload import shard
+    rank, local, world = dist.init("gloo")
+    lo4, hi4, d4 = c4_shard(args.c4_total, rank, world, args.seed)
+    lo5, hi5 = shard(args.c5_vehicles, rank, world)
+    solves, elapsed_max, _ = dist.aggregate(float(args.batch + (hi4 - lo4)), 0.1 * (rank + 1), 0.0)
+    c4_first = float(d4["x0"][0, 0])
+    rows = [None] * world
+    import torch.distributed as tdist
+    if tdist.is_initialized():
+        tdist.all_gather_object(rows, (rank, local, lo4, hi4, lo5, hi5, c4_first))
+    else:
+        rows = [(rank, local, lo4, hi4, lo5, hi5, c4_first)]
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run", "n_gpus": world, "solves": solves, "elapsed_max": elapsed_max,
+                          "ranks": rows}), flush=True)
+    dist.shutdown()
 
 
 def cpu_baseline_c5(x0, track, sample_vehicles=8, sample_steps=8):
@@ -447,14 +550,23 @@ def run_c5(args, dev, stream, rank, world, dist):
 
 def main():
     args = parse()
+    from vcmpc import dist
+    if dist.needs_launch(args.gpus):
+        # `bench.py --gpus N` outside torchrun: start N ranks of this same command (one
+        # process per GPU, LOCAL_RANK = GPU index) before anything touches the GPU
+        sys.exit(dist.launch([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], args.gpus))
+    if args.dry_run:
+        return dry_run(args)
     import numpy as np
     import torch
 
-    from vcmpc import Context, _abi, dist
+    from vcmpc import Context, _abi
     from vcmpc.config import load_config
     from vcmpc.workload import kinematic_batch
 
     rank, local, world = dist.env_rank()
+    if args.gpus > 1 and world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist.init("nccl", dev)
@@ -510,6 +622,12 @@ def main():
         ctx.solve(host["x0"], host["kappa"], host["ds"], host["ubar"].copy())
     host_rate = B * reps / (time.perf_counter() - th)
     solves, elapsed_max, kern_ms_max = dist.aggregate(float(B * args.steps), elapsed, kern_ms, dev)
+    c4 = None
+    if not args.no_c4:
+        try:
+            c4 = run_c4(args, dev, stream, rank, world, dist, max(3, args.steps // 4))
+        except Exception as e:  # the headline line must still print
+            c4 = {"error": f"{type(e).__name__}: {e}"}
     c3 = c3_data = None
     if not args.no_c3:
         try:
@@ -579,6 +697,8 @@ def main():
                 from oracle.track import load_track
                 otrack = load_track(os.path.join(ROOT, "vehicle-control_amd", "config", "tracks", "ippodromo.yaml"))
                 c5["cpu_baseline"] = cpu_baseline_c5(c5_aux[0], otrack)
+        if c4 is not None:
+            out["c4"] = c4
         if c3 is not None:
             out["c3"] = c3
         if ca is not None:

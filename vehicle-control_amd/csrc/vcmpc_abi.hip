@@ -275,6 +275,21 @@ extern "C" {
 int vc_abi_version(void) { return VCMPC_ABI_VERSION; }
 int vc_params_sizeof(void) { return (int)sizeof(vc_params); }
 
+// Shared by vc_create and vc_set_obstacles: NULL when the set is usable, else the reason.
+static const char* obstacles_invalid(const vc_obstacles& o) {
+  static thread_local char msg[96];
+  if (o.n < 0 || o.n > VC_MAX_OBSTACLES) {
+    snprintf(msg, sizeof msg, "n=%d obstacles outside [0,%d]", o.n, VC_MAX_OBSTACLES);
+    return msg;
+  }
+  for (int j = 0; j < o.n; ++j)
+    if (!std::isfinite(o.s[j]) || !std::isfinite(o.ey[j]) || !std::isfinite(o.radius[j])) {
+      snprintf(msg, sizeof msg, "obstacle %d is not finite", j);
+      return msg;
+    }
+  return nullptr;
+}
+
 vc_ctx* vc_create(int device, int model, int N, int max_batch, int dtype, const vc_params* params) {
   g_create_err.clear();
   if (!params) { fail(nullptr, VC_E_ARG, "params is NULL"); return nullptr; }
@@ -298,16 +313,17 @@ vc_ctx* vc_create(int device, int model, int N, int max_batch, int dtype, const 
   if (device < 0 || device >= ndev) { fail(nullptr, VC_E_ARG, "device %d not in [0,%d)", device, ndev); return nullptr; }
   e = hipSetDevice(device);
   if (e != hipSuccess) { fail(nullptr, VC_E_HIP, "hipSetDevice: %s", hipGetErrorString(e)); return nullptr; }
+  // the obstacle set is validated by the same rule as vc_set_obstacles, before any allocation
+  if (const char* why = obstacles_invalid(params->obs)) {
+    fail(nullptr, VC_E_ARG, "params->obs: %s", why);
+    return nullptr;
+  }
   vc_ctx* c = new vc_ctx();
   c->device = device;
   c->model = model;
   c->N = N;
   c->max_batch = max_batch;
   c->dtype = dtype;
-  if (params->obs.n < 0 || params->obs.n > VC_MAX_OBSTACLES) {
-    fail(nullptr, VC_E_ARG, "obs.n=%d outside [0,%d]", params->obs.n, VC_MAX_OBSTACLES);
-    return nullptr;
-  }
   c->p = *params;
   if (!(c->p.obs.margin_min > 0)) c->p.obs.margin_min = VC_OBS_MARGIN_MIN;
   e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking);
@@ -347,12 +363,11 @@ int vc_set_obstacles(vc_ctx* c, int n, const double* s, const double* ey, const 
   o.n = n;
   o.margin_min = margin_min > 0 ? margin_min : c->p.obs.margin_min;
   for (int j = 0; j < n; ++j) {
-    if (!std::isfinite(s[j]) || !std::isfinite(ey[j]) || !std::isfinite(radius[j]))
-      return fail(c, VC_E_ARG, "obstacle %d is not finite", j);
     o.s[j] = s[j];
     o.ey[j] = ey[j];
     o.radius[j] = radius[j];
   }
+  if (const char* why = obstacles_invalid(o)) return fail(c, VC_E_ARG, "%s", why);
   c->p.obs = o;
   return 0;
 }

@@ -15,6 +15,58 @@ def env_rank():
             int(os.environ.get("WORLD_SIZE", 1)))
 
 
+def needs_launch(nprocs: int) -> bool:
+    """True when `nprocs` > 1 ranks were asked for but this process is not one of them
+    (no WORLD_SIZE from torchrun or from `launch`)."""
+    return nprocs > 1 and "WORLD_SIZE" not in os.environ
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(argv, nprocs: int, port: int | None = None, timeout: float | None = None) -> int:
+    """Run `argv` (a full command, e.g. [sys.executable, "bench.py", ...]) as `nprocs`
+    single-node ranks -- the torchrun environment (RANK, LOCAL_RANK, WORLD_SIZE,
+    LOCAL_WORLD_SIZE, MASTER_ADDR = 127.0.0.1, MASTER_PORT) set per child -- and return
+    the first non-zero exit code (0 when every rank succeeded).  The children are
+    started with subprocess (never exec) and the caller must not have touched the GPU:
+    each rank binds its own device by LOCAL_RANK.  If a rank fails, the others are
+    terminated so a collective cannot wait forever on the missing peer."""
+    import subprocess
+    import time
+    port = port or _free_port()
+    procs = []
+    for r in range(nprocs):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nprocs),
+                   LOCAL_WORLD_SIZE=str(nprocs), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(list(argv), env=env))
+    t0 = time.monotonic()
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:
+                    q.terminate()
+        if timeout is not None and time.monotonic() - t0 > timeout and live:
+            for q in live:
+                q.kill()
+            rc = rc or 124
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc
+
+
 def init(backend: str, device=None):
     """Initialise torch.distributed from the torchrun environment (world > 1 only)."""
     import torch.distributed as dist
