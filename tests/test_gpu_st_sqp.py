@@ -1,0 +1,121 @@
+"""GPU parity of the fp64 single-track SQP kernel (csrc/st_sqp.hip: stagewise Riccati
+interior point) through the C ABI, against the fp64 oracle (oracle/dyn_sqp.py, exact
+dense QPs) and its golden vectors -- BASELINE config 3's contract at N = 40 and the
+reference's own horizons N = 50 / 60 (config/controllers/singletrack.yaml:2, recorded runs
+experiments/data/*/singletrack_config.yaml).
+
+Tolerance: the north star's ||u* - u*_ref||_inf < 1e-5, here in the reference's own
+units (Fx [N], w [rad/s]) -- no scaling needed in fp64.
+"""
+import copy
+
+import numpy as np
+import pytest
+
+from oracle import dyn_sqp as D
+from oracle import models as M
+
+pytestmark = pytest.mark.gpu
+
+U_TOL = 1e-5   # max |u* - u*_oracle|, Fx in N and w in rad/s
+X_TOL = 1e-6   # x* = rollout(u*), absolute
+
+
+def _ctx(N, mpc_cfg=None, tyre="linear", max_batch=4096, obstacles=None):
+    from vcmpc import Context, _abi
+    from vcmpc.config import load_config, make_params
+    cfg = mpc_cfg if mpc_cfg is not None else load_config("dynamic_mpc")
+    params = make_params(dyn_car=load_config("dynamic_car"), dyn_mpc=cfg, tyre=tyre, obstacles=obstacles)
+    return Context(model=_abi.VC_MODEL_DYNAMIC, N=N, max_batch=max_batch, dtype=_abi.VC_F64, params=params)
+
+
+@pytest.fixture(scope="module")
+def golden():
+    import os
+    from conftest import GOLDEN
+    return {k: v.astype(np.float64) for k, v in np.load(os.path.join(GOLDEN, "dyn_sqp_golden.npz")).items()}
+
+
+def _W(cfg_name="dynamic_mpc"):
+    from vcmpc.config import load_config
+    return D.dyn_weights(load_config(cfg_name))
+
+
+def test_st_sqp_vs_golden_n40(golden):
+    g = golden
+    with _ctx(40) as ctx:
+        ub = g["ubar"].copy()
+        u0, xs, us, st, it, dg = ctx.solve(g["x0"], g["kappa"], g["ds"], ub, diag=True)
+    assert (st == 0).all(), (st, dg)
+    err = np.abs(us - g["u_star"]).max()
+    print(f"N=40 golden: max |u* - u*_oracle| = {err:.3e} (Fx in N), IPM iterations {it.min()}..{it.max()}")
+    assert err < U_TOL
+    np.testing.assert_array_equal(u0, us[:, 0])
+    assert np.abs(xs - g["x_star"]).max() < X_TOL
+
+
+@pytest.mark.parametrize("N,tyre,cfg_name", [(40, "fiala", "dynamic_mpc"), (50, "fiala", "singletrack_mpc"),
+                                             (60, "fiala", "singletrack_mpc"), (60, "linear", "singletrack_mpc")])
+def test_st_sqp_reference_horizons_vs_oracle(N, tyre, cfg_name, dyn_params):
+    """Fresh C3-sampler problems at the reference's horizons vs the oracle run here."""
+    from vcmpc.config import load_config
+    from vcmpc.workload import dynamic_batch
+    cfg = load_config(cfg_name)
+    W = D.dyn_weights(cfg)
+    d = {k: v.astype(np.float64) for k, v in dynamic_batch(6, N=N, seed=100 + N, tyre=tyre).items()}
+    ref = D.dyn_sqp_solve(d["x0"], d["ubar"], d["kappa"], d["ds"], dyn_params, W, tyre)
+    with _ctx(N, cfg, tyre) as ctx:
+        ub = d["ubar"].copy()
+        u0, xs, us, st, it = ctx.solve(d["x0"], d["kappa"], d["ds"], ub)
+    assert (st == 0).all(), st
+    err = np.abs(us - ref["u_star"]).max()
+    print(f"N={N} {tyre}: max |u* - u*_oracle| = {err:.3e}, IPM iterations {it.min()}..{it.max()}")
+    assert err < U_TOL
+    assert np.abs(xs - ref["x_star"]).max() < X_TOL
+
+
+def test_st_sqp_obstacles_vs_oracle(dyn_params):
+    """Obstacle barrier terms (cascaded_mpc.py:173-176) on problems whose
+    horizon crosses ippodromo's obstacle field."""
+    import os
+    from conftest import GOLDEN
+    from vcmpc.config import load_config
+    g = np.load(os.path.join(GOLDEN, "obs_golden.npz"))
+    if "dyn_x0" not in g:
+        pytest.skip("no dynamic obstacle problems in obs_golden.npz")
+    d = {k: g["dyn_" + k].astype(np.float64) for k in ("x0", "kappa", "ds", "ubar")}
+    obs = [tuple(r) for r in g["obstacles"]]
+    cfg = load_config("dynamic_mpc")
+    W = D.dyn_weights(cfg)
+    W["obstacles"] = obs
+    ref = D.dyn_sqp_solve(d["x0"], d["ubar"], d["kappa"], d["ds"], dyn_params, W, "linear")
+    with _ctx(40, cfg, "linear", obstacles=obs) as ctx:
+        ub = d["ubar"].copy()
+        u0, xs, us, st, it = ctx.solve(d["x0"], d["kappa"], d["ds"], ub)
+    err = np.abs(us - ref["u_star"]).max()
+    print(f"obstacles: max |u* - u*_oracle| = {err:.3e}, status {np.bincount(st)}")
+    assert (st == 0).all()
+    assert err < U_TOL
+
+
+def test_st_sqp_batch_properties():
+    """C3-sized batch (B = 4096, N = 40) in fp64: every problem solved, inputs inside
+    their boxes, bit-identical reruns, host = device pointers."""
+    import torch
+    from vcmpc.config import load_config
+    from vcmpc.workload import dynamic_batch
+    B = 4096
+    d = {k: v.astype(np.float64) for k, v in dynamic_batch(B, N=40, seed=77).items()}
+    cfg = load_config("dynamic_mpc")
+    with _ctx(40, cfg, "linear", max_batch=B) as ctx:
+        ub = d["ubar"].copy()
+        u0, xs, us, st, it = ctx.solve(d["x0"], d["kappa"], d["ds"], ub)
+        t = {k: torch.from_numpy(v).cuda() for k, v in d.items()}
+        r = ctx.solve(t["x0"], t["kappa"], t["ds"], t["ubar"])
+        torch.cuda.synchronize()
+        us2 = r[2].cpu().numpy()
+    print(f"B=4096: solved {(st == 0).mean():.4f}, IPM iterations mean {it.mean():.1f} max {it.max()}")
+    assert (st == 0).all(), np.bincount(st)
+    np.testing.assert_array_equal(us, us2)
+    ic = cfg["input_constraints"]
+    assert us[..., 1].max() <= ic["w_max"] + 1e-9 and us[..., 1].min() >= ic["w_min"] - 1e-9

@@ -1,0 +1,735 @@
+// st_sqp.hip -- fused single-track SQP step, fp64, one wavefront per problem, with a
+// stagewise Riccati interior point.
+//
+// Replaces the IPOPT solve of CascadedMPC in single-track mode (controllers/mpc/
+// cascaded_mpc.py:17-39,91-179,279-314, horizon_pm = 0) for the reference's own horizons
+// (config/controllers/singletrack.yaml N = 60; recorded runs N = 50 / 60) and BASELINE's
+// N = 40.  Contract: oracle/dyn_sqp.py (the same QP as the fp32 condensed kernel
+// dyn_sqp.hip, solved to fp64 accuracy).  Per SQP iteration:
+//   predict    lane 0: RK4 spatial rollout (vc_models.hpp dyn_spatial_ode_alg)
+//   linearize  one lane per (stage, seed pair): Dual<2> RK4 step -> two columns of
+//              [A B] and of the t-row; one lane per (stage, seed) for the stage terms
+//              (slip residuals, power and tyre-force rows) with Dual<1>
+//   QP         restated stage by stage (scripts/riccati_proto.py): QP state
+//              xt_k = (dUx, dUy, dr, ddelta, dey, depsi, p_k), p_k = dz_{k-1,Fx} (the Fx
+//              slew couples neighbouring stages), input u_k = dz_k = (dFx/S, dw); s is
+//              fixed (s' = 1) and t only enters w_time t_{N-1}, which becomes linear stage
+//              terms through each step's t-row.  Stage Hessians have 20 nonzeros; the 12
+//              one-sided rows of a stage touch (Ux, Uy, r, delta, dFx, dw) only.
+//              Mehrotra predictor-corrector; each Newton step is an LQ problem solved by
+//              a backward Riccati recursion (7 states + 2 inputs per stage: O(N) work per
+//              iteration, where the condensed form pays O(N^3)), then forward sweeps.
+//              Lane k owns stage k's rows, slacks and multipliers in registers; the
+//              recursions run on lanes 0..44 with the stage matrices in LDS.
+//   update     ubar += dz (Fx scaled back by fx_scale)
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "vc_dual.hpp"
+#include "vc_kernels.hpp"
+
+namespace vc {
+namespace {
+
+constexpr int WTH = 64;
+constexpr int NQ = 20;  // nonzeros of a stage Hessian over v = (Ux, Uy, r, delta, ey, epsi, p, dFx, dw)
+constexpr int NR = 12;  // one-sided rows per stage
+// slots of the stage Hessian's nonzeros (block {Ux, Uy, r, delta, dFx} + five diagonal-ish)
+enum { Q00, Q01, Q02, Q03, Q07, Q11, Q12, Q13, Q17, Q22, Q23, Q27, Q33, Q37, Q77, Q44, Q55, Q66, Q67, Q88 };
+
+__host__ __device__ constexpr int qslot(int i, int j) {
+  if (i > j) { const int t = i; i = j; j = t; }
+  const int a = i == 7 ? 4 : (i < 4 ? i : -1), b = j == 7 ? 4 : (j < 4 ? j : -1);
+  if (a >= 0 && b >= 0) {
+    constexpr int blk[5][5] = {{Q00, Q01, Q02, Q03, Q07}, {Q01, Q11, Q12, Q13, Q17}, {Q02, Q12, Q22, Q23, Q27},
+                               {Q03, Q13, Q23, Q33, Q37}, {Q07, Q17, Q27, Q37, Q77}};
+    return blk[a][b];
+  }
+  if (i == 4 && j == 4) return Q44;
+  if (i == 5 && j == 5) return Q55;
+  if (i == 6 && j == 6) return Q66;
+  if (i == 6 && j == 7) return Q67;
+  if (i == 8 && j == 8) return Q88;
+  return -1;
+}
+// stage vector index -> column of [A6 | B6] (-1 for p: no dynamics enters through it)
+__host__ __device__ constexpr int vcol(int i) { return i < 6 ? i : (i == 6 ? -1 : i - 1); }
+
+template <int N>
+struct StSmem {
+  double xs[N][8];    // prediction (N columns, dynamics for k < N-1)
+  double ub[N][2];    // current ubar
+  double kap[N], dsv[N];
+  double J[N][6][8];  // [A6 | B6 diag(S, 1)] of step k (rows/cols Ux, Uy, r, delta, ey, epsi | dFx, dw)
+  union {
+    struct {
+      double Qt[N][NQ];  // stage Hessian + barrier, this iteration
+      double gr[N][9];   // stage gradient Q v + q + C' lam
+      double h[N][9];    // linear term of the current LQ solve
+      double v[N][9];    // QP iterate (xt, u)
+      double dv[N][9];   // Newton direction
+      double K[N][2][7];
+      double Hi[N][3];   // Huu^-1 (00, 01, 11)
+      double kk[N][2];
+    } q;
+    struct {
+      double trow[N][8];     // t-row of step k over (y | dFx, dw)
+      double st[N][7][6];    // stage functions: value + gradient over (Ux, Uy, r, delta, Fx)
+    } l;
+  } u;
+  double P[7][7];
+  double T[7][8];
+  double Hm[9][9];
+  int flag[4];
+};
+
+__device__ __forceinline__ double bcast(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double wmax(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ double wmin(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ double wsum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double step_to_bound(double x, double dx) { return dx < 0.0 ? -x / dx : 1e300; }
+
+// Stage k's one-sided rows C v <= d (lane-owned):
+//   0: -Ux <= Ux - Ux_min          1: delta <= delta_max - delta   2: -delta <= delta - delta_min
+//   3..7: c_r . (Ux, Uy, r, delta, dFx) <= d_r   (power limit, tyre force bounds front / rear)
+//   8: dw <= ..   9: -dw <= ..   10: dFx <= trust   11: -dFx <= trust
+struct Rows {
+  double c[5][5];
+  double d[NR];
+  double m[NR];
+};
+
+__device__ __forceinline__ void row_values(const Rows& R, const double* v, double* o) {
+  o[0] = -v[0];
+  o[1] = v[3];
+  o[2] = -v[3];
+#pragma unroll
+  for (int r = 0; r < 5; ++r)
+    o[3 + r] = R.c[r][0] * v[0] + R.c[r][1] * v[1] + R.c[r][2] * v[2] + R.c[r][3] * v[3] + R.c[r][4] * v[7];
+  o[8] = v[8];
+  o[9] = -v[8];
+  o[10] = v[7];
+  o[11] = -v[7];
+}
+// out += C' y
+__device__ __forceinline__ void row_adjoint(const Rows& R, const double* y, double* out) {
+  out[0] -= y[0];
+  out[3] += y[1] - y[2];
+#pragma unroll
+  for (int r = 0; r < 5; ++r) {
+    out[0] += R.c[r][0] * y[3 + r];
+    out[1] += R.c[r][1] * y[3 + r];
+    out[2] += R.c[r][2] * y[3 + r];
+    out[3] += R.c[r][3] * y[3 + r];
+    out[7] += R.c[r][4] * y[3 + r];
+  }
+  out[8] += y[8] - y[9];
+  out[7] += y[10] - y[11];
+}
+// out = Q v (symmetric, 20 slots)
+__device__ __forceinline__ void qmul(const double* Q, const double* v, double* o) {
+  o[0] = Q[Q00] * v[0] + Q[Q01] * v[1] + Q[Q02] * v[2] + Q[Q03] * v[3] + Q[Q07] * v[7];
+  o[1] = Q[Q01] * v[0] + Q[Q11] * v[1] + Q[Q12] * v[2] + Q[Q13] * v[3] + Q[Q17] * v[7];
+  o[2] = Q[Q02] * v[0] + Q[Q12] * v[1] + Q[Q22] * v[2] + Q[Q23] * v[3] + Q[Q27] * v[7];
+  o[3] = Q[Q03] * v[0] + Q[Q13] * v[1] + Q[Q23] * v[2] + Q[Q33] * v[3] + Q[Q37] * v[7];
+  o[4] = Q[Q44] * v[4];
+  o[5] = Q[Q55] * v[5];
+  o[6] = Q[Q66] * v[6] + Q[Q67] * v[7];
+  o[7] = Q[Q07] * v[0] + Q[Q17] * v[1] + Q[Q27] * v[2] + Q[Q37] * v[3] + Q[Q67] * v[6] + Q[Q77] * v[7];
+  o[8] = Q[Q88] * v[8];
+}
+
+template <int N, int TYRE>
+__global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
+  static_assert(N >= 2 && N <= WTH, "one lane per stage");
+  __shared__ StSmem<N> s;
+  const int l = threadIdx.x;
+  const int b = blockIdx.x;
+  DynCoef<double> c = A.car;
+  c.tyre = TYRE;
+  const vc_dyn_mpc& W = A.w;
+  const double S = W.fx_scale;
+  const bool stl = l < N;
+  const int k = stl ? l : 0;  // this lane's stage
+
+  for (int i = l; i < N; i += WTH) {
+    s.kap[i] = A.kappa[(size_t)b * N + i];
+    s.dsv[i] = A.ds[(size_t)b * N + i];
+    s.ub[i][0] = A.ubar[((size_t)b * N + i) * 2];
+    s.ub[i][1] = A.ubar[((size_t)b * N + i) * 2 + 1];
+  }
+  if (l < 8) s.xs[0][l] = A.x0[(size_t)b * 8 + l];
+  if (l == 0) s.flag[0] = VC_SOLVED;
+  __syncthreads();
+
+  // Riccati lane roles (fixed per lane): H entry (hi, hj), hi <= hj, for lanes < 45
+  int hi = 0, hj = 0;
+  {
+    int q = l < 45 ? l : 0, i = 0;
+    while (q >= 9 - i) { q -= 9 - i; ++i; }
+    hi = i;
+    hj = i + q;
+  }
+  const int hslot = qslot(hi, hj), hci = vcol(hi), hcj = vcol(hj);
+  // P entry (pi, pj) for lanes < 28
+  int pi = 0, pj = 0;
+  {
+    int q = l < 28 ? l : 0, i = 0;
+    while (q >= 7 - i) { q -= 7 - i; ++i; }
+    pi = i;
+    pj = i + q;
+  }
+  const int sc = l < 9 ? vcol(l) : -1;  // sweep lanes 0..8: column of [A6 | B6] of v index l
+
+  int it_total = 0, it_max = 0;
+  bool all_conv = true, any_fail = false;
+  double last_res = 0.0, last_mu = 0.0;
+  const double tol_r = 1e-10, tol_mu = 1e-13;
+
+  for (int sq = 0;; ++sq) {
+    // ---------------- predict (lane 0, serial RK4) ----------------
+    if (l == 0) {
+      double x[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) x[i] = s.xs[0][i];
+      bool fin = true;
+      for (int kk = 0; kk < N - 1; ++kk) {
+        const double u2[2] = {s.ub[kk][0], s.ub[kk][1]};
+        const double kp = s.kap[kk];
+        double xn[8];
+        rk4_apply<double, 8>(x, s.dsv[kk], [&](const double* xx, double* f) { dyn_spatial_ode_alg<double, double>(xx, u2, kp, c, f); }, xn);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          x[i] = xn[i];
+          s.xs[kk + 1][i] = xn[i];
+          fin = fin && isfinite(xn[i]);
+        }
+      }
+      if (!fin) s.flag[0] = VC_NONFINITE;
+    }
+    __syncthreads();
+    if (sq == W.sqp_iters || s.flag[0] == VC_NONFINITE) break;
+
+    // ---------------- linearize + stage functions ----------------
+    {
+      constexpr int NLIN = 4 * (N - 1), NTASK = NLIN + 5 * N;
+      using D2 = Dual<2, double>;
+      using D1 = Dual<1, double>;
+#pragma unroll 1
+      for (int task = l; task < NTASK; task += WTH) {
+        if (task < NLIN) {
+          const int kk = task >> 2, pr = task & 3;
+          // seed pairs: (Ux, Uy), (r, delta), (ey, epsi), (Fx, w)
+          const int a0 = pr == 0 ? 0 : (pr == 1 ? 2 : (pr == 2 ? 5 : -1));
+          const int a1 = pr == 0 ? 1 : (pr == 1 ? 3 : (pr == 2 ? 6 : -1));
+          D2 x[8], u2[2], xn[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            x[i] = D2(s.xs[kk][i]);
+            x[i].d[0] = i == a0 ? 1.0 : 0.0;
+            x[i].d[1] = i == a1 ? 1.0 : 0.0;
+          }
+          u2[0] = D2(s.ub[kk][0]);
+          u2[1] = D2(s.ub[kk][1]);
+          u2[0].d[0] = pr == 3 ? 1.0 : 0.0;
+          u2[1].d[1] = pr == 3 ? 1.0 : 0.0;
+          const D2 kp(s.kap[kk]);
+          rk4_apply<D2, 8>(x, D2(s.dsv[kk]), [&](const D2* xx, D2* f) { dyn_spatial_ode_alg<D2, double>(xx, u2, kp, c, f); }, xn);
+          // columns of [A6 | B6] (y index of the seeds) and the t-row
+          const int c0 = pr < 3 ? 2 * pr : 6, c1 = c0 + 1;
+          const double s0 = pr == 3 ? S : 1.0;
+          const int yr[6] = {0, 1, 2, 3, 5, 6};
+#pragma unroll
+          for (int r = 0; r < 6; ++r) {
+            s.J[kk][r][c0] = xn[yr[r]].d[0] * s0;
+            s.J[kk][r][c1] = xn[yr[r]].d[1];
+          }
+          s.u.l.trow[kk][c0] = xn[7].d[0] * s0;
+          s.u.l.trow[kk][c1] = xn[7].d[1];
+        } else {
+          const int q = task - NLIN, kk = q / 5, j = q % 5;
+          D1 X5[5], o[7];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) X5[i] = D1(s.xs[kk][i]);
+          X5[4] = D1(s.ub[kk][0]);
+#pragma unroll
+          for (int i = 0; i < 5; ++i) X5[i].d[0] = i == j ? 1.0 : 0.0;
+          dyn_stage_terms_alg<D1, double>(X5, c, o);
+#pragma unroll
+          for (int r = 0; r < 7; ++r) {
+            s.u.l.st[kk][r][1 + j] = o[r].d[0];
+            if (j == 0) s.u.l.st[kk][r][0] = o[r].v;
+          }
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---------------- stage QP data (lane k, registers) ----------------
+    double Qc[NQ], qc[9];
+    Rows R;
+#pragma unroll
+    for (int e = 0; e < NQ; ++e) Qc[e] = 0.0;
+#pragma unroll
+    for (int e = 0; e < 9; ++e) qc[e] = 0.0;
+    {
+      const double ds = s.dsv[k];
+      const double ey = s.xs[k][5];
+      // boundary + deviation (cascaded_mpc.py:139-151), obstacle barrier (:173-176) in ey
+      const double cdev = W.w_dev * ds;
+      const double blo = ey < W.ey_min ? W.w_b * ds : 0.0, bhi = ey > W.ey_max ? W.w_b * ds : 0.0;
+      Qc[Q44] += 2.0 * (cdev + blo + bhi);
+      qc[4] += 2.0 * (cdev * ey + blo * (ey - W.ey_min) + bhi * (ey - W.ey_max));
+      if (A.obs.n > 0) {
+        double po, qo;
+        obstacle_ey_model<double>(A.obs, s.xs[k][4], ey, W.w_obs * ds, po, qo);
+        Qc[Q44] += qo;
+        qc[4] += po;
+      }
+      // w^2 (:153), prox on the scaled step
+      Qc[Q88] += 2.0 * W.w_w + 2.0 * A.qp.prox;
+      qc[8] += 2.0 * W.w_w * s.ub[k][1];
+      Qc[Q77] += 2.0 * A.qp.prox;
+      // slip-angle penalties when active at the prediction (:155-165)
+#pragma unroll
+      for (int sr = 0; sr < 2; ++sr) {
+        const double fv = s.u.l.st[k][sr][0];
+        const double wsl = fv >= 0.0 ? 2.0 * W.w_slip : 0.0;
+        const double a5[5] = {s.u.l.st[k][sr][1], s.u.l.st[k][sr][2], s.u.l.st[k][sr][3], s.u.l.st[k][sr][4],
+                              s.u.l.st[k][sr][5] * S};
+        constexpr int ix[5] = {0, 1, 2, 3, 7};
+#pragma unroll
+        for (int a = 0; a < 5; ++a) {
+          qc[ix[a]] += wsl * fv * a5[a];
+#pragma unroll
+          for (int e = a; e < 5; ++e) Qc[qslot(ix[a], ix[e])] += wsl * a5[a] * a5[e];
+        }
+      }
+      // Fx slew with the previous stage (:167-171): c (dFx_k - p_k + (Fx_k - Fx_{k-1}) / S)^2 S^2
+      if (k >= 1) {
+        const double cs = 2.0 * W.w_Fx / s.dsv[k - 1] * S * S;
+        const double r0 = (s.ub[k][0] - s.ub[k - 1][0]) / S;
+        Qc[Q66] += cs;
+        Qc[Q67] -= cs;
+        Qc[Q77] += cs;
+        qc[6] -= cs * r0;
+        qc[7] += cs * r0;
+      }
+      // w_time t_{N-1} = sum_k t-row_k . (y_k, u_k): linear stage terms (:292)
+      if (k < N - 1) {
+        constexpr int iy[8] = {0, 1, 2, 3, 4, 5, 7, 8};
+#pragma unroll
+        for (int a = 0; a < 8; ++a) qc[iy[a]] += W.w_time * s.u.l.trow[k][a];
+      }
+      // terminal (:290-303)
+      if (k == N - 1) {
+        const double Ux = s.xs[k][0];
+        if (Ux >= W.max_speed) {
+          Qc[Q00] += 2.0 * W.w_speed;
+          qc[0] += 2.0 * W.w_speed * (Ux - W.max_speed);
+        }
+        Qc[Q44] += 2.0 * W.w_ey;
+        qc[4] += 2.0 * W.w_ey * ey;
+        Qc[Q55] += 2.0 * W.w_epsi;
+        qc[5] += 2.0 * W.w_epsi * s.xs[k][6];
+      }
+      // rows (:101-128, trust region)
+      const double mk = (stl && k >= 1) ? 1.0 : 0.0;
+      R.d[0] = s.xs[k][0] - W.Ux_min;
+      R.d[1] = W.delta_max - s.xs[k][3];
+      R.d[2] = s.xs[k][3] - W.delta_min;
+      R.m[0] = R.m[1] = R.m[2] = mk;
+#pragma unroll
+      for (int r = 0; r < 5; ++r) {
+        const int fn = 2 + r;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) R.c[r][a] = s.u.l.st[k][fn][1 + a] / S;
+        R.c[r][4] = s.u.l.st[k][fn][5];
+        R.d[3 + r] = -s.u.l.st[k][fn][0] / S;
+        R.m[3 + r] = stl ? 1.0 : 0.0;
+      }
+      const double wv = s.ub[k][1];
+      double up = W.w_max - wv, dn = wv - W.w_min;
+      if (A.qp.trust_w > 0) {
+        up = fmin(up, A.qp.trust_w);
+        dn = fmin(dn, A.qp.trust_w);
+      }
+      R.d[8] = up;
+      R.d[9] = dn;
+      R.m[8] = R.m[9] = stl ? 1.0 : 0.0;
+      R.d[10] = R.d[11] = W.trust_Fx / S;
+      R.m[10] = R.m[11] = (stl && W.trust_Fx > 0) ? 1.0 : 0.0;
+#pragma unroll
+      for (int i = 0; i < NR; ++i)
+        if (R.m[i] == 0.0) R.d[i] = 1.0;
+    }
+    double sl[NR], la[NR];
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      sl[i] = R.m[i] > 0.0 ? fmax(R.d[i], 1.0) : 1.0;
+      la[i] = R.m[i];
+    }
+    double mc = 0.0;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) mc += R.m[i];
+    const double mcount = wsum(mc);
+    __syncthreads();  // the linearisation scratch is dead from here: the QP arrays alias it
+    if (stl) {
+#pragma unroll
+      for (int e = 0; e < 9; ++e) s.u.q.v[k][e] = 0.0;
+    }
+    __syncthreads();
+
+    // ---- LQ machinery -----------------------------------------------------------------
+    // Riccati factorisation of the stage Hessians s.u.q.Qt (backward): K, Hi per stage.
+    auto factor = [&]() -> bool {
+      bool ok = true;
+#pragma unroll 1
+      for (int kk = N - 1; kk >= 0; --kk) {
+        if (kk < N - 1) {
+          // T = P [A6 | B6 ; 0 | e_Fx]  (7 x 8)
+          if (l < 56) {
+            const int a = l >> 3, j = l & 7;
+            double acc = j == 6 ? s.P[a][6] : 0.0;
+#pragma unroll
+            for (int e = 0; e < 6; ++e) acc += s.P[a][e] * s.J[kk][e][j];
+            s.T[a][j] = acc;
+          }
+          __syncthreads();
+        }
+        if (l < 45) {
+          double hv = hslot >= 0 ? s.u.q.Qt[kk][hslot] : 0.0;
+          if (kk < N - 1 && hci >= 0 && hcj >= 0) {
+            double acc = hci == 6 ? s.T[6][hcj] : 0.0;
+#pragma unroll
+            for (int e = 0; e < 6; ++e) acc += s.J[kk][e][hci] * s.T[e][hcj];
+            hv += acc;
+          }
+          s.Hm[hi][hj] = hv;
+          s.Hm[hj][hi] = hv;
+        }
+        __syncthreads();
+        const double h00 = s.Hm[7][7], h01 = s.Hm[7][8], h11 = s.Hm[8][8];
+        const double det = h00 * h11 - h01 * h01;
+        ok = ok && h00 > 0.0 && det > 0.0;
+        const double id = 1.0 / det;
+        const double i00 = h11 * id, i01 = -h01 * id, i11 = h00 * id;
+        if (l < 28) {
+          const double x0 = s.Hm[7][pi], x1 = s.Hm[8][pi], y0 = s.Hm[7][pj], y1 = s.Hm[8][pj];
+          const double pv = s.Hm[pi][pj] - (x0 * (i00 * y0 + i01 * y1) + x1 * (i01 * y0 + i11 * y1));
+          s.P[pi][pj] = pv;
+          s.P[pj][pi] = pv;
+        } else if (l < 42) {
+          const int cc = (l - 28) / 7, i = (l - 28) % 7;
+          const double x0 = s.Hm[7][i], x1 = s.Hm[8][i];
+          s.u.q.K[kk][cc][i] = cc == 0 ? -(i00 * x0 + i01 * x1) : -(i01 * x0 + i11 * x1);
+        } else if (l == 42) {
+          s.u.q.Hi[kk][0] = i00;
+          s.u.q.Hi[kk][1] = i01;
+          s.u.q.Hi[kk][2] = i11;
+        }
+        __syncthreads();
+      }
+      return ok;
+    };
+
+    // LQ solve with linear terms s.u.q.h -> direction s.u.q.dv (backward vector pass with the
+    // factor, then the forward rollout u = K xt + kk)
+    auto lq_solve = [&]() {
+      double pv = 0.0;  // lanes 0..6: p_{k+1}
+#pragma unroll 1
+      for (int kk = N - 1; kk >= 0; --kk) {
+        double g = l < 9 ? s.u.q.h[kk][l] : 0.0;
+        if (kk < N - 1) {
+          double pb[7];
+#pragma unroll
+          for (int a = 0; a < 7; ++a) pb[a] = bcast(pv, a);
+          if (sc >= 0) {
+            double acc = sc == 6 ? pb[6] : 0.0;
+#pragma unroll
+            for (int e = 0; e < 6; ++e) acc += s.J[kk][e][sc] * pb[e];
+            g += acc;
+          }
+        }
+        const double gu0 = bcast(g, 7), gu1 = bcast(g, 8);
+        const double* Hk = s.u.q.Hi[kk];
+        const double k0 = -(Hk[0] * gu0 + Hk[1] * gu1), k1 = -(Hk[1] * gu0 + Hk[2] * gu1);
+        if (l == 0) {
+          s.u.q.kk[kk][0] = k0;
+          s.u.q.kk[kk][1] = k1;
+        }
+        const int li = l < 7 ? l : 0;
+        pv = l < 7 ? g + s.u.q.K[kk][0][li] * gu0 + s.u.q.K[kk][1][li] * gu1 : 0.0;
+      }
+      __syncthreads();
+      double X = 0.0;  // lanes 0..6: xt_k
+#pragma unroll 1
+      for (int kk = 0; kk < N; ++kk) {
+        double xb[7];
+#pragma unroll
+        for (int a = 0; a < 7; ++a) xb[a] = bcast(X, a);
+        double u0 = s.u.q.kk[kk][0], u1 = s.u.q.kk[kk][1];
+#pragma unroll
+        for (int a = 0; a < 7; ++a) {
+          u0 += s.u.q.K[kk][0][a] * xb[a];
+          u1 += s.u.q.K[kk][1][a] * xb[a];
+        }
+        if (l < 7) s.u.q.dv[kk][l] = X;
+        if (l == 7) s.u.q.dv[kk][7] = u0;
+        if (l == 8) s.u.q.dv[kk][8] = u1;
+        if (kk < N - 1) {
+          const int r = l < 6 ? l : 0;
+          double xn = s.J[kk][r][6] * u0 + s.J[kk][r][7] * u1;
+#pragma unroll
+          for (int e = 0; e < 6; ++e) xn += s.J[kk][r][e] * xb[e];
+          X = l < 6 ? xn : (l == 6 ? u0 : 0.0);
+        }
+      }
+      __syncthreads();
+    };
+
+    // condensed dual residual max |d/du (sum_k gr_k . v_k)| through the dynamics (adjoint sweep)
+    auto dual_residual = [&]() -> double {
+      double rho = 0.0, rmax = 0.0;
+#pragma unroll 1
+      for (int kk = N - 1; kk >= 0; --kk) {
+        double g = l < 9 ? s.u.q.gr[kk][l] : 0.0;
+        if (kk < N - 1) {
+          double pb[7];
+#pragma unroll
+          for (int a = 0; a < 7; ++a) pb[a] = bcast(rho, a);
+          if (sc >= 0) {
+            double acc = sc == 6 ? pb[6] : 0.0;
+#pragma unroll
+            for (int e = 0; e < 6; ++e) acc += s.J[kk][e][sc] * pb[e];
+            g += acc;
+          }
+        }
+        if (l == 7 || l == 8) rmax = fmax(rmax, fabs(g));
+        rho = l < 7 ? g : 0.0;
+      }
+      return wmax(rmax);
+    };
+
+    // ---------------- interior point (Mehrotra predictor-corrector) ----------------
+    int it = 0;
+    bool conv = false, fail = false;
+#pragma unroll 1
+    for (; it < A.qp.max_iter; ++it) {
+      // (a) residuals, stage gradients, barrier-augmented stage Hessians
+      double vk[9], rp[NR], wg[NR], grk[9], val[NR];
+      double rpm = 0.0, mus = 0.0;
+#pragma unroll
+      for (int e = 0; e < 9; ++e) vk[e] = s.u.q.v[k][e];
+      row_values(R, vk, val);
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        rp[i] = R.m[i] * (val[i] + sl[i] - R.d[i]);
+        wg[i] = R.m[i] * la[i] / sl[i];
+        rpm = fmax(rpm, fabs(rp[i]));
+        mus += R.m[i] * sl[i] * la[i];
+      }
+      qmul(Qc, vk, grk);
+#pragma unroll
+      for (int e = 0; e < 9; ++e) grk[e] += qc[e];
+      {
+        double ml[NR];
+#pragma unroll
+        for (int i = 0; i < NR; ++i) ml[i] = R.m[i] * la[i];
+        row_adjoint(R, ml, grk);
+      }
+      if (stl) {
+#pragma unroll
+        for (int e = 0; e < 9; ++e) s.u.q.gr[k][e] = grk[e];
+        double Qt[NQ];
+#pragma unroll
+        for (int e = 0; e < NQ; ++e) Qt[e] = Qc[e];
+        Qt[Q00] += wg[0];
+        Qt[Q33] += wg[1] + wg[2];
+        Qt[Q88] += wg[8] + wg[9];
+        Qt[Q77] += wg[10] + wg[11];
+        constexpr int ix[5] = {0, 1, 2, 3, 7};
+#pragma unroll
+        for (int r = 0; r < 5; ++r)
+#pragma unroll
+          for (int a = 0; a < 5; ++a)
+#pragma unroll
+            for (int e = a; e < 5; ++e) Qt[qslot(ix[a], ix[e])] += wg[3 + r] * R.c[r][a] * R.c[r][e];
+#pragma unroll
+        for (int e = 0; e < NQ; ++e) s.u.q.Qt[k][e] = Qt[e];
+      } else {
+        rpm = 0.0;
+        mus = 0.0;
+      }
+      __syncthreads();
+      rpm = wmax(rpm);
+      const double mu = wsum(mus) / mcount;
+      const double rdm = dual_residual();
+      last_res = fmax(rdm, rpm);
+      last_mu = mu;
+      if (!(last_res == last_res) || !(mu == mu) || last_res > 1e300) { fail = true; break; }
+      if (last_res <= tol_r && mu <= tol_mu) { conv = true; break; }
+
+      // (b) Riccati factorisation of H + C'WC
+      if (!factor()) { fail = true; break; }
+
+      // (c) predictor: h = gr + C'(W rp - lam)
+      auto set_h = [&](const double* rc_over_s) {
+        if (stl) {
+          double y[NR], hk[9];
+#pragma unroll
+          for (int i = 0; i < NR; ++i) y[i] = R.m[i] * (wg[i] * rp[i] - rc_over_s[i]);
+#pragma unroll
+          for (int e = 0; e < 9; ++e) hk[e] = grk[e];
+          row_adjoint(R, y, hk);
+#pragma unroll
+          for (int e = 0; e < 9; ++e) s.u.q.h[k][e] = hk[e];
+        }
+        __syncthreads();
+      };
+      set_h(la);
+      lq_solve();
+      double dsa[NR], dla[NR], cdv[NR], dvk[9];
+      double amin = 1.0;
+#pragma unroll
+      for (int e = 0; e < 9; ++e) dvk[e] = s.u.q.dv[k][e];
+      row_values(R, dvk, cdv);
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        dsa[i] = R.m[i] * (-rp[i] - cdv[i]);
+        dla[i] = R.m[i] * (wg[i] * (cdv[i] + rp[i]) - la[i]);
+        if (stl && R.m[i] > 0.0) amin = fmin(amin, fmin(step_to_bound(sl[i], dsa[i]), step_to_bound(la[i], dla[i])));
+      }
+      amin = wmin(amin);
+      double ms = 0.0;
+      if (stl) {
+#pragma unroll
+        for (int i = 0; i < NR; ++i) ms += R.m[i] * (sl[i] + amin * dsa[i]) * (la[i] + amin * dla[i]);
+      }
+      ms = wsum(ms) / mcount;
+      const double ratio = mu > 0.0 ? fmin(1.0, ms / mu) : 0.0;
+      const double smu = ratio * ratio * ratio * mu;
+
+      // (d) corrector: rc = s lam + ds_a dl_a - sigma mu
+      double rcs[NR];
+#pragma unroll
+      for (int i = 0; i < NR; ++i) rcs[i] = R.m[i] * (sl[i] * la[i] + dsa[i] * dla[i] - smu) / sl[i];
+      set_h(rcs);
+      lq_solve();
+#pragma unroll
+      for (int e = 0; e < 9; ++e) dvk[e] = s.u.q.dv[k][e];
+      row_values(R, dvk, cdv);
+      amin = 1.0;
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        dsa[i] = R.m[i] * (-rp[i] - cdv[i]);
+        dla[i] = R.m[i] * (wg[i] * (cdv[i] + rp[i]) - rcs[i]);
+        if (stl && R.m[i] > 0.0) amin = fmin(amin, fmin(step_to_bound(sl[i], dsa[i]), step_to_bound(la[i], dla[i])));
+      }
+      const double alpha = fmin(1.0, 0.99 * wmin(amin));
+      if (stl) {
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          if (R.m[i] > 0.0) {
+            sl[i] = fmax(sl[i] + alpha * dsa[i], 1e-300);
+            la[i] = fmax(la[i] + alpha * dla[i], 1e-300);
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 9; ++e) s.u.q.v[k][e] = vk[e] + alpha * dvk[e];
+      }
+      __syncthreads();
+    }
+    it_total += it;
+    it_max = max(it_max, it);
+    all_conv = all_conv && conv;
+    any_fail = any_fail || fail;
+
+    // ---------------- SQP update: ubar += dz ----------------
+    if (stl) {
+      s.ub[k][0] += s.u.q.v[k][7] * S;
+      s.ub[k][1] += s.u.q.v[k][8];
+    }
+    __syncthreads();
+  }
+
+  // ---------------- outputs: u*, x* = rollout(u*), u0, status ----------------
+  bool finite = true;
+  for (int e = l; e < 2 * N; e += WTH) {
+    const double v = s.ub[e >> 1][e & 1];
+    finite = finite && isfinite(v);
+    A.u_out[(size_t)b * 2 * N + e] = v;
+  }
+  for (int e = l; e < 8 * N; e += WTH) {
+    const double v = s.xs[e >> 3][e & 7];
+    finite = finite && isfinite(v);
+    A.x_out[(size_t)b * 8 * N + e] = v;
+  }
+  finite = __all(finite ? 1 : 0) != 0;
+  if (l < 2) A.u0[(size_t)b * 2 + l] = s.ub[0][l];
+  if (l == 0) {
+    int32_t st;
+    if (!finite || s.flag[0] == VC_NONFINITE) st = VC_NONFINITE;
+    else if (all_conv) st = VC_SOLVED;
+    else st = VC_MAX_ITER;
+    A.status[b] = st;
+    A.iters[b] = it_total;
+    if (A.diag) {
+      A.diag[(size_t)b * 4 + 0] = last_res;
+      A.diag[(size_t)b * 4 + 1] = last_mu;
+      A.diag[(size_t)b * 4 + 2] = double((any_fail ? 1 : 0) | (all_conv ? 2 : 0));
+      A.diag[(size_t)b * 4 + 3] = double(it_max);
+    }
+  }
+}
+
+}  // namespace
+
+// ---- host launcher ---------------------------------------------------------------
+#define VC_ST_HORIZONS(X) X(20) X(30) X(40) X(50) X(60)
+
+bool st_sqp_built(int N) {
+  switch (N) {
+#define VC_CASE(n) case n:
+    VC_ST_HORIZONS(VC_CASE)
+#undef VC_CASE
+    return true;
+    default:
+      return false;
+  }
+}
+
+hipError_t launch_st_sqp(const StSqpArgs& a, int N, hipStream_t stream) {
+  if (a.B <= 0) return hipSuccess;
+  const bool lin = a.car.tyre == VC_TYRE_LINEAR;
+  switch (N) {
+#define VC_CASE(n)                                                                                          \
+  case n:                                                                                                  \
+    if (lin) hipLaunchKernelGGL((st_sqp_kernel<n, VC_TYRE_LINEAR>), dim3(a.B), dim3(WTH), 0, stream, a);  \
+    else hipLaunchKernelGGL((st_sqp_kernel<n, VC_TYRE_FIALA>), dim3(a.B), dim3(WTH), 0, stream, a);       \
+    return hipGetLastError();
+    VC_ST_HORIZONS(VC_CASE)
+#undef VC_CASE
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace vc

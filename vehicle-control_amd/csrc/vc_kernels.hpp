@@ -84,6 +84,25 @@ struct DynSqpArgs {
   vc_obstacles obs;
 };
 
+// Fused single-track SQP step with a stagewise Riccati interior point (st_sqp.hip), fp64.
+struct StSqpArgs {
+  const double* x0;     // [B][8]
+  const double* kappa;  // [B][N]
+  const double* ds;     // [B][N]
+  const double* ubar;   // [B][N][2]  warm start (may alias u_out)
+  double* u_out;        // [B][N][2]  u*
+  double* x_out;        // [B][N][8]  x* = rollout(u*)
+  double* u0;           // [B][2]
+  int32_t* status;      // [B]
+  int32_t* iters;       // [B]
+  double* diag;         // [B][4] optional diagnostics, may be null
+  int B;
+  DynCoef<double> car;
+  vc_dyn_mpc w;
+  vc_qp qp;
+  vc_obstacles obs;
+};
+
 // Fused cascaded (single-track + point-mass) SQP step (casc_sqp.hip), fp64.
 struct CascSqpArgs {
   const double* x0;     // [B][8]
@@ -139,6 +158,8 @@ hipError_t launch_drive(const ModelArgs& m, int dtype, const TrackTable& tt, dou
 hipError_t launch_kin_ltv(const KinLtvArgs& a, int N, hipStream_t stream);
 hipError_t launch_dyn_sqp(const DynSqpArgs& a, int N, hipStream_t stream);
 hipError_t launch_casc_sqp(const CascSqpArgs& a, int N, int M, hipStream_t stream);
+hipError_t launch_st_sqp(const StSqpArgs& a, int N, hipStream_t stream);
+bool st_sqp_built(int N);
 bool casc_sqp_built(int N, int M);
 size_t dyn_sqp_smem_bytes(int N);
 int dyn_sqp_debug_stride();

@@ -133,7 +133,9 @@ bool kin_solve_built(const vc_ctx* c) {
   return c->model == VC_MODEL_KINEMATIC && c->dtype == VC_F64 && vc::kin_ltv_smem_bytes(c->N) > 0;
 }
 bool dyn_solve_built(const vc_ctx* c) {
-  return c->model == VC_MODEL_DYNAMIC && c->dtype == VC_F32 && vc::dyn_sqp_smem_bytes(c->N) > 0;
+  if (c->model != VC_MODEL_DYNAMIC) return false;
+  if (c->dtype == VC_F32) return vc::dyn_sqp_smem_bytes(c->N) > 0;
+  return vc::st_sqp_built(c->N);
 }
 bool casc_solve_built(const vc_ctx* c) {
   return c->model == VC_MODEL_CASCADED && c->dtype == VC_F64 && vc::casc_sqp_built(c->N, c->p.casc.horizon_pm);
@@ -213,6 +215,57 @@ int casc_solve(vc_ctx* c, int B, const void* x0, const void* kappa, const void* 
   return 0;
 }
 
+// Dynamic single-track SQP, fp64 (st_sqp.hip, stagewise Riccati interior point): xbar has
+// N state columns.
+int st_solve(vc_ctx* c, int B, const void* x0, const void* kappa, const void* ds, void* xbar, void* ubar, void* u0,
+             int32_t* status, int32_t* iters, void* diag, int flags) {
+  const int N = c->N, nx = 8, nu = 2;
+  const vc_dyn_mpc& w = c->p.dyn_mpc;
+  vc::StSqpArgs a{};
+  a.B = B;
+  a.car = vc::make_dyn_coef<double>(c->p.dyn_car);
+  a.w = w;
+  a.qp = c->p.qp;
+  a.obs = c->p.obs;
+  std::vector<Slot> slots;
+  if (flags == VC_HOST_PTRS) {
+    slots = {{x0, nullptr, (size_t)B * nx * 8, nullptr},
+             {kappa, nullptr, (size_t)B * N * 8, nullptr},
+             {ds, nullptr, (size_t)B * N * 8, nullptr},
+             {ubar, ubar, (size_t)B * N * nu * 8, nullptr},
+             {nullptr, xbar, (size_t)B * N * nx * 8, nullptr},
+             {nullptr, u0, (size_t)B * nu * 8, nullptr},
+             {nullptr, status, (size_t)B * 4, nullptr},
+             {nullptr, iters, (size_t)B * 4, nullptr},
+             {nullptr, diag, diag ? (size_t)B * 4 * 8 : 0, nullptr}};
+    if (int r = stage(c, slots)) return r;
+    a.x0 = (const double*)slots[0].dev;
+    a.kappa = (const double*)slots[1].dev;
+    a.ds = (const double*)slots[2].dev;
+    a.ubar = (const double*)slots[3].dev;
+    a.u_out = (double*)slots[3].dev;
+    a.x_out = (double*)slots[4].dev;
+    a.u0 = (double*)slots[5].dev;
+    a.status = (int32_t*)slots[6].dev;
+    a.iters = (int32_t*)slots[7].dev;
+    a.diag = diag ? (double*)slots[8].dev : nullptr;
+  } else {
+    a.x0 = (const double*)x0;
+    a.kappa = (const double*)kappa;
+    a.ds = (const double*)ds;
+    a.ubar = (const double*)ubar;
+    a.u_out = (double*)ubar;
+    a.x_out = (double*)xbar;
+    a.u0 = (double*)u0;
+    a.status = status;
+    a.iters = iters;
+    a.diag = (double*)diag;
+  }
+  VC_HIP(c, vc::launch_st_sqp(a, N, c->stream));
+  if (flags == VC_HOST_PTRS) return unstage(c, slots);
+  return 0;
+}
+
 // Dynamic single-track SQP (dyn_sqp.hip), fp32: xbar has N state columns.
 int dyn_solve(vc_ctx* c, int B, const void* x0, const void* kappa, const void* ds, void* xbar, void* ubar, void* u0,
               int32_t* status, int32_t* iters, void* diag, int flags, void* dbg = nullptr) {
@@ -221,6 +274,7 @@ int dyn_solve(vc_ctx* c, int B, const void* x0, const void* kappa, const void* d
   if (w.sqp_iters < 1 || w.sqp_iters > 64) return fail(c, VC_E_ARG, "dyn_mpc.sqp_iters=%d outside [1,64]", w.sqp_iters);
   if (!(w.fx_scale > 0)) return fail(c, VC_E_ARG, "dyn_mpc.fx_scale must be > 0");
   if (c->p.qp.max_iter < 1) return fail(c, VC_E_ARG, "qp.max_iter must be >= 1");
+  if (c->dtype == VC_F64) return st_solve(c, B, x0, kappa, ds, xbar, ubar, u0, status, iters, diag, flags);
   vc::DynSqpArgs a{};
   a.B = B;
   a.car = vc::make_dyn_coef<float>(c->p.dyn_car);
