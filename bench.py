@@ -72,6 +72,26 @@ C3_FLOP_ITER = (sum(2 * (2 * k) * 7 * 7 + (2 * k) ** 2 * 7 for k in range(1, C3_
 C3_FLOP_SQP = 4 * (C3_N - 1) * 9 * 300 + C3_n * (C3_N - 1) * 7 * 7 * 2
 
 
+def c3_bytes(N, word):
+    """Compulsory HBM bytes per single-track solve: in x0 + kappa + ds + ubar, out u* + x*
+    (N columns) + u0, + status + iters."""
+    return (C3_NX + 2 * N + 2 * N) * word + (2 * N + N * C3_NX + 2) * word + 8
+
+
+def st_flops(ipm_iters_total, N, sqp_iters=3):
+    """Algorithmic fp64 FLOPs of one stagewise-Riccati SQP solve (csrc/st_sqp.hip):
+    per interior-point iteration the Riccati factorisation (per stage T = P [A B] 7x8x6, the
+    45 stage-Hessian entries x 6, the 28 + 14 Schur / gain entries: ~1.7 K FLOP), two LQ
+    solves (backward + forward sweeps, ~0.45 K FLOP per stage each) and the adjoint residual
+    sweep (~0.1 K), plus the stage-local rows (~1 K per stage: 12 rows, barrier Hessian,
+    residuals, two step computations); per SQP iteration the RK4 rollout (~1.2 K FLOP per
+    stage), the dual-number Jacobians (4 seed pairs x 3 x 1.2 K) and stage functions
+    (5 x 2 x 0.25 K)."""
+    per_stage_iter = 2 * (56 * 6 + 45 * 7 + 28 * 6 + 14 * 2) + 2 * 450 + 100 + 1000
+    per_stage_sqp = 1200 + 4 * 3 * 1200 + 5 * 2 * 250
+    return ipm_iters_total * N * per_stage_iter + (sqp_iters + 1) * N * per_stage_sqp
+
+
 def c3_flops(pdip_iters_total, sqp_iters=3, polish_rounds=2):
     """fp32 FLOPs of one C3 solve given its total interior-point iterations."""
     return (sqp_iters * C3_FLOP_SQP + (pdip_iters_total + sqp_iters * polish_rounds) * C3_FLOP_ITER
@@ -199,8 +219,10 @@ def cpu_baseline_c3(data, sample):
                       f"complex-step linearisation + exact QP, numpy fp64, 1 thread) in {dt:.2f} s"}
 
 
-def run_c3(args, dev, stream, rank, dist, steps):
-    """Secondary measurement: BASELINE config 3 on this rank (weak scaling)."""
+def run_c3(args, dev, stream, rank, dist, steps, f64=False, N=C3_N, cfg_name="dynamic_mpc"):
+    """Secondary measurement: BASELINE config 3 on this rank (weak scaling).  f64=True runs
+    the same workload through the fp64 stagewise-Riccati kernel (csrc/st_sqp.hip); with
+    N = 60 / cfg_name = "singletrack_mpc" it is the reference's own single-track horizon."""
     import numpy as np
     import torch
 
@@ -209,15 +231,16 @@ def run_c3(args, dev, stream, rank, dist, steps):
     from vcmpc.workload import dynamic_batch
 
     B = args.c3_batch
-    data = dynamic_batch(B, N=C3_N, seed=args.seed + 104729 * rank)
-    t = {k: torch.from_numpy(v).to(dev) for k, v in data.items()}
+    data = dynamic_batch(B, N=N, seed=args.seed + 104729 * rank)
+    tdt = torch.float64 if f64 else torch.float32
+    t = {k: torch.from_numpy(v).to(dev, tdt) for k, v in data.items()}
     ubar0 = t["ubar"].clone()
-    params = make_params(dyn_car=load_config("dynamic_car"), dyn_mpc=load_config("dynamic_mpc"), tyre="linear")
-    ctx = Context(model=_abi.VC_MODEL_DYNAMIC, N=C3_N, max_batch=B, dtype=_abi.VC_F32, device=dev.index,
-                  params=params)
+    params = make_params(dyn_car=load_config("dynamic_car"), dyn_mpc=load_config(cfg_name), tyre="linear")
+    ctx = Context(model=_abi.VC_MODEL_DYNAMIC, N=N, max_batch=B, dtype=_abi.VC_F64 if f64 else _abi.VC_F32,
+                  device=dev.index, params=params)
     ctx.set_stream(stream.cuda_stream)
-    xbar = torch.empty((B, C3_N, C3_NX), dtype=torch.float32, device=dev)
-    u0 = torch.empty((B, 2), dtype=torch.float32, device=dev)
+    xbar = torch.empty((B, N, C3_NX), dtype=tdt, device=dev)
+    u0 = torch.empty((B, 2), dtype=tdt, device=dev)
     status = torch.empty((B,), dtype=torch.int32, device=dev)
     iters = torch.empty((B,), dtype=torch.int32, device=dev)
 
@@ -244,17 +267,25 @@ def run_c3(args, dev, stream, rank, dist, steps):
     st, it = status.cpu().numpy(), iters.cpu().numpy()
     solves, elapsed_max, kern_ms_max = dist.aggregate(float(B * steps), elapsed, kern_ms, dev)
     ctx.close()
-    flops = c3_flops(float(it.mean()))
-    out = {"metric": "MPC solves/sec (batched, N=40, 3 SQP iterations)", "value": solves / elapsed_max,
-           "unit": "solves/s", "steps": steps, "ms_per_step": elapsed_max / steps * 1e3, "dtype": "f32",
+    if f64:
+        flops = st_flops(float(it.mean()), N)
+        word, kern, peak, bpsolve = 8, f"st_sqp_kernel<{N}, linear>", FP64_VALU_PEAK, c3_bytes(N, 8)
+    else:
+        flops = c3_flops(float(it.mean()))
+        word, kern, peak, bpsolve = 4, "dyn_sqp_kernel<40, linear>", FP32_PEAK_TFS, C3_BYTES_PER_SOLVE
+    dname = "fp64" if f64 else "fp32"
+    out = {"metric": f"MPC solves/sec (batched, N={N}, 3 SQP iterations)", "value": solves / elapsed_max,
+           "unit": "solves/s", "steps": steps, "ms_per_step": elapsed_max / steps * 1e3,
+           "dtype": "f64" if f64 else "f32",
            "config": {"workload": f"C3 dynamic-bicycle (linear tyre) single-track NMPC via SQP, B={B} per GPU, "
-                                  f"N={C3_N}, fp32", "batch_per_gpu": B, "horizon": C3_N},
-           "roofline": {"bound": "mfma", "kernel": "dyn_sqp_kernel<40, linear>", "kernel_ms": kern_ms,
+                                  f"N={N}, {dname}" + ("" if cfg_name == "dynamic_mpc" else f", {cfg_name}.yaml"),
+                      "batch_per_gpu": B, "horizon": N},
+           "roofline": {"bound": "fp64-valu" if f64 else "mfma", "kernel": kern, "kernel_ms": kern_ms,
                         "flops_per_solve": flops, "achieved": flops * B / (kern_ms / 1e3) / 1e12,
-                        "peak": FP32_PEAK_TFS, "unit": "TFLOP/s",
-                        "frac": flops * B / (kern_ms / 1e3) / 1e12 / FP32_PEAK_TFS,
-                        "hbm": {"bytes_per_solve": C3_BYTES_PER_SOLVE,
-                                "achieved": C3_BYTES_PER_SOLVE * B / (kern_ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
+                        "peak": peak, "unit": "TFLOP/s",
+                        "frac": flops * B / (kern_ms / 1e3) / 1e12 / peak,
+                        "hbm": {"bytes_per_solve": bpsolve,
+                                "achieved": bpsolve * B / (kern_ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
                                 "unit": "GB/s"}},
            "solver": {"solved_frac": float((st == 0).mean()), "pdip_iters_mean": float(it.mean()),
                       "pdip_iters_max": int(it.max())}}
@@ -628,12 +659,21 @@ def main():
             c4 = run_c4(args, dev, stream, rank, world, dist, max(3, args.steps // 4))
         except Exception as e:  # the headline line must still print
             c4 = {"error": f"{type(e).__name__}: {e}"}
-    c3 = c3_data = None
+    c3 = c3_data = c3f = st60 = None
     if not args.no_c3:
         try:
             c3, c3_data = run_c3(args, dev, stream, rank, dist, max(3, args.steps // 4))
         except Exception as e:  # the headline line must still print
             c3 = {"error": f"{type(e).__name__}: {e}"}
+        try:
+            c3f, _ = run_c3(args, dev, stream, rank, dist, max(3, args.steps // 4), f64=True)
+        except Exception as e:
+            c3f = {"error": f"{type(e).__name__}: {e}"}
+        try:
+            st60, _ = run_c3(args, dev, stream, rank, dist, max(3, args.steps // 4), f64=True, N=60,
+                             cfg_name="singletrack_mpc")
+        except Exception as e:
+            st60 = {"error": f"{type(e).__name__}: {e}"}
     ca = ca_data = None
     if not args.no_casc:
         try:
@@ -701,6 +741,10 @@ def main():
             out["c4"] = c4
         if c3 is not None:
             out["c3"] = c3
+        if c3f is not None:
+            out["c3_f64"] = c3f
+        if st60 is not None:
+            out["singletrack_n60_f64"] = st60
         if ca is not None:
             out["cascaded"] = ca
         if c5 is not None:

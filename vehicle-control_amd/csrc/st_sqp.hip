@@ -106,6 +106,25 @@ __device__ __forceinline__ double wsum(double v) {
 }
 __device__ __forceinline__ double step_to_bound(double x, double dx) { return dx < 0.0 ? -x / dx : 1e300; }
 
+// Section timing (debug builds only, -DVC_TIMING, `make timing`): lane 0's s_memtime stamps,
+// accumulated per section and written to diag[b][4 + slot] (scripts/st_section_timing.py).
+enum { ST_PRED = 0, ST_LIN, ST_SETUP, ST_RESID, ST_DUAL, ST_FACT, ST_SOLVE, ST_STEP, ST_TOTAL, ST_NSLOT };
+#ifdef VC_TIMING
+#define ST_STAMP(var)                                \
+  __builtin_amdgcn_sched_barrier(0);                 \
+  const uint64_t var = __builtin_amdgcn_s_memtime(); \
+  __builtin_amdgcn_sched_barrier(0);
+#define ST_ACC(slot, t0)                               \
+  {                                                    \
+    __builtin_amdgcn_sched_barrier(0);                 \
+    tacc[slot] += __builtin_amdgcn_s_memtime() - (t0); \
+    __builtin_amdgcn_sched_barrier(0);                 \
+  }
+#else
+#define ST_STAMP(var)
+#define ST_ACC(slot, t0)
+#endif
+
 // Stage k's one-sided rows C v <= d (lane-owned):
 //   0: -Ux <= Ux - Ux_min          1: delta <= delta_max - delta   2: -delta <= delta - delta_min
 //   3..7: c_r . (Ux, Uy, r, delta, dFx) <= d_r   (power limit, tyre force bounds front / rear)
@@ -177,6 +196,10 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
   }
   if (l < 8) s.xs[0][l] = A.x0[(size_t)b * 8 + l];
   if (l == 0) s.flag[0] = VC_SOLVED;
+#ifdef VC_TIMING
+  uint64_t tacc[ST_NSLOT] = {};
+  const uint64_t t_start = __builtin_amdgcn_s_memtime();
+#endif
   __syncthreads();
 
   // Riccati lane roles (fixed per lane): H entry (hi, hj), hi <= hj, for lanes < 45
@@ -205,6 +228,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
 
   for (int sq = 0;; ++sq) {
     // ---------------- predict (lane 0, serial RK4) ----------------
+    ST_STAMP(t_p0)
     if (l == 0) {
       double x[8];
 #pragma unroll
@@ -225,9 +249,11 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       if (!fin) s.flag[0] = VC_NONFINITE;
     }
     __syncthreads();
+    ST_ACC(ST_PRED, t_p0)
     if (sq == W.sqp_iters || s.flag[0] == VC_NONFINITE) break;
 
     // ---------------- linearize + stage functions ----------------
+    ST_STAMP(t_l0)
     {
       constexpr int NLIN = 4 * (N - 1), NTASK = NLIN + 5 * N;
       using D2 = Dual<2, double>;
@@ -281,6 +307,8 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       }
     }
     __syncthreads();
+    ST_ACC(ST_LIN, t_l0)
+    ST_STAMP(t_s0)
 
     // ---------------- stage QP data (lane k, registers) ----------------
     double Qc[NQ], qc[9];
@@ -396,6 +424,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       for (int e = 0; e < 9; ++e) s.u.q.v[k][e] = 0.0;
     }
     __syncthreads();
+    ST_ACC(ST_SETUP, t_s0)
 
     // ---- LQ machinery -----------------------------------------------------------------
     // Riccati factorisation of the stage Hessians s.u.q.Qt (backward): K, Hi per stage.
@@ -534,6 +563,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
 #pragma unroll 1
     for (; it < A.qp.max_iter; ++it) {
       // (a) residuals, stage gradients, barrier-augmented stage Hessians
+      ST_STAMP(t_r0)
       double vk[9], rp[NR], wg[NR], grk[9], val[NR];
       double rpm = 0.0, mus = 0.0;
 #pragma unroll
@@ -581,14 +611,20 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       __syncthreads();
       rpm = wmax(rpm);
       const double mu = wsum(mus) / mcount;
+      ST_ACC(ST_RESID, t_r0)
+      ST_STAMP(t_d0)
       const double rdm = dual_residual();
+      ST_ACC(ST_DUAL, t_d0)
       last_res = fmax(rdm, rpm);
       last_mu = mu;
       if (!(last_res == last_res) || !(mu == mu) || last_res > 1e300) { fail = true; break; }
       if (last_res <= tol_r && mu <= tol_mu) { conv = true; break; }
 
       // (b) Riccati factorisation of H + C'WC
-      if (!factor()) { fail = true; break; }
+      ST_STAMP(t_f0)
+      const bool fok = factor();
+      ST_ACC(ST_FACT, t_f0)
+      if (!fok) { fail = true; break; }
 
       // (c) predictor: h = gr + C'(W rp - lam)
       auto set_h = [&](const double* rc_over_s) {
@@ -604,8 +640,13 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
         }
         __syncthreads();
       };
+      ST_STAMP(t_q0)
       set_h(la);
+      ST_ACC(ST_STEP, t_q0)
+      ST_STAMP(t_q1)
       lq_solve();
+      ST_ACC(ST_SOLVE, t_q1)
+      ST_STAMP(t_q2)
       double dsa[NR], dla[NR], cdv[NR], dvk[9];
       double amin = 1.0;
 #pragma unroll
@@ -632,7 +673,11 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
 #pragma unroll
       for (int i = 0; i < NR; ++i) rcs[i] = R.m[i] * (sl[i] * la[i] + dsa[i] * dla[i] - smu) / sl[i];
       set_h(rcs);
+      ST_ACC(ST_STEP, t_q2)
+      ST_STAMP(t_q3)
       lq_solve();
+      ST_ACC(ST_SOLVE, t_q3)
+      ST_STAMP(t_q4)
 #pragma unroll
       for (int e = 0; e < 9; ++e) dvk[e] = s.u.q.dv[k][e];
       row_values(R, dvk, cdv);
@@ -656,6 +701,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
         for (int e = 0; e < 9; ++e) s.u.q.v[k][e] = vk[e] + alpha * dvk[e];
       }
       __syncthreads();
+      ST_ACC(ST_STEP, t_q4)
     }
     it_total += it;
     it_max = max(it_max, it);
@@ -692,10 +738,17 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     A.status[b] = st;
     A.iters[b] = it_total;
     if (A.diag) {
-      A.diag[(size_t)b * 4 + 0] = last_res;
-      A.diag[(size_t)b * 4 + 1] = last_mu;
-      A.diag[(size_t)b * 4 + 2] = double((any_fail ? 1 : 0) | (all_conv ? 2 : 0));
-      A.diag[(size_t)b * 4 + 3] = double(it_max);
+#ifdef VC_TIMING
+      constexpr size_t DS = 4 + ST_NSLOT;
+      tacc[ST_TOTAL] = __builtin_amdgcn_s_memtime() - t_start;
+      for (int i = 0; i < ST_NSLOT; ++i) A.diag[(size_t)b * DS + 4 + i] = double(tacc[i]);
+#else
+      constexpr size_t DS = 4;
+#endif
+      A.diag[(size_t)b * DS + 0] = last_res;
+      A.diag[(size_t)b * DS + 1] = last_mu;
+      A.diag[(size_t)b * DS + 2] = double((any_fail ? 1 : 0) | (all_conv ? 2 : 0));
+      A.diag[(size_t)b * DS + 3] = double(it_max);
     }
   }
 }

@@ -20,10 +20,12 @@
 #define VC_DIAG_COLS 13      // 4 diagnostics + 9 section-cycle counters (kin_ltv.hip T_*)
 #define VC_DYN_DIAG_COLS 19  // 4 diagnostics + 15 section-cycle counters (dyn_sqp.hip DT_*)
 #define VC_CASC_DIAG_COLS 17 // 4 diagnostics + 13 section-cycle counters (casc_sqp.hip CT_*)
+#define VC_ST_DIAG_COLS 13   // 4 diagnostics + 9 section-cycle counters (st_sqp.hip ST_*)
 #else
 #define VC_DIAG_COLS 4
 #define VC_DYN_DIAG_COLS 4
 #define VC_CASC_DIAG_COLS 4
+#define VC_ST_DIAG_COLS 4
 #endif
 
 struct vc_ctx {
@@ -237,7 +239,7 @@ int st_solve(vc_ctx* c, int B, const void* x0, const void* kappa, const void* ds
              {nullptr, u0, (size_t)B * nu * 8, nullptr},
              {nullptr, status, (size_t)B * 4, nullptr},
              {nullptr, iters, (size_t)B * 4, nullptr},
-             {nullptr, diag, diag ? (size_t)B * 4 * 8 : 0, nullptr}};
+             {nullptr, diag, diag ? (size_t)B * VC_ST_DIAG_COLS * 8 : 0, nullptr}};
     if (int r = stage(c, slots)) return r;
     a.x0 = (const double*)slots[0].dev;
     a.kappa = (const double*)slots[1].dev;
