@@ -84,6 +84,16 @@ struct StSmem {
   int flag[4];
 };
 
+// Workgroup = one wavefront: LDS operations of a wave execute in order, so a sync only has to
+// stop the compiler from moving memory operations across it (no s_barrier, and no wait for
+// outstanding loads other than the ones actually used).
+#define WSYNC()                          \
+  do {                                   \
+    asm volatile("" ::: "memory");       \
+    __builtin_amdgcn_wave_barrier();     \
+    asm volatile("" ::: "memory");       \
+  } while (0)
+
 __device__ __forceinline__ double bcast(double v, int l) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
   const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
@@ -200,7 +210,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
   uint64_t tacc[ST_NSLOT] = {};
   const uint64_t t_start = __builtin_amdgcn_s_memtime();
 #endif
-  __syncthreads();
+  WSYNC();
 
   // Riccati lane roles (fixed per lane): H entry (hi, hj), hi <= hj, for lanes < 45
   int hi = 0, hj = 0;
@@ -248,7 +258,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       }
       if (!fin) s.flag[0] = VC_NONFINITE;
     }
-    __syncthreads();
+    WSYNC();
     ST_ACC(ST_PRED, t_p0)
     if (sq == W.sqp_iters || s.flag[0] == VC_NONFINITE) break;
 
@@ -306,7 +316,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
         }
       }
     }
-    __syncthreads();
+    WSYNC();
     ST_ACC(ST_LIN, t_l0)
     ST_STAMP(t_s0)
 
@@ -418,141 +428,232 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
 #pragma unroll
     for (int i = 0; i < NR; ++i) mc += R.m[i];
     const double mcount = wsum(mc);
-    __syncthreads();  // the linearisation scratch is dead from here: the QP arrays alias it
+    WSYNC();  // the linearisation scratch is dead from here: the QP arrays alias it
     if (stl) {
 #pragma unroll
       for (int e = 0; e < 9; ++e) s.u.q.v[k][e] = 0.0;
     }
-    __syncthreads();
+    WSYNC();
     ST_ACC(ST_SETUP, t_s0)
 
     // ---- LQ machinery -----------------------------------------------------------------
+    // Every stage loop below is branch-free in its lanes (clamped addresses, 0/1 masks) and
+    // loads the next stage's operands before the current stage's dependent chain, so LDS
+    // latency stays off the recursion; cross-lane values move by v_readlane.
+    //
     // Riccati factorisation of the stage Hessians s.u.q.Qt (backward): K, Hi per stage.
-    auto factor = [&]() -> bool {
-      bool ok = true;
-#pragma unroll 1
-      for (int kk = N - 1; kk >= 0; --kk) {
-        if (kk < N - 1) {
-          // T = P [A6 | B6 ; 0 | e_Fx]  (7 x 8)
-          if (l < 56) {
-            const int a = l >> 3, j = l & 7;
-            double acc = j == 6 ? s.P[a][6] : 0.0;
+    //   T = P [A6 B6 ; 0 e_Fx]      lanes 0..55  (a, j) = (l / 8, l % 8)
+    //   H = Qt + [..]' T            lanes 0..44  (hi, hj)
+    //   P' = Hxx - Hux' Huu^-1 Hux  lanes 0..27, K = -Huu^-1 Hux lanes 28..41, Huu^-1 lane 42
+    const int ta = l < 56 ? (l >> 3) : 0, tj = l & 7;
+    const double tpm = tj == 6 ? 1.0 : 0.0;
+    const int hcic = hci < 0 ? 0 : hci, hcjc = hcj < 0 ? 0 : hcj;
+    const double hdyn = (l < 45 && hci >= 0 && hcj >= 0) ? 1.0 : 0.0, hpm = hci == 6 ? 1.0 : 0.0;
+    const int hsc = hslot < 0 ? 0 : hslot;
+    const double hq = (l < 45 && hslot >= 0) ? 1.0 : 0.0;
+    // The stage loops are unrolled by two with ping-pong operand buffers (A for kk, B for
+    // the next stage): no register rotation at the loop latch, so the next stage's loads
+    // stay in flight across the current stage's chain.
+    struct FacOps {
+      double JT[6], JH[6], qv;
+    };
+    auto fac_load = [&](int kk, FacOps& o) {
 #pragma unroll
-            for (int e = 0; e < 6; ++e) acc += s.P[a][e] * s.J[kk][e][j];
-            s.T[a][j] = acc;
-          }
-          __syncthreads();
-        }
-        if (l < 45) {
-          double hv = hslot >= 0 ? s.u.q.Qt[kk][hslot] : 0.0;
-          if (kk < N - 1 && hci >= 0 && hcj >= 0) {
-            double acc = hci == 6 ? s.T[6][hcj] : 0.0;
+      for (int e = 0; e < 6; ++e) {
+        o.JT[e] = s.J[kk][e][tj];
+        o.JH[e] = s.J[kk][e][hcic];
+      }
+      o.qv = s.u.q.Qt[kk][hsc];
+    };
+    auto fac_stage = [&](int kk, const FacOps& o) -> bool {
+      double hv = hq * o.qv;
+      if (kk < N - 1) {  // uniform
+        double acc = tpm * s.P[ta][6];
 #pragma unroll
-            for (int e = 0; e < 6; ++e) acc += s.J[kk][e][hci] * s.T[e][hcj];
-            hv += acc;
-          }
-          s.Hm[hi][hj] = hv;
-          s.Hm[hj][hi] = hv;
-        }
-        __syncthreads();
-        const double h00 = s.Hm[7][7], h01 = s.Hm[7][8], h11 = s.Hm[8][8];
-        const double det = h00 * h11 - h01 * h01;
-        ok = ok && h00 > 0.0 && det > 0.0;
-        const double id = 1.0 / det;
-        const double i00 = h11 * id, i01 = -h01 * id, i11 = h00 * id;
+        for (int e = 0; e < 6; ++e) acc += s.P[ta][e] * o.JT[e];
+        if (l < 56) s.T[ta][tj] = acc;
+        WSYNC();
+        double a2 = hpm * s.T[6][hcjc];
+#pragma unroll
+        for (int e = 0; e < 6; ++e) a2 += o.JH[e] * s.T[e][hcjc];
+        hv += hdyn * a2;
+      }
+      if (l < 45) {
+        s.Hm[hi][hj] = hv;
+        s.Hm[hj][hi] = hv;
+      }
+      WSYNC();
+      const double h00 = s.Hm[7][7], h01 = s.Hm[7][8], h11 = s.Hm[8][8];
+      const double det = h00 * h11 - h01 * h01;
+      // 1 / det: v_rcp_f64 + two Newton steps (full fp64 accuracy, no IEEE divide sequence)
+      double id = __builtin_amdgcn_rcp(det);
+      id = id * (2.0 - det * id);
+      id = id * (2.0 - det * id);
+      const double i00 = h11 * id, i01 = -h01 * id, i11 = h00 * id;
+      {
+        // lanes 0..27: P entry (pi, pj); lanes 28..41: K entry; lane 42: Huu^-1
+        const int kc = l >= 28 && l < 42 ? (l - 28) / 7 : 0, ki = l >= 28 && l < 42 ? (l - 28) % 7 : 0;
+        const int ci = l < 28 ? pi : ki;
+        const double x0 = s.Hm[7][ci], x1 = s.Hm[8][ci], y0 = s.Hm[7][pj], y1 = s.Hm[8][pj];
+        const double hpp = s.Hm[pi][pj];
         if (l < 28) {
-          const double x0 = s.Hm[7][pi], x1 = s.Hm[8][pi], y0 = s.Hm[7][pj], y1 = s.Hm[8][pj];
-          const double pv = s.Hm[pi][pj] - (x0 * (i00 * y0 + i01 * y1) + x1 * (i01 * y0 + i11 * y1));
+          const double pv = hpp - (x0 * (i00 * y0 + i01 * y1) + x1 * (i01 * y0 + i11 * y1));
           s.P[pi][pj] = pv;
           s.P[pj][pi] = pv;
         } else if (l < 42) {
-          const int cc = (l - 28) / 7, i = (l - 28) % 7;
-          const double x0 = s.Hm[7][i], x1 = s.Hm[8][i];
-          s.u.q.K[kk][cc][i] = cc == 0 ? -(i00 * x0 + i01 * x1) : -(i01 * x0 + i11 * x1);
+          s.u.q.K[kk][kc][ki] = kc == 0 ? -(i00 * x0 + i01 * x1) : -(i01 * x0 + i11 * x1);
         } else if (l == 42) {
           s.u.q.Hi[kk][0] = i00;
           s.u.q.Hi[kk][1] = i01;
           s.u.q.Hi[kk][2] = i11;
         }
-        __syncthreads();
+      }
+      WSYNC();
+      return h00 > 0.0 && det > 0.0;
+    };
+    // Riccati factorisation of the stage Hessians s.u.q.Qt (backward): K, Hi per stage.
+    auto factor = [&]() -> bool {
+      bool ok = true;
+      FacOps A0, B0;
+      fac_load(N - 1, A0);
+#pragma unroll 1
+      for (int kk = N - 1; kk >= 0; kk -= 2) {
+        const int k1 = kk >= 1 ? kk - 1 : 0, k2 = kk >= 2 ? kk - 2 : 0;
+        fac_load(k1, B0);
+        ok = fac_stage(kk, A0) && ok;
+        if (kk >= 1) {  // uniform
+          fac_load(k2, A0);
+          ok = fac_stage(kk - 1, B0) && ok;
+        }
       }
       return ok;
+    };
+
+    // Sweep lanes 0..8 own the stage-vector components v = (y0..y5, p, dFx, dw).
+    const int sl9 = l < 9 ? l : 8;
+    const int scol = vcol(sl9) < 0 ? 0 : vcol(sl9);                 // column of [A6 | B6]
+    const double smsk = (l < 9 && vcol(sl9) >= 0) ? 1.0 : 0.0;      // p (l = 6) has no dynamics column
+    const double spm = (l < 9 && vcol(sl9) == 6) ? 1.0 : 0.0;       // dFx picks up the p costate
+    // backward pass extras: lanes 0..6 read K[kk][0][l], K[kk][1][l]; lanes 7, 8 read the
+    // Huu^-1 pair of their kk component -> one formula t = a gu0 + b gu1 for both
+    const int bl7 = l < 7 ? l : 0;
+    // forward pass: lanes 0..5 read J row l; lanes 7, 8 read K row (l - 7) and kk
+    const int fr = l < 6 ? l : 0, fc = l == 8 ? 1 : 0;
+    const bool fk = l == 7 || l == 8;
+
+    struct BwdOps {
+      double J6[6], h, a, b;
+    };
+    // vec: s.u.q.h (solve) or s.u.q.gr (dual residual)
+    auto bwd_load = [&](int kk, const double (*vec)[9], BwdOps& o) {
+#pragma unroll
+      for (int e = 0; e < 6; ++e) o.J6[e] = s.J[kk][e][scol];
+      o.h = vec[kk][sl9];
+      // lane-selected addresses, one unconditional load each (a value select would make
+      // the compiler predicate the loads and wait on the whole prefetch)
+      const double* pa = l < 7 ? &s.u.q.K[kk][0][bl7] : &s.u.q.Hi[kk][l == 7 ? 0 : 1];
+      const double* pb = l < 7 ? &s.u.q.K[kk][1][bl7] : &s.u.q.Hi[kk][l == 7 ? 1 : 2];
+      o.a = *pa;
+      o.b = *pb;
+    };
+    // g = vec_k + [A6 | B6 ; 0 e_Fx]' p_{k+1} on lanes 0..8
+    auto bwd_g = [&](int kk, const BwdOps& o, double pv) -> double {
+      double g = o.h;
+      if (kk < N - 1) {  // uniform
+        double pb[7];
+#pragma unroll
+        for (int a = 0; a < 7; ++a) pb[a] = bcast(pv, a);
+        double acc = spm * pb[6];
+#pragma unroll
+        for (int e = 0; e < 6; ++e) acc += o.J6[e] * pb[e];
+        g += smsk * acc;
+      }
+      return g;
+    };
+    struct FwdOps {
+      double w[8];
+    };
+    auto fwd_load = [&](int kk, FwdOps& o) {
+      const double* src = fk ? &s.u.q.K[kk][fc][0] : &s.J[kk][fr][0];
+      const double* src7 = fk ? &s.u.q.kk[kk][fc] : &s.J[kk][fr][7];
+#pragma unroll
+      for (int e = 0; e < 7; ++e) o.w[e] = src[e];
+      o.w[7] = *src7;
+    };
+    // one forward stage: writes dv[kk], returns xt_{k+1} (lanes 0..6)
+    auto fwd_stage = [&](int kk, const FwdOps& o, double X) -> double {
+      double xb[7];
+#pragma unroll
+      for (int a = 0; a < 7; ++a) xb[a] = bcast(X, a);
+      double acc = 0.0;
+#pragma unroll
+      for (int e = 0; e < 6; ++e) acc += o.w[e] * xb[e];
+      const double uk = acc + o.w[6] * xb[6] + o.w[7];  // lanes 7, 8: u_c = K_c xt + kk_c
+      const double u0 = bcast(uk, 7), u1 = bcast(uk, 8);
+      if (l < 9) s.u.q.dv[kk][l] = fk ? uk : X;
+      const double xn = acc + o.w[6] * u0 + o.w[7] * u1;  // lanes 0..5
+      return l < 6 ? xn : (l == 6 ? u0 : 0.0);
     };
 
     // LQ solve with linear terms s.u.q.h -> direction s.u.q.dv (backward vector pass with the
     // factor, then the forward rollout u = K xt + kk)
     auto lq_solve = [&]() {
+      BwdOps A1, B1;
+      bwd_load(N - 1, s.u.q.h, A1);
       double pv = 0.0;  // lanes 0..6: p_{k+1}
-#pragma unroll 1
-      for (int kk = N - 1; kk >= 0; --kk) {
-        double g = l < 9 ? s.u.q.h[kk][l] : 0.0;
-        if (kk < N - 1) {
-          double pb[7];
-#pragma unroll
-          for (int a = 0; a < 7; ++a) pb[a] = bcast(pv, a);
-          if (sc >= 0) {
-            double acc = sc == 6 ? pb[6] : 0.0;
-#pragma unroll
-            for (int e = 0; e < 6; ++e) acc += s.J[kk][e][sc] * pb[e];
-            g += acc;
-          }
-        }
+      auto bstage = [&](int kk, const BwdOps& o) {
+        const double g = bwd_g(kk, o, pv);
         const double gu0 = bcast(g, 7), gu1 = bcast(g, 8);
-        const double* Hk = s.u.q.Hi[kk];
-        const double k0 = -(Hk[0] * gu0 + Hk[1] * gu1), k1 = -(Hk[1] * gu0 + Hk[2] * gu1);
-        if (l == 0) {
-          s.u.q.kk[kk][0] = k0;
-          s.u.q.kk[kk][1] = k1;
+        const double t2 = o.a * gu0 + o.b * gu1;
+        pv = g + t2;
+        if (fk) s.u.q.kk[kk][l - 7] = -t2;
+      };
+#pragma unroll 1
+      for (int kk = N - 1; kk >= 0; kk -= 2) {
+        const int k1 = kk >= 1 ? kk - 1 : 0, k2 = kk >= 2 ? kk - 2 : 0;
+        bwd_load(k1, s.u.q.h, B1);
+        bstage(kk, A1);
+        if (kk >= 1) {
+          bwd_load(k2, s.u.q.h, A1);
+          bstage(kk - 1, B1);
         }
-        const int li = l < 7 ? l : 0;
-        pv = l < 7 ? g + s.u.q.K[kk][0][li] * gu0 + s.u.q.K[kk][1][li] * gu1 : 0.0;
       }
-      __syncthreads();
+      WSYNC();
+      FwdOps A2, B2;
+      fwd_load(0, A2);
       double X = 0.0;  // lanes 0..6: xt_k
 #pragma unroll 1
-      for (int kk = 0; kk < N; ++kk) {
-        double xb[7];
-#pragma unroll
-        for (int a = 0; a < 7; ++a) xb[a] = bcast(X, a);
-        double u0 = s.u.q.kk[kk][0], u1 = s.u.q.kk[kk][1];
-#pragma unroll
-        for (int a = 0; a < 7; ++a) {
-          u0 += s.u.q.K[kk][0][a] * xb[a];
-          u1 += s.u.q.K[kk][1][a] * xb[a];
-        }
-        if (l < 7) s.u.q.dv[kk][l] = X;
-        if (l == 7) s.u.q.dv[kk][7] = u0;
-        if (l == 8) s.u.q.dv[kk][8] = u1;
-        if (kk < N - 1) {
-          const int r = l < 6 ? l : 0;
-          double xn = s.J[kk][r][6] * u0 + s.J[kk][r][7] * u1;
-#pragma unroll
-          for (int e = 0; e < 6; ++e) xn += s.J[kk][r][e] * xb[e];
-          X = l < 6 ? xn : (l == 6 ? u0 : 0.0);
+      for (int kk = 0; kk < N; kk += 2) {
+        const int k1 = kk + 1 < N ? kk + 1 : kk, k2 = kk + 2 < N ? kk + 2 : kk;
+        fwd_load(k1, B2);
+        X = fwd_stage(kk, A2, X);
+        if (kk + 1 < N) {
+          fwd_load(k2, A2);
+          X = fwd_stage(kk + 1, B2, X);
         }
       }
-      __syncthreads();
+      WSYNC();
     };
 
     // condensed dual residual max |d/du (sum_k gr_k . v_k)| through the dynamics (adjoint sweep)
     auto dual_residual = [&]() -> double {
+      BwdOps A3, B3;
+      bwd_load(N - 1, s.u.q.gr, A3);
       double rho = 0.0, rmax = 0.0;
+      auto rstage = [&](int kk, const BwdOps& o) {
+        const double g = bwd_g(kk, o, rho);
+        rmax = fk ? fmax(rmax, fabs(g)) : rmax;
+        rho = g;
+      };
 #pragma unroll 1
-      for (int kk = N - 1; kk >= 0; --kk) {
-        double g = l < 9 ? s.u.q.gr[kk][l] : 0.0;
-        if (kk < N - 1) {
-          double pb[7];
-#pragma unroll
-          for (int a = 0; a < 7; ++a) pb[a] = bcast(rho, a);
-          if (sc >= 0) {
-            double acc = sc == 6 ? pb[6] : 0.0;
-#pragma unroll
-            for (int e = 0; e < 6; ++e) acc += s.J[kk][e][sc] * pb[e];
-            g += acc;
-          }
+      for (int kk = N - 1; kk >= 0; kk -= 2) {
+        const int k1 = kk >= 1 ? kk - 1 : 0, k2 = kk >= 2 ? kk - 2 : 0;
+        bwd_load(k1, s.u.q.gr, B3);
+        rstage(kk, A3);
+        if (kk >= 1) {
+          bwd_load(k2, s.u.q.gr, A3);
+          rstage(kk - 1, B3);
         }
-        if (l == 7 || l == 8) rmax = fmax(rmax, fabs(g));
-        rho = l < 7 ? g : 0.0;
       }
       return wmax(rmax);
     };
@@ -608,7 +709,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
         rpm = 0.0;
         mus = 0.0;
       }
-      __syncthreads();
+      WSYNC();
       rpm = wmax(rpm);
       const double mu = wsum(mus) / mcount;
       ST_ACC(ST_RESID, t_r0)
@@ -638,7 +739,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
 #pragma unroll
           for (int e = 0; e < 9; ++e) s.u.q.h[k][e] = hk[e];
         }
-        __syncthreads();
+        WSYNC();
       };
       ST_STAMP(t_q0)
       set_h(la);
@@ -700,7 +801,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
 #pragma unroll
         for (int e = 0; e < 9; ++e) s.u.q.v[k][e] = vk[e] + alpha * dvk[e];
       }
-      __syncthreads();
+      WSYNC();
       ST_ACC(ST_STEP, t_q4)
     }
     it_total += it;
@@ -713,7 +814,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       s.ub[k][0] += s.u.q.v[k][7] * S;
       s.ub[k][1] += s.u.q.v[k][8];
     }
-    __syncthreads();
+    WSYNC();
   }
 
   // ---------------- outputs: u*, x* = rollout(u*), u0, status ----------------

@@ -11,8 +11,10 @@ at import, :13), the same horizon-parameter construction ``_init_horizon``
 and ``get_state_prediction`` (:340-352).
 
 What changes is the solve (cascaded_mpc.py:308, IPOPT + HSL MA27 on the NLP): a fixed
-number of sequential-QP iterations in one fused fp32 gfx950 kernel (csrc/dyn_sqp.hip;
-contract: oracle/dyn_sqp.py).  ``BatchedSingleTrackMPC`` is the same controller for B
+number of sequential-QP iterations in one fused gfx950 kernel -- fp64 with a stagewise
+Riccati interior point by default (csrc/st_sqp.hip, N = 20..60), or the condensed fp32
+kernel of BASELINE config 3 (csrc/dyn_sqp.hip, N = 40, ``dtype="f32"``); contract:
+oracle/dyn_sqp.py.  ``BatchedSingleTrackMPC`` is the same controller for B
 vehicles at once.  With ``horizon_pm > 0`` (the cascaded point-mass tail,
 cascaded_mpc.py:181-277) ``CascadedMPC`` / ``BatchedCascadedMPC`` run the fp64 cascaded
 SQP (csrc/casc_sqp.hip, contract oracle/casc_sqp.py); obstacle barrier terms
@@ -43,19 +45,27 @@ def dyn_horizon_params(s0, ux_pred, mpc_dt, k_of_s):
 
 
 class BatchedSingleTrackMPC(Controller):
-    """B independent single-track NMPCs solved in one launch (fp32, N = horizon)."""
+    """B independent single-track NMPCs solved in one launch (N = horizon).
 
-    def __init__(self, car, config, batch: int, device: int = 0, seed: int | None = 31):
+    ``dtype="f64"`` (default, the reference's precision) runs the stagewise-Riccati SQP
+    (csrc/st_sqp.hip, N = 20..60, the reference's own horizons included); ``"f32"`` the
+    condensed fp32 kernel of BASELINE config 3 (csrc/dyn_sqp.hip, N = 40)."""
+
+    def __init__(self, car, config, batch: int, device: int = 0, seed: int | None = 31, dtype: str = "f64"):
         super().__init__()
         if int(config.get("horizon_pm", 0)) > 0:
             raise ValueError("horizon_pm > 0: use BatchedCascadedMPC (the point-mass tail, cascaded_mpc.py:181-277)")
+        if dtype not in ("f64", "f32"):
+            raise ValueError(f"dtype must be 'f64' or 'f32', got {dtype!r}")
         self.config = config
         self.car = car
         self.N = int(config["horizon"])
         self.dt = float(config["mpc_dt"])
         self.ns, self.na = len(car.state), len(car.input)
         self.B = int(batch)
-        self.ctx = Context(model=_abi.VC_MODEL_DYNAMIC, N=self.N, max_batch=self.B, dtype=_abi.VC_F32, device=device,
+        self.np_dtype = np.float64 if dtype == "f64" else np.float32
+        vdt = _abi.VC_F64 if dtype == "f64" else _abi.VC_F32
+        self.ctx = Context(model=_abi.VC_MODEL_DYNAMIC, N=self.N, max_batch=self.B, dtype=vdt, device=device,
                            params=make_params(dyn_car=car.config, dyn_mpc=config, tyre=getattr(car, "tyre", "fiala"),
                                               obstacles=obstacle_list(car, config)))
         # warm starts: cascaded_mpc.py:72-76
@@ -77,16 +87,17 @@ class BatchedSingleTrackMPC(Controller):
         simulator instead swallows the solver exception (racing.py:416-423)."""
         x0 = np.asarray(states, np.float64).reshape(self.B, self.ns)
         ds, kappa = dyn_horizon_params(x0[:, IS], self.state_prediction[:, IUX, :], self.dt, self.car.track.k)
-        ubar = np.ascontiguousarray(np.swapaxes(self.action_prediction, 1, 2), dtype=np.float32)
+        cast = lambda a: np.ascontiguousarray(a, dtype=self.np_dtype)
+        ubar = cast(np.swapaxes(self.action_prediction, 1, 2))
         ic = self.config["input_constraints"]
         np.clip(ubar[..., IW], ic["w_min"], ic["w_max"], out=ubar[..., IW])
-        f32 = lambda a: np.ascontiguousarray(a, dtype=np.float32)
-        x0f, kf, dsf = f32(x0), f32(kappa), f32(ds)
+        x0f, kf, dsf = cast(x0), cast(kappa), cast(ds)
         u0, xbar, ustar, status, iters = self.ctx.solve(x0f, kf, dsf, ubar)
         bad = status != 0
         if bad.any():
             idx = np.nonzero(bad)[0]
-            r = self.ctx.solve(f32(x0f[idx]), f32(kf[idx]), f32(dsf[idx]), np.zeros((len(idx), self.N, self.na), np.float32))
+            r = self.ctx.solve(cast(x0f[idx]), cast(kf[idx]), cast(dsf[idx]),
+                               np.zeros((len(idx), self.N, self.na), self.np_dtype))
             u0[idx], xbar[idx], ustar[idx], status[idx], iters[idx] = r
         self.action_prediction = np.swapaxes(ustar, 1, 2).astype(np.float64)
         self.state_prediction = np.swapaxes(xbar, 1, 2).astype(np.float64)
@@ -182,17 +193,18 @@ class BatchedCascadedMPC(Controller):
 
 class CascadedMPC(BatchedSingleTrackMPC):
     """Single-vehicle drop-in for ``CascadedMPC(car, point_mass, config)`` (cascaded_mpc.py:16-39).
-    ``horizon_pm: 0`` runs the single-track SQP (csrc/dyn_sqp.hip, fp32); ``horizon_pm > 0``
+    ``horizon_pm: 0`` runs the single-track SQP (fp64 csrc/st_sqp.hip by default, fp32
+    csrc/dyn_sqp.hip with ``dtype="f32"``); ``horizon_pm > 0``
     returns a :class:`CascadedTailMPC` (point-mass tail, csrc/casc_sqp.hip, fp64)."""
 
-    def __new__(cls, car, point_mass, config, device: int = 0):
+    def __new__(cls, car, point_mass, config, device: int = 0, dtype: str = "f64"):
         if cls is CascadedMPC and int(config.get("horizon_pm", 0) or 0) > 0:
             return object.__new__(CascadedTailMPC)
         return object.__new__(cls)
 
-    def __init__(self, car, point_mass, config, device: int = 0):
+    def __init__(self, car, point_mass, config, device: int = 0, dtype: str = "f64"):
         self.point_mass = point_mass
-        super().__init__(car, config, batch=1, device=device, seed=None)
+        super().__init__(car, config, batch=1, device=device, seed=None, dtype=dtype)
         self.state_prediction = self.state_prediction[0]
         # cascaded_mpc.py:74-76 draws from the global numpy RNG seeded at import
         self.action_prediction = np.ones((self.na, self.N)) + np.random.random((self.na, self.N))
@@ -218,7 +230,7 @@ class CascadedTailMPC(BatchedCascadedMPC, CascadedMPC):
     """``CascadedMPC(car, point_mass, config)`` with ``horizon_pm > 0`` (the reference's
     cascaded controller, config/controllers/cascaded.yaml) for one vehicle."""
 
-    def __init__(self, car, point_mass, config, device: int = 0):
+    def __init__(self, car, point_mass, config, device: int = 0, dtype: str = "f64"):
         self.point_mass = point_mass
         BatchedCascadedMPC.__init__(self, car, config, batch=1, device=device, seed=None)
         self.state_prediction = self.state_prediction[0]
