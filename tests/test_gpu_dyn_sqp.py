@@ -176,11 +176,14 @@ def test_sqp_edge_batches(sqp, golden):
 def test_unsupported_dynamic_combination():
     from vcmpc import Context, _abi
     from vcmpc.config import load_config
-    with Context(model=_abi.VC_MODEL_DYNAMIC, N=40, max_batch=4, dtype=_abi.VC_F64,
-                 dyn_car=load_config("dynamic_car")) as c:
-        with pytest.raises(_abi.VcError) as e:
-            c.solve(np.zeros((1, 8)), np.zeros((1, N)), np.zeros((1, N)), np.zeros((1, N, 2)))
-        assert e.value.code == _abi.VC_E_UNSUPPORTED
+    # fp64 single-track contexts are built at N = 20, 30, 40, 50, 60 (st_sqp.hip), fp32 at 40
+    for n, dt in ((45, _abi.VC_F64), (50, _abi.VC_F32)):
+        with Context(model=_abi.VC_MODEL_DYNAMIC, N=n, max_batch=4, dtype=dt, dyn_car=load_config("dynamic_car"),
+                     dyn_mpc=load_config("dynamic_mpc")) as c:
+            z = np.float64 if dt == _abi.VC_F64 else np.float32
+            with pytest.raises(_abi.VcError) as e:
+                c.solve(np.zeros((1, 8), z), np.zeros((1, n), z), np.zeros((1, n), z), np.zeros((1, n, 2), z))
+            assert e.value.code == _abi.VC_E_UNSUPPORTED
 
 
 @pytest.mark.parametrize("tyre", ["linear", "fiala"])
