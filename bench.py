@@ -528,6 +528,7 @@ def run_c5(args, dev, stream, rank, world, dist):
     import numpy as np
     import torch
 
+    from vcmpc import _abi
     from vcmpc.config import load_config
     from vcmpc.environment import Track
     from vcmpc.models import DynamicCar
@@ -568,7 +569,8 @@ def run_c5(args, dev, stream, rank, world, dist):
     vsteps, elapsed_max, gpu_ms_max = dist.aggregate(float(B * K), elapsed, gpu_ms, dev)
     out = {"metric": "closed-loop vehicle-steps/s (N=40 NMPC solve + fp64 plant per vehicle-step)",
            "value": vsteps / elapsed_max, "unit": "vehicle-steps/s", "solves_per_s": vsteps / elapsed_max,
-           "steps": K, "ms_per_step": elapsed_max / K * 1e3, "gpu_ms_total": gpu_ms_max, "dtype": "f32 solve, f64 plant",
+           "steps": K, "ms_per_step": elapsed_max / K * 1e3, "gpu_ms_total": gpu_ms_max,
+           "dtype": ("f64" if sim.ctx.dtype == _abi.VC_F64 else "f32") + " solve, f64 plant",
            "scaling": "strong",
            "config": {"workload": f"C5 closed loop on ippodromo: {args.c5_vehicles} vehicles x {K} steps (dt 0.05 s), "
                                   f"dynamic-bicycle (Fiala) single-track NMPC N={C3_N}, mpc_dt {C5_MPC_DT}, "

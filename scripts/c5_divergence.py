@@ -24,10 +24,12 @@ def main():
     ap.add_argument("--vehicles", type=int, default=8192)
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--seed", type=int, default=31)
+    ap.add_argument("--fp32", action="store_true", help="fp32 solve (dyn_sqp.hip) instead of fp64 (st_sqp.hip)")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "c5_div.npz"))
     args = ap.parse_args()
     import torch
 
+    from vcmpc import _abi
     from vcmpc.config import load_config
     from vcmpc.environment import Track
     from vcmpc.models import DynamicCar
@@ -40,7 +42,8 @@ def main():
     cfg["mpc_dt"] = C5_MPC_DT
     car = DynamicCar(load_config("dynamic_car"), track, tyre="fiala")
     B, K = args.vehicles, args.steps
-    sim = BatchedRacingSimulator(car, cfg, track, batch=B, device=0)
+    dt = _abi.VC_F32 if args.fp32 else _abi.VC_F64
+    sim = BatchedRacingSimulator(car, cfg, track, batch=B, device=0, dtype=dt)
     sim.reset(x_all)
     sim._init_warm_start(args.seed)
     xb0, ub0 = sim.xbar.clone(), sim.ubar.clone()
@@ -59,7 +62,7 @@ def main():
         np.savez(args.out, bad=bad)
         return
     nb = len(bad)
-    sub = BatchedRacingSimulator(car, cfg, track, batch=nb, device=0)
+    sub = BatchedRacingSimulator(car, cfg, track, batch=nb, device=0, dtype=dt)
     sub.reset(x_all[bad])
     sub.xbar.copy_(xb0[bad])
     sub.ubar.copy_(ub0[bad])

@@ -1,0 +1,229 @@
+"""Design prototype (numpy) of the stagewise Riccati interior point for the kinematic LTV-QP
+contract (oracle/ltv_qp.py), before it is written as the fp64 HIP kernel csrc/kin_ric.hip
+(any horizon N <= 63: the reference's kinematic.yaml uses N = 50, where the condensed
+n = 100 formulation of kin_ltv.hip would pay an O(n^3) factorisation per iteration).
+
+Stage form: QP state xt_k = (dv, ddelta, dey, depsi, p_k), p_k = da_{k-1} (the slew
+w_a (a_{k+1} - a_k)^2 couples neighbouring inputs), input u_k = (da, dw), stages k = 0..N
+(stage N has no input).  s is fixed (s' = 1) and t enters only the terminal w_time t_N, a
+linear term on each stage's y through the t-row of its Jacobian.  Every constraint row is a
+bound on one stage variable, so the barrier Hessian is diagonal and the stage Hessians keep
+the pattern diag + (p, da).
+
+    python scripts/kin_riccati_proto.py
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "vehicle-control_amd")]
+
+from oracle import ltv_qp as Q  # noqa: E402
+from oracle import obstacles as OB  # noqa: E402
+
+Y = [0, 1, 3, 4]          # v, delta, ey, epsi
+NXT, NV = 5, 7            # QP state (y, p), stage vector (y, p, da, dw)
+# rows: (variable, sign): da <= , -da <=, dw <=, -dw <=, -dv <=, ddelta <=, -ddelta <=
+ROWS = [(5, 1.0), (5, -1.0), (6, 1.0), (6, -1.0), (0, -1.0), (1, 1.0), (1, -1.0)]
+
+
+def stage_qp(x0, ubar, kappa, ds, L, W):
+    B, N = ubar.shape[:2]
+    xbar = Q.kin_predict(x0, ubar, kappa, ds, L)
+    A, Bm = Q.kin_linearize(xbar, ubar, kappa, ds, L)
+    F = np.zeros((B, N, NXT, NV))          # xt_{k+1} = F_k v_k
+    F[:, :, :4, :4] = A[:, :, Y][:, :, :, Y]
+    F[:, :, :4, 5:] = Bm[:, :, Y]
+    F[:, :, 4, 5] = 1.0
+    assert np.abs(A[:, :, Y][:, :, :, [2, 5]]).max() == 0.0 and np.abs(Bm[:, :, 5]).max() == 0.0
+    trow = A[:, :, 5][:, :, Y]             # d t_{k+1} / d y_k
+    Qm = np.zeros((B, N + 1, NV, NV))
+    q = np.zeros((B, N + 1, NV))
+    for k in range(1, N):
+        ey = xbar[:, k, Q.IEY]
+        c = W["w_dev"] * ds[:, k] + np.where(ey < W["ey_min"], W["w_b"] * ds[:, k], 0.0) \
+            + np.where(ey > W["ey_max"], W["w_b"] * ds[:, k], 0.0)
+        r0 = (W["w_dev"] * ds[:, k] * ey + np.where(ey < W["ey_min"], W["w_b"] * ds[:, k] * (ey - W["ey_min"]), 0.0)
+              + np.where(ey > W["ey_max"], W["w_b"] * ds[:, k] * (ey - W["ey_max"]), 0.0))
+        Qm[:, k, 2, 2] += 2 * c
+        q[:, k, 2] += 2 * r0
+        if W.get("obstacles"):
+            p_o, q_o = OB.ey_model(xbar[:, k, Q.IS], ey, W["w_obs"] * ds[:, k], W["obstacles"],
+                                   W.get("obs_margin_min", OB.MARGIN_MIN))
+            Qm[:, k, 2, 2] += q_o
+            q[:, k, 2] += p_o
+    for k in range(N):
+        Qm[:, k, 6, 6] += 2 * W["w_w"] + 2 * W["prox"]
+        q[:, k, 6] += 2 * W["w_w"] * ubar[:, k, 1]
+        Qm[:, k, 5, 5] += 2 * W["prox"]
+        if k >= 1:  # w_a (abar_k + da_k - abar_{k-1} - p_k)^2
+            r0 = ubar[:, k, 0] - ubar[:, k - 1, 0]
+            Qm[:, k, 4, 4] += 2 * W["w_a"]
+            Qm[:, k, 5, 5] += 2 * W["w_a"]
+            Qm[:, k, 4, 5] -= 2 * W["w_a"]
+            Qm[:, k, 5, 4] -= 2 * W["w_a"]
+            q[:, k, 4] -= 2 * W["w_a"] * r0
+            q[:, k, 5] += 2 * W["w_a"] * r0
+        q[:, k, :4] += W["w_time"] * trow[:, k]
+    vN = xbar[:, N, Q.IV]
+    cv = np.where(vN >= W["v_max"], W["w_v"], 0.0)
+    Qm[:, N, 0, 0] += 2 * cv
+    q[:, N, 0] += 2 * cv * (vN - W["v_max"])
+    Qm[:, N, 2, 2] += 2 * W["w_ey"]
+    q[:, N, 2] += 2 * W["w_ey"] * xbar[:, N, Q.IEY]
+    Qm[:, N, 3, 3] += 2 * W["w_epsi"]
+    q[:, N, 3] += 2 * W["w_epsi"] * xbar[:, N, Q.IEP]
+    # rows C v <= d
+    d = np.ones((B, N + 1, 7))
+    m = np.zeros((B, N + 1, 7))
+    tr = (W.get("trust_a", 0.0), W.get("trust_w", 0.0))
+    for k in range(N):
+        for j, (lo, hi) in enumerate(((W["a_min"], W["a_max"]), (W["w_min"], W["w_max"]))):
+            up, dn = hi - ubar[:, k, j], ubar[:, k, j] - lo
+            if tr[j] > 0:
+                up, dn = np.minimum(up, tr[j]), np.minimum(dn, tr[j])
+            d[:, k, 2 * j], d[:, k, 2 * j + 1] = up, dn
+            m[:, k, 2 * j:2 * j + 2] = 1
+        if k >= 1:
+            d[:, k, 4] = xbar[:, k, Q.IV] - W["v_min"]
+            d[:, k, 5] = W["delta_max"] - xbar[:, k, Q.ID]
+            d[:, k, 6] = xbar[:, k, Q.ID] - W["delta_min"]
+            m[:, k, 4:] = 1
+    C = np.zeros((7, NV))
+    for r, (i, sg) in enumerate(ROWS):
+        C[r, i] = sg
+    return dict(xbar=xbar, F=F, trow=trow, Q=Qm, q=q, C=C, d=d, m=m)
+
+
+def riccati(Qt, F, h):
+    B, N1 = h.shape[:2]
+    N = N1 - 1
+    K = np.zeros((B, N, 2, NXT)); kk = np.zeros((B, N, 2))
+    P = Qt[:, N, :NXT, :NXT].copy()
+    pv = h[:, N, :NXT].copy()
+    for k in range(N - 1, -1, -1):
+        Fk = F[:, k]
+        Hm = Qt[:, k] + np.swapaxes(Fk, 1, 2) @ P @ Fk
+        g = h[:, k] + np.einsum("bji,bj->bi", Fk, pv)
+        Huu, Hux = Hm[:, 5:, 5:], Hm[:, 5:, :5]
+        Hi = np.linalg.inv(Huu)
+        K[:, k] = -Hi @ Hux
+        kk[:, k] = -np.einsum("bij,bj->bi", Hi, g[:, 5:])
+        P = Hm[:, :5, :5] + np.swapaxes(Hux, 1, 2) @ K[:, k]
+        P = 0.5 * (P + np.swapaxes(P, 1, 2))
+        pv = g[:, :5] + np.einsum("bji,bj->bi", K[:, k], g[:, 5:])
+    v = np.zeros((B, N + 1, NV))
+    xt = np.zeros((B, NXT))
+    for k in range(N):
+        u = np.einsum("bij,bj->bi", K[:, k], xt) + kk[:, k]
+        v[:, k, :5], v[:, k, 5:] = xt, u
+        xt = np.einsum("bij,bj->bi", F[:, k], v[:, k])
+    v[:, N, :5] = xt
+    return v
+
+
+def rollout(F, u):
+    B, N = u.shape[:2]
+    v = np.zeros((B, N + 1, NV))
+    xt = np.zeros((B, NXT))
+    for k in range(N):
+        v[:, k, :5], v[:, k, 5:] = xt, u[:, k]
+        xt = np.einsum("bij,bj->bi", F[:, k], v[:, k])
+    v[:, N, :5] = xt
+    return v
+
+
+def adjoint_u(F, gr):
+    B, N1 = gr.shape[:2]
+    N = N1 - 1
+    out = np.zeros((B, N, 2))
+    rho = gr[:, N, :5].copy()
+    for k in range(N - 1, -1, -1):
+        g = gr[:, k] + np.einsum("bji,bj->bi", F[:, k], rho)
+        out[:, k] = g[:, 5:]
+        rho = g[:, :5]
+    return out
+
+
+def ipm(sq_, tol=1e-10, max_iter=60):
+    F, Qm, q, C, d, m = (sq_[k] for k in ("F", "Q", "q", "C", "d", "m"))
+    B, N1 = q.shape[:2]
+    N = N1 - 1
+    u = np.zeros((B, N, 2))
+    s = np.where(m > 0, np.maximum(d, 1.0), 1.0)
+    lam = m.copy()
+    mcount = m.sum(axis=(1, 2))
+    iters = np.full(B, max_iter)
+    done = np.zeros(B, bool)
+    rtol = tol * (1.0 + np.abs(q).max(axis=(1, 2)))   # residual floor grows with the data
+    for it in range(max_iter):
+        v = rollout(F, u)
+        Cv = np.einsum("ri,bki->bkr", C, v)
+        rp = m * (Cv + s - d)
+        grad = np.einsum("bkij,bkj->bki", Qm, v) + q + np.einsum("ri,bkr->bki", C, m * lam)
+        rd = adjoint_u(F, grad)
+        mu = (m * s * lam).sum(axis=(1, 2)) / mcount
+        res = np.maximum(np.abs(rd).max(axis=(1, 2)), np.abs(rp).max(axis=(1, 2)))
+        conv = (res <= rtol) & (mu <= 1e-3 * tol)
+        iters[conv & ~done] = it
+        done |= conv
+        if done.all():
+            break
+        w = m * lam / s
+        Qt = Qm + np.einsum("ri,bkr,rj->bkij", C, w, C)
+
+        def direction(rc):
+            h = grad + np.einsum("ri,bkr->bki", C, m * (w * rp - rc / s))
+            dv = riccati(Qt, F, h)
+            Cdv = np.einsum("ri,bki->bkr", C, dv)
+            return dv, m * (-rp - Cdv), m * (w * (Cdv + rp) - rc / s)
+
+        def step(x, dx):
+            with np.errstate(divide="ignore", invalid="ignore"):
+                r = np.where((m > 0) & (dx < 0), -x / dx, np.inf)
+            return np.minimum(1.0, r.min(axis=(1, 2)))
+
+        dv, dsa, dla = direction(m * s * lam)
+        aa = np.minimum(step(s, dsa), step(lam, dla))
+        mu_a = (m * (s + aa[:, None, None] * dsa) * (lam + aa[:, None, None] * dla)).sum(axis=(1, 2)) / mcount
+        sig = np.minimum(1.0, mu_a / np.maximum(mu, 1e-300)) ** 3
+        rc = m * (s * lam + dsa * dla - (sig * mu)[:, None, None])
+        dv, dsl, dla2 = direction(rc)
+        al = np.minimum(0.99 * np.minimum(step(s, dsl), step(lam, dla2)), 1.0)
+        al = np.where(done, 0.0, al)
+        u = u + al[:, None, None] * dv[:, :N, 5:]
+        s = np.where(m > 0, np.maximum(s + al[:, None, None] * dsl, 1e-300), 1.0)
+        lam = np.where(m > 0, np.maximum(lam + al[:, None, None] * dla2, 1e-300), 0.0)
+    return u, iters, done
+
+
+def main():
+    from vcmpc.config import load_config
+    W = Q.kin_weights(load_config("kinematic_mpc"))
+    g = {k: v for k, v in np.load(os.path.join(ROOT, "tests", "golden", "kin_ltv_golden.npz")).items()}
+    sq_ = stage_qp(g["x0"], g["ubar"], g["kappa"], g["ds"], 2.5, W)
+    du, it, ok = ipm(sq_)
+    us = g["ubar"] + du
+    print(f"N=20 golden: max |u* - u*_oracle| = {np.abs(us - g['u_star']).max():.3e}, "
+          f"iterations {it.min()}..{it.max()} mean {it.mean():.1f}, all conv {ok.all()}")
+    from vcmpc.workload import kinematic_batch
+    for N in (20, 50):
+        d = kinematic_batch(32, N=N, seed=5 + N)
+        ref = Q.kin_ltv_solve(d["x0"], d["ubar"], d["kappa"], d["ds"], 2.5, W)
+        sq_ = stage_qp(d["x0"], d["ubar"], d["kappa"], d["ds"], 2.5, W)
+        du, it, ok = ipm(sq_)
+        # x* = xbar + dx (t from the t-rows)
+        v = rollout(sq_["F"], du)
+        err = np.abs(d["ubar"] + du - ref["u_star"]).max()
+        dx = np.zeros_like(ref["x_star"])
+        dx[:, :, Y] = v[:, :, :4]
+        dx[:, 1:, 5] = np.cumsum(np.einsum("bki,bki->bk", sq_["trow"], v[:, :N, :4]), axis=1)
+        xerr = np.abs(sq_["xbar"] + dx - ref["x_star"]).max()
+        print(f"N={N}: max |u* - u*_oracle| = {err:.3e}, |x* - x*_oracle| = {xerr:.3e}, "
+              f"iterations {it.min()}..{it.max()} mean {it.mean():.1f}, all conv {ok.all()}")
+
+
+if __name__ == "__main__":
+    main()

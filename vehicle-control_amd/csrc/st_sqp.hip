@@ -810,9 +810,11 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     any_fail = any_fail || fail;
 
     // ---------------- SQP update: ubar += dz ----------------
+    // w is projected onto its box: exact at a converged QP (|violation| <= tol_r), and it
+    // keeps a non-converged iterate (infeasible-start interior point) from leaving it
     if (stl) {
       s.ub[k][0] += s.u.q.v[k][7] * S;
-      s.ub[k][1] += s.u.q.v[k][8];
+      s.ub[k][1] = fmin(fmax(s.ub[k][1] + s.u.q.v[k][8], W.w_min), W.w_max);
     }
     WSYNC();
   }

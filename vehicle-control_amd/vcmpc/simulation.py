@@ -24,6 +24,7 @@ from .solver import Context
 
 IV_KIN, IS_KIN = 0, 2
 IUX, IS_DYN = 0, 4
+ST_SQP_HORIZONS = (20, 30, 40, 50, 60)   # fp64 single-track kernel instances (csrc/st_sqp.hip)
 
 
 def _is_dynamic(car) -> bool:
@@ -35,12 +36,13 @@ class BatchedRacingSimulator:
 
     ``car`` is a ``KinematicCar`` or ``DynamicCar`` (its config and tyre are used),
     ``controller_config`` the matching controller yaml (``kinematic_mpc`` /
-    ``dynamic_mpc``), ``track`` a ``vcmpc.environment.Track``.  Buffers live on
+    ``dynamic_mpc``), ``track`` a ``vcmpc.environment.Track``.  ``dtype`` picks the
+    dynamic solve precision (default fp64 where the fp64 kernel is built for N).  Buffers live on
     ``cuda:<device>`` as torch tensors when torch is importable (the fast path),
     else in host numpy arrays staged by every call."""
 
     def __init__(self, car, controller_config, track, batch: int, device: int = 0, seed: int | None = 31,
-                 use_torch: bool = True):
+                 use_torch: bool = True, dtype: int | None = None):
         cfg = controller_config
         if int(cfg.get("horizon_pm", 0)) > 0:
             raise NotImplementedError("the cascaded point-mass tail (cascaded_mpc.py:181-277) is SURVEY 8(f) row 3")
@@ -52,7 +54,11 @@ class BatchedRacingSimulator:
         if self.dynamic:
             params = make_params(dyn_car=car.config, dyn_mpc=cfg, tyre=getattr(car, "tyre", "fiala"),
                                  obstacles=obstacle_list(track, cfg))
-            model, dtype = _abi.VC_MODEL_DYNAMIC, _abi.VC_F32
+            # fp64 (csrc/st_sqp.hip, the reference's own precision) where it is built, else
+            # the fp32 condensed kernel (csrc/dyn_sqp.hip, N = 40)
+            model = _abi.VC_MODEL_DYNAMIC
+            if dtype is None:
+                dtype = _abi.VC_F64 if self.N in ST_SQP_HORIZONS else _abi.VC_F32
         else:
             # the kinematic controller's real-time-iteration trust region (controllers/
             # kinematic_mpc.py RTI_TRUST) unless the config's qp block sets its own
