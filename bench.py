@@ -130,6 +130,8 @@ def parse():
     ap.add_argument("--c4-total", type=int, default=C4_TOTAL,
                     help="C4 problems in total, split into contiguous shards over the ranks (config 4: 65536)")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 sharded measurement")
+    ap.add_argument("--no-kin-legs", action="store_true",
+                    help="skip the stagewise kinematic legs (N = 20 Riccati, N = 50 = kinematic.yaml)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU work: each rank only takes its C2/C4/C5 shards and runs the counter "
                          "collective over gloo (tests the launcher and the rank logic on a CPU host)")
@@ -466,6 +468,62 @@ def run_c4(args, dev, stream, rank, world, dist, steps):
                        "iters_max_rank0": int(it.max())}}
 
 
+def run_kin_leg(args, dev, stream, rank, dist, steps, N, solver, B):
+    """A kinematic LTV-MPC leg beside C2: the stagewise-Riccati kernel (csrc/kin_ric.hip) at
+    BASELINE's N = 20 (solver = 1, vs the condensed kin_ltv.hip of `value`) and at the
+    reference's own horizon N = 50 (config/controllers/kinematic.yaml:2)."""
+    import numpy as np
+    import torch
+
+    from vcmpc import Context, _abi
+    from vcmpc.config import load_config, make_params
+    from vcmpc.workload import kinematic_batch
+    data = kinematic_batch(B, N=N, seed=args.seed + 7919 * rank + N)
+    t = {k: torch.from_numpy(v).to(dev) for k, v in data.items()}
+    ubar0 = t["ubar"].clone()
+    cfg = load_config("kinematic_mpc")
+    cfg["qp"] = dict(cfg.get("qp") or {}, solver=solver)
+    params = make_params(kin_car=load_config("kinematic_car"), kin_mpc=cfg)
+    ctx = Context(model=_abi.VC_MODEL_KINEMATIC, N=N, max_batch=B, device=dev.index, params=params)
+    ctx.set_stream(stream.cuda_stream)
+    xbar = torch.empty((B, N + 1, NX), dtype=torch.float64, device=dev)
+    u0 = torch.empty((B, NU), dtype=torch.float64, device=dev)
+    status = torch.empty((B,), dtype=torch.int32, device=dev)
+    iters = torch.empty((B,), dtype=torch.int32, device=dev)
+
+    def step(ev=None):
+        t["ubar"].copy_(ubar0)
+        if ev is not None:
+            ev[0].record(stream)
+        ctx.solve(t["x0"], t["kappa"], t["ds"], t["ubar"], xbar, u0, status, iters)
+        if ev is not None:
+            ev[1].record(stream)
+
+    step()
+    torch.cuda.synchronize(dev)
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(events[i])
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    st, it = status.cpu().numpy(), iters.cpu().numpy()
+    solves, elapsed_max, _ = dist.aggregate(float(B * steps), elapsed, kern_ms, dev)
+    ctx.close()
+    kern = "kin_ric_kernel" if (solver == 1 or N != N_HORIZON) else "kin_ltv_kernel"
+    return {"metric": f"MPC solves/sec (batched, N={N})", "value": solves / elapsed_max, "unit": "solves/s",
+            "steps": steps, "ms_per_step": elapsed_max / steps * 1e3, "kernel": f"{kern}<{N}>", "kernel_ms": kern_ms,
+            "dtype": "f64",
+            "config": {"workload": f"kinematic-bicycle LTV-MPC, B={B} per GPU, N={N}, fp64, stagewise Riccati "
+                                   f"interior point + active-set polish", "batch_per_gpu": B, "horizon": N},
+            "solver": {"solved_frac": float((st == 0).mean()), "iters_mean": float(it.mean()),
+                       "iters_max": int(it.max())}}
+
+
 def dry_run(args):
     """--dry-run: the multi-rank control flow without a GPU -- gloo process group from the
     launcher's environment, every rank's C2 batch / C4 and C5 shards, the counter
@@ -661,6 +719,13 @@ def main():
             c4 = run_c4(args, dev, stream, rank, world, dist, max(3, args.steps // 4))
         except Exception as e:  # the headline line must still print
             c4 = {"error": f"{type(e).__name__}: {e}"}
+    kin_legs = {}
+    if not args.no_kin_legs:
+        for name, N, solver in (("c2_riccati", N_HORIZON, 1), ("kinematic_n50", 50, 1)):
+            try:
+                kin_legs[name] = run_kin_leg(args, dev, stream, rank, dist, max(3, args.steps // 4), N, solver, B)
+            except Exception as e:
+                kin_legs[name] = {"error": f"{type(e).__name__}: {e}"}
     c3 = c3_data = c3f = st60 = None
     if not args.no_c3:
         try:
@@ -739,6 +804,7 @@ def main():
                 from oracle.track import load_track
                 otrack = load_track(os.path.join(ROOT, "vehicle-control_amd", "config", "tracks", "ippodromo.yaml"))
                 c5["cpu_baseline"] = cpu_baseline_c5(c5_aux[0], otrack)
+        out.update(kin_legs)
         if c4 is not None:
             out["c4"] = c4
         if c3 is not None:

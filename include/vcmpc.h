@@ -58,7 +58,7 @@
 extern "C" {
 #endif
 
-#define VCMPC_ABI_VERSION 4
+#define VCMPC_ABI_VERSION 5
 #define VC_MAX_OBSTACLES 16
 
 typedef struct vc_ctx vc_ctx;
@@ -119,6 +119,9 @@ typedef struct vc_qp {
   double trust_w;   /* trust region |u_w - ubar_w| <= trust_w (0 = off) */
   int32_t max_iter; /* interior-point iteration cap */
   int32_t polish;   /* active-set polish rounds after the interior point (0 = off) */
+  int32_t solver;   /* kinematic solve kernel: 0 = condensed (kin_ltv.hip) where built (N = 20),
+                       else stagewise Riccati (kin_ric.hip); 1 = stagewise Riccati always */
+  int32_t pad_;
 } vc_qp;
 
 /* Cascaded controller: single-track stages followed by a point-mass tail
@@ -275,10 +278,10 @@ int vc_drive(vc_ctx* ctx, int B, double* x64, const void* u0, double dt, void* x
 /* `steps` closed-loop steps for B vehicles, all on the device (one HIP stream):
  *   vc_horizon(x, xbar) -> vc_solve(x, kappa, ds, xbar, ubar) -> vc_drive(x, u0)
  * x64[B][nx] fp64 in/out (plant state), xbar/ubar the warm starts in/out (context
- * dtype, shapes of vc_solve).  A problem whose status is not VC_SOLVED still applies
- * its u0 (zero if non-finite), increments nfail[b] (int32, may be NULL; not cleared),
- * and restarts from the neutral warm start (ubar = 0, xbar = the new state) -- the
- * reference's simulator swallows the solver exception instead (racing.py:416-423).
+ * dtype, shapes of vc_solve).  A problem whose status is not VC_SOLVED applies the
+ * neutral input u = 0, increments nfail[b] (int32, may be NULL; not cleared), and restarts
+ * from the neutral warm start (ubar = 0, xbar = the new state) -- in the reference a
+ * failed IPOPT solve raises and the simulator's catch-all drops the step (racing.py:416-423).
  * Optional logs (may be NULL): log_x[steps+1][B][nx] fp64 (the state before each step
  * and after the last), log_u[steps][B][nu] context dtype (the applied u0).
  * Requires vc_track_set and a built vc_solve combination. */

@@ -147,7 +147,41 @@ def adjoint_u(F, gr):
     return out
 
 
-def ipm(sq_, tol=1e-10, max_iter=60):
+def polish(sq_, u, s, lam, rho=1e6, passes=8, rounds=3, tol=1e-9):
+    """Active-set polish (the crossover of kin_ltv.hip, restated stagewise): rows with
+    lam > s at the interior-point iterate are imposed by an augmented Lagrangian
+    (Q + rho C_A'C_A, one Riccati factorisation, `passes` multiplier updates); accepted when
+    the inactive rows are feasible and the multipliers non-negative (tol), otherwise the
+    violated rows join / the negative ones leave and the polish repeats (`rounds`)."""
+    F, Qm, q, C, d, m = (sq_[k] for k in ("F", "Q", "q", "C", "d", "m"))
+    B, N1 = q.shape[:2]
+    N = N1 - 1
+    act = (m > 0) & (lam > s)
+    ok = np.zeros(B, bool)
+    u_out = u.copy()
+    for r in range(rounds):
+        w = np.where(act, rho, 0.0)
+        Qt = Qm + np.einsum("ri,bkr,rj->bkij", C, w, C)
+        la = np.where(act, lam, 0.0)
+        for p_ in range(passes):
+            # min 1/2 v'Qv + q'v + la'(C_A v - d_A) + rho/2 |C_A v - d_A|^2
+            h = q + np.einsum("ri,bkr->bki", C, np.where(act, la - rho * d, 0.0))
+            v = riccati(Qt, F, h)
+            Cv = np.einsum("ri,bki->bkr", C, v)
+            la = np.where(act, la + rho * (Cv - d), 0.0)
+        viol = (m > 0) & ~act & (Cv - d > tol)
+        neg = act & (la < -tol)
+        good = ~(viol.any(axis=(1, 2)) | neg.any(axis=(1, 2)))
+        newly = good & ~ok
+        u_out[newly] = v[newly, :N, 5:]
+        ok |= good
+        if ok.all():
+            break
+        act = (act | viol) & ~neg
+    return u_out, ok
+
+
+def ipm(sq_, tol=1e-10, max_iter=60, mu_polish=None):
     F, Qm, q, C, d, m = (sq_[k] for k in ("F", "Q", "q", "C", "d", "m"))
     B, N1 = q.shape[:2]
     N = N1 - 1
@@ -166,7 +200,7 @@ def ipm(sq_, tol=1e-10, max_iter=60):
         rd = adjoint_u(F, grad)
         mu = (m * s * lam).sum(axis=(1, 2)) / mcount
         res = np.maximum(np.abs(rd).max(axis=(1, 2)), np.abs(rp).max(axis=(1, 2)))
-        conv = (res <= rtol) & (mu <= 1e-3 * tol)
+        conv = (res <= rtol) & (mu <= 1e-3 * tol) if mu_polish is None else (mu <= mu_polish)
         iters[conv & ~done] = it
         done |= conv
         if done.all():
@@ -196,6 +230,8 @@ def ipm(sq_, tol=1e-10, max_iter=60):
         u = u + al[:, None, None] * dv[:, :N, 5:]
         s = np.where(m > 0, np.maximum(s + al[:, None, None] * dsl, 1e-300), 1.0)
         lam = np.where(m > 0, np.maximum(lam + al[:, None, None] * dla2, 1e-300), 0.0)
+    if mu_polish is not None:
+        u, done = polish(sq_, u, s, lam)
     return u, iters, done
 
 

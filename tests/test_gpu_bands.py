@@ -14,7 +14,8 @@ reproducible to 1e-5 across solvers):
   * lap length within 3 % of the recorded lap of the same config (measured: 442 vs 442,
     455 vs 448, 434 vs 433, 429 vs 428 steps);
   * median Ux within 0.3 m/s; Fx inside the recorded envelope [-7876, 6055] N widened by
-    5 %; |w| <= 0.4; |ey| inside the 9 m track (recorded max 5.06 m);
+    5 %; |w| <= 0.4; |ey| inside the 9 m track or within 10 % of the recorded lap's max
+    (the recorded N = 50 / max_speed 20 lap itself reaches 5.06 m);
   * at most one non-solved step (the first step, from the reference's random first guess
     1 + U[0, 1) of cascaded_mpc.py:72-76).
 """
@@ -74,5 +75,6 @@ def test_singletrack_lap_within_recorded_bands(N, vmax):
     assert abs(stats["Ux_median"] - rec["Ux_median"]) <= UX_MED_ABS
     assert -7876 * 1.05 <= stats["Fx_min"] and stats["Fx_max"] <= 6055 * 1.05
     assert np.abs(Ul[:, 1]).max() <= 0.4 + 1e-9
-    assert stats["ey_absmax"] < track.width / 2
+    # on the track, or no further off it than the recorded lap (N = 50 / max_speed 20: 5.06 m)
+    assert stats["ey_absmax"] < max(track.width / 2, 1.1 * rec["ey_absmax"])
     assert stats["nfail"] <= 1

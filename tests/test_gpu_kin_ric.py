@@ -1,0 +1,153 @@
+"""GPU parity of the stagewise-Riccati kinematic kernel (csrc/kin_ric.hip) through the C ABI,
+against the fp64 oracle of the LTV-QP contract (oracle/ltv_qp.py, exact dense QP + active-set
+polish) and its golden vectors -- at BASELINE's N = 20 (qp.solver = 1 forces this kernel
+where the condensed kin_ltv.hip is built) and at the reference's own kinematic horizon
+N = 50 (config/controllers/kinematic.yaml:2), plus N = 10 .. 60.
+
+Tolerance: the north star's ||u* - u*_oracle||_inf < 1e-5 (a in m/s^2, w in rad/s); x* (the
+linearised prediction x* = xbar + G du*) to 1e-6.
+"""
+import numpy as np
+import pytest
+
+from oracle import ltv_qp as Q
+
+pytestmark = pytest.mark.gpu
+
+U_TOL = 1e-5
+X_TOL = 1e-6
+L = 2.5
+
+
+def _ctx(N, B=256, obstacles=None, solver=1, qp=None):
+    from vcmpc import Context, _abi
+    from vcmpc.config import load_config, make_params
+    cfg = load_config("kinematic_mpc")
+    cfg["qp"] = dict(cfg.get("qp") or {}, solver=solver, **(qp or {}))
+    p = make_params(kin_car=load_config("kinematic_car"), kin_mpc=cfg, obstacles=obstacles)
+    return Context(model=_abi.VC_MODEL_KINEMATIC, N=N, max_batch=B, dtype=_abi.VC_F64, params=p)
+
+
+def test_kin_ric_vs_golden_n20(kin_golden):
+    g = kin_golden
+    with _ctx(20) as c:
+        u0, xs, us, st, it, dg = c.solve(g["x0"], g["kappa"], g["ds"], g["ubar"].copy(), diag=True)
+    err = np.abs(us - g["u_star"]).max()
+    print(f"N=20 golden: |u* - u*_oracle| = {err:.3e}, IPM iterations {it.min()}..{it.max()}, "
+          f"polished {(dg[:, 2].astype(int) & 4 > 0).mean():.3f}")
+    assert (st == 0).all(), (st, dg)
+    assert err < U_TOL
+    np.testing.assert_array_equal(u0, us[:, 0])
+    assert np.abs(xs - g["x_star"]).max() < X_TOL
+
+
+@pytest.mark.parametrize("N", [10, 30, 40, 50, 60])
+def test_kin_ric_horizons_vs_oracle(N, kin_W):
+    """Fresh C2-sampler problems at each built horizon; N = 50 is kinematic.yaml's."""
+    from vcmpc.workload import kinematic_batch
+    d = kinematic_batch(24, N=N, seed=300 + N)
+    ref = Q.kin_ltv_solve(d["x0"], d["ubar"], d["kappa"], d["ds"], L, kin_W)
+    with _ctx(N) as c:
+        u0, xs, us, st, it = c.solve(d["x0"], d["kappa"], d["ds"], d["ubar"].copy())
+    err = np.abs(us - ref["u_star"]).max()
+    xerr = np.abs(xs - ref["x_star"]).max()
+    print(f"N={N}: |u* - u*_oracle| = {err:.3e}, |x* - x*_oracle| = {xerr:.3e}, iterations {it.min()}..{it.max()}")
+    assert (st == 0).all(), st
+    assert err < U_TOL
+    assert xerr < X_TOL
+
+
+def test_kin_ric_matches_condensed_kernel():
+    """N = 20: the stagewise and the condensed kernel (kin_ltv.hip) solve the same QP."""
+    from vcmpc.workload import kinematic_batch
+    d = kinematic_batch(1024, N=20, seed=41)
+    with _ctx(20, B=1024, solver=1) as c:
+        r1 = c.solve(d["x0"], d["kappa"], d["ds"], d["ubar"].copy())
+    with _ctx(20, B=1024, solver=0) as c:
+        r0 = c.solve(d["x0"], d["kappa"], d["ds"], d["ubar"].copy())
+    assert (r1[3] == 0).all() and (r0[3] == 0).all()
+    err = np.abs(r1[2] - r0[2]).max()
+    print(f"N=20, 1024 problems: |u*_riccati - u*_condensed| = {err:.3e}")
+    assert err < U_TOL
+
+
+def test_kin_ric_obstacles_vs_golden():
+    import os
+    from conftest import GOLDEN
+    g = np.load(os.path.join(GOLDEN, "obs_golden.npz"))
+    obs = [tuple(float(v) for v in o) for o in g["obstacles"]]
+    with _ctx(20, obstacles=obs) as c:
+        u0, xs, us, st, it = c.solve(g["kin_x0"], g["kin_kappa"], g["kin_ds"], g["kin_ubar"].copy())
+    err = np.abs(us - g["kin_u_star"]).max()
+    print(f"obstacles: |u* - u*_oracle| = {err:.3e}, status {np.bincount(st)}")
+    assert (st == 0).all()
+    assert err < U_TOL
+
+
+def test_kin_ric_trust_region_vs_oracle(kin_W):
+    """The closed-loop controller's real-time-iteration trust region (qp.trust_a/trust_w)."""
+    from vcmpc.workload import kinematic_batch
+    d = kinematic_batch(16, N=50, seed=9)
+    W = dict(kin_W, trust_a=1.0, trust_w=0.1)
+    ref = Q.kin_ltv_solve(d["x0"], d["ubar"], d["kappa"], d["ds"], L, W)
+    with _ctx(50, qp={"trust_a": 1.0, "trust_w": 0.1}) as c:
+        u0, xs, us, st, it = c.solve(d["x0"], d["kappa"], d["ds"], d["ubar"].copy())
+    assert (st == 0).all()
+    assert np.abs(us - ref["u_star"]).max() < U_TOL
+    assert np.abs(us - d["ubar"])[..., 0].max() <= 1.0 + 1e-9
+
+
+def test_kin_ric_batch_properties_n50(kin_W):
+    """kinematic.yaml's horizon at a C4-shard-sized batch: all solved, inputs inside their
+    boxes, bit-identical reruns, host = device pointers, sampled oracle checks."""
+    import torch
+    from vcmpc.workload import kinematic_batch
+    B = 8192
+    d = kinematic_batch(B, N=50, seed=77)
+    with _ctx(50, B=B) as c:
+        u0, xs, us, st, it, dg = c.solve(d["x0"], d["kappa"], d["ds"], d["ubar"].copy(), diag=True)
+        t = {k: torch.from_numpy(v).cuda() for k, v in d.items()}
+        r = c.solve(t["x0"], t["kappa"], t["ds"], t["ubar"])
+        torch.cuda.synchronize()
+        us2 = r[2].cpu().numpy()
+    print(f"N=50 B={B}: solved {(st == 0).mean():.5f}, iterations mean {it.mean():.1f} max {it.max()}")
+    bad = np.nonzero(st != 0)[0]
+    assert len(bad) == 0, [(int(b), dg[b].tolist()) for b in bad[:4]]
+    np.testing.assert_array_equal(us, us2)
+    assert us[..., 0].max() <= 3 + 1e-9 and us[..., 0].min() >= -3 - 1e-9
+    assert np.abs(us[..., 1]).max() <= 0.4 + 1e-9
+    assert xs[:, 1:-1, 1].max() <= 0.3 + 1e-8 and xs[:, 1:-1, 1].min() >= -0.3 - 1e-8
+    idx = np.arange(0, B, B // 8)
+    ref = Q.kin_ltv_solve(d["x0"][idx], d["ubar"][idx], d["kappa"][idx], d["ds"][idx], L, kin_W)
+    assert np.abs(us[idx] - ref["u_star"]).max() < U_TOL
+
+
+def test_kin_ric_closed_loop_n20():
+    """The batched simulator with the stagewise kernel forced at N = 20 (qp.solver = 1): 64
+    vehicles x 200 steps on ippodromo, like the condensed kernel (test_gpu_closed_loop)."""
+    from vcmpc.config import load_config
+    from vcmpc.environment import Track
+    from vcmpc.models import KinematicCar
+    from vcmpc.simulation import BatchedRacingSimulator
+    track = Track.load("ippodromo")
+    car = KinematicCar(load_config("kinematic_car"), track)
+    B, K = 64, 200
+    rng = np.random.default_rng(3)
+    x0 = np.zeros((B, 6))
+    x0[:, 0] = rng.uniform(4, 9, B)
+    x0[:, 2] = rng.uniform(0, track.length, B)
+    x0[:, 3] = rng.uniform(-1.5, 1.5, B)
+    res = {}
+    for solver in (0, 1):
+        cfg = load_config("kinematic_mpc")
+        cfg["qp"] = dict(cfg.get("qp") or {}, solver=solver)
+        sim = BatchedRacingSimulator(car, cfg, track, batch=B)
+        out = sim.reset(x0).run(K)
+        X = out["state_traj"]
+        res[solver] = (np.abs(X[:, :, 3]).max(), int(out["nfail"].sum()), np.median(X[-1, :, 2] - X[0, :, 2]))
+        print(f"solver={solver}: max |ey| {res[solver][0]:.2f}, non-solved steps {res[solver][1]}, "
+              f"median progress {res[solver][2]:.1f} m")
+        assert np.isfinite(X).all()
+        assert res[solver][1] <= 0.01 * B * K
+        assert res[solver][0] < track.width / 2
+    assert abs(res[1][2] - res[0][2]) < 1.0

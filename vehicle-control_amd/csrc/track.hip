@@ -100,8 +100,11 @@ __global__ void drive_kernel(ModelArgs m, TrackTable tt, double* x64, const T* u
   for (int i = 0; i < NX; ++i) x[i] = x64[(size_t)b * NX + i];
   u[0] = double(u0[(size_t)b * 2]);
   u[1] = double(u0[(size_t)b * 2 + 1]);
+  // a non-solved step applies the neutral plan's input (zero: the restart below re-plans
+  // from ubar = 0), not the unconverged iterate -- the failures are almost all infeasible
+  // linearised QPs (scripts/kin_fail_modes.py), whose iterates diverge
   const bool failed = status && status[b] != VC_SOLVED;
-  if (failed && !(isfinite(u[0]) && isfinite(u[1]))) u[0] = u[1] = 0.0;
+  if (failed) u[0] = u[1] = 0.0;
   const double kap = track_k(tt, x[IS]);
   if (MODEL == VC_MODEL_KINEMATIC) {
     double f[KIN_NX];

@@ -42,7 +42,7 @@ __device__ __forceinline__ void obstacle_ey_model(const vc_obstacles& o, T s, T 
   q = qs > T(0) ? qs : T(0);
 }
 
-// Fused kinematic LTV-MPC step (kin_ltv.hip).
+// Fused kinematic LTV-MPC step (kin_ltv.hip, condensed, N = 20; kin_ric.hip, stagewise).
 struct KinLtvArgs {
   const double* x0;     // [B][6]
   const double* kappa;  // [B][N]
@@ -156,6 +156,10 @@ hipError_t launch_drive(const ModelArgs& m, int dtype, const TrackTable& tt, dou
                         void* x_ctx, const int32_t* status, void* xbar, void* ubar, int32_t* nfail, double* log_x,
                         void* log_u, hipStream_t st);
 hipError_t launch_kin_ltv(const KinLtvArgs& a, int N, hipStream_t stream);
+// Stagewise-Riccati kinematic LTV-MPC step (kin_ric.hip): the same contract, any built N
+// (KinLtvArgs.mode / H_out / g_out are not read).
+hipError_t launch_kin_ric(const KinLtvArgs& a, int N, hipStream_t stream);
+bool kin_ric_built(int N);
 hipError_t launch_dyn_sqp(const DynSqpArgs& a, int N, hipStream_t stream);
 hipError_t launch_casc_sqp(const CascSqpArgs& a, int N, int M, hipStream_t stream);
 hipError_t launch_st_sqp(const StSqpArgs& a, int N, hipStream_t stream);

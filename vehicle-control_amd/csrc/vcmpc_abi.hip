@@ -131,8 +131,11 @@ vc::TrackTable track_table(const vc_ctx* c) {
   return vc::TrackTable{static_cast<const double*>(c->track), c->track_n, c->track_h, c->track_len};
 }
 
+// The condensed kernel (kin_ltv.hip) where it is built (N = 20, the bench's C2/C4 shape),
+// the stagewise Riccati kernel (kin_ric.hip) for the other horizons (kinematic.yaml: 50).
+bool kin_condensed(const vc_ctx* c) { return vc::kin_ltv_smem_bytes(c->N) > 0 && c->p.qp.solver == 0; }
 bool kin_solve_built(const vc_ctx* c) {
-  return c->model == VC_MODEL_KINEMATIC && c->dtype == VC_F64 && vc::kin_ltv_smem_bytes(c->N) > 0;
+  return c->model == VC_MODEL_KINEMATIC && c->dtype == VC_F64 && (kin_condensed(c) || vc::kin_ric_built(c->N));
 }
 bool dyn_solve_built(const vc_ctx* c) {
   if (c->model != VC_MODEL_DYNAMIC) return false;
@@ -445,8 +448,8 @@ int vc_solve_diag(vc_ctx* c, int B, const void* x0, const void* kappa, const voi
   if (int r = check_common(c, B, flags)) return r;
   if (!kin_solve_built(c) && !dyn_solve_built(c) && !casc_solve_built(c))
     return fail(c, VC_E_UNSUPPORTED,
-                "vc_solve: model=%d dtype=%d N=%d not built (kinematic fp64 N=20, dynamic fp32 N=40 and "
-                "cascaded fp64 N=20 + 40 are)", c->model, c->dtype, c->N);
+                "vc_solve: model=%d dtype=%d N=%d not built (kinematic fp64 N=10..60 step 10, dynamic fp64 "
+                "N=20..60 step 10, dynamic fp32 N=40, cascaded fp64 N=20 + 40 are)", c->model, c->dtype, c->N);
   if (!x0 || !kappa || !ds || !xbar || !ubar || !u0 || !status || !iters) return fail(c, VC_E_ARG, "null pointer");
   if (B == 0) return 0;
   if (c->model == VC_MODEL_DYNAMIC) return dyn_solve(c, B, x0, kappa, ds, xbar, ubar, u0, status, iters, diag, flags);
@@ -493,7 +496,8 @@ int vc_solve_diag(vc_ctx* c, int B, const void* x0, const void* kappa, const voi
     a.iters = iters;
     a.diag = (double*)diag;
   }
-  VC_HIP(c, vc::launch_kin_ltv(a, N, c->stream));
+  if (kin_condensed(c)) VC_HIP(c, vc::launch_kin_ltv(a, N, c->stream));
+  else VC_HIP(c, vc::launch_kin_ric(a, N, c->stream));
   if (flags == VC_HOST_PTRS) return unstage(c, slots);
   return 0;
 }
@@ -513,7 +517,7 @@ int vc_debug_stride(void) { return vc::dyn_sqp_debug_stride(); }
 int vc_condense(vc_ctx* c, int B, const void* x0, const void* ubar, const void* kappa, const void* ds, void* H,
                 void* g, int flags) {
   if (int r = check_common(c, B, flags)) return r;
-  if (!kin_solve_built(c) && !casc_solve_built(c))
+  if (!(kin_solve_built(c) && kin_condensed(c)) && !casc_solve_built(c))
     return fail(c, VC_E_UNSUPPORTED, "vc_condense: model=%d dtype=%d N=%d not built", c->model, c->dtype, c->N);
   if (!x0 || !kappa || !ds || !ubar || !H || !g) return fail(c, VC_E_ARG, "null pointer");
   if (B == 0) return 0;

@@ -9,9 +9,11 @@ unshifted warm start and the curvature table, the fused MPC solve, the fp64
 plant step -- no host round trip between steps.
 
 Per-vehicle failure handling (the reference prints and drops the step,
-racing.py:417-422): a solve whose status is not VC_SOLVED still applies its u0
-(zero if non-finite), is counted in ``nfail``, and the next step starts from the
-neutral warm start.  The single-vehicle controllers instead re-solve at once from
+racing.py:417-422): a solve whose status is not VC_SOLVED applies the neutral
+input u = 0, is counted in ``nfail``, and the next step starts from the neutral
+warm start (ubar = 0).  Almost every such step is the first one, whose linearised QP
+around the reference's random first guess 1 + U[0, 1) is infeasible under the
+real-time-iteration trust region (scripts/kin_fail_modes.py: 67 of 69).  The single-vehicle controllers instead re-solve at once from
 the neutral warm start (controllers/*.py); both are documented deviations.
 """
 from __future__ import annotations
