@@ -15,7 +15,7 @@ Monte-Carlo, 8192 vehicles x 500 steps on ippodromo (horizon -> NMPC solve -> fp
 plant, all on the device, vc_simulate), vehicles sharded over the ranks.  Under
 "cascaded": the reference's cascaded NMPC (20 single-track + 40 point-mass stages,
 config/controllers/cascaded.yaml), B = 4096 per GPU, fp64
-(csrc/casc_sqp.hip).
+(csrc/casc_ric.hip, stagewise Riccati).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--c3-batch B3]
                     [--c5-vehicles V] [--c5-steps S] [--no-c3] [--no-c5] [--no-cpu-baseline]
@@ -354,13 +354,15 @@ def run_casc(args, dev, stream, rank, dist, steps):
     st, it = status.cpu().numpy(), iters.cpu().numpy()
     solves, elapsed_max, kern_ms_max = dist.aggregate(float(B * steps), elapsed, kern_ms, dev)
     ctx.close()
-    flops = 3 * CA_FLOP_SQP + float(it.mean()) * CA_FLOP_ITER
+    # stagewise Riccati kernel (csrc/casc_ric.hip): st_sqp's per-stage count over the H stages
+    # (the point-mass stages are cheaper: an upper estimate)
+    flops = st_flops(float(it.mean()), CA_H)
     out = {"metric": "MPC solves/sec (batched, N=20 single-track + 40 point-mass stages, 3 SQP iterations)",
            "value": solves / elapsed_max, "unit": "solves/s", "steps": steps,
            "ms_per_step": elapsed_max / steps * 1e3, "dtype": "f64",
            "config": {"workload": f"cascaded NMPC (config/controllers/cascaded.yaml), B={B} per GPU, "
                                   f"H={CA_N}+{CA_M}, fp64, Fiala tyre", "batch_per_gpu": B, "horizon": CA_H},
-           "roofline": {"bound": "fp64-valu", "kernel": "casc_sqp_kernel<20, 40, fiala>", "kernel_ms": kern_ms,
+           "roofline": {"bound": "fp64-valu", "kernel": "casc_ric_kernel<20, 40, fiala>", "kernel_ms": kern_ms,
                         "flops_per_solve": flops, "achieved": flops * B / (kern_ms / 1e3) / 1e12,
                         "peak": FP64_VALU_PEAK, "unit": "TFLOP/s",
                         "frac": flops * B / (kern_ms / 1e3) / 1e12 / FP64_VALU_PEAK,

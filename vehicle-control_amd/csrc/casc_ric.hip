@@ -1,27 +1,31 @@
-// st_sqp.hip -- fused single-track SQP step, fp64, one wavefront per problem, with a
-// stagewise Riccati interior point.
+// casc_ric.hip -- fused cascaded (single-track + point-mass) SQP step, fp64, one wavefront
+// per problem, with a stagewise Riccati interior point: any tail length M with
+// H = N + M <= 64 stages.
 //
-// Replaces the IPOPT solve of CascadedMPC in single-track mode (controllers/mpc/
-// cascaded_mpc.py:17-39,91-179,279-314, horizon_pm = 0) for the reference's own horizons
-// (config/controllers/singletrack.yaml N = 60; recorded runs N = 50 / 60) and BASELINE's
-// N = 40.  Contract: oracle/dyn_sqp.py (the same QP as the fp32 condensed kernel
-// dyn_sqp.hip, solved to fp64 accuracy).  Per SQP iteration:
-//   predict    lane 0: RK4 spatial rollout (vc_models.hpp dyn_spatial_ode_alg)
-//   linearize  one lane per (stage, seed pair): Dual<2> RK4 step -> two columns of
-//              [A B] and of the t-row; one lane per (stage, seed) for the stage terms
-//              (slip residuals, power and tyre-force rows) with Dual<1>
-//   QP         restated stage by stage (scripts/riccati_proto.py): QP state
-//              xt_k = (dUx, dUy, dr, ddelta, dey, depsi, p_k), p_k = dz_{k-1,Fx} (the Fx
-//              slew couples neighbouring stages), input u_k = dz_k = (dFx/S, dw); s is
-//              fixed (s' = 1) and t only enters w_time t_{N-1}, which becomes linear stage
-//              terms through each step's t-row.  Stage Hessians have 20 nonzeros; the 12
-//              one-sided rows of a stage touch (Ux, Uy, r, delta, dFx, dw) only.
-//              Mehrotra predictor-corrector; each Newton step is an LQ problem solved by
-//              a backward Riccati recursion (7 states + 2 inputs per stage: O(N) work per
-//              iteration, where the condensed form pays O(N^3)), then forward sweeps.
-//              Lane k owns stage k's rows, slacks and multipliers in registers; the
-//              recursions run on lanes 0..44 with the stage matrices in LDS.
-//   update     ubar += dz (Fx scaled back by fx_scale)
+// Replaces the IPOPT solve of CascadedMPC with horizon_pm > 0 (controllers/mpc/
+// cascaded_mpc.py:17-39,91-304; config/controllers/cascaded.yaml N = 20 + M = 40, and the
+// recorded runs' M = 15 / 25 / 35, experiments/data/*/cascaded_config.yaml).  Contract:
+// oracle/casc_sqp.py, the same QPs the condensed kernel casc_sqp.hip solves.  The QP is
+// restated stage by stage (the single-track part exactly as st_sqp.hip):
+//   stage vector v_k (9) = (y_k, p_k, u_k), QP state xt_k = (y_k, p_k), p_k = dFx_{k-1} (the Fx
+//   slews and the switching Fx term couple neighbouring inputs)
+//     single-track k < N:  y = (dUx, dUy, dr, ddelta, dey, depsi), u = (dFx / S, dw)
+//     point mass  k >= N:  y = (dV, dey, depsi, c, 0, 0),           u = (dFx / S, dFy / S)
+//   where c = dFy_{k-1} / S for k > N (the Fy slew) and, at the first point-mass stage k = N,
+//   the linearised change of the lateral tyre forces Fy_f + Fy_r of stage N-1 (the switching
+//   cost's lateral residual, cascaded_mpc.py:241-255) -- so every cost term is stage-local.
+//   Transitions xt_{k+1} = [A6 | 0 | B6; 0 | 0 | e_Fx] v_k: single-track RK4 Jacobians; the
+//   switching map (cascaded_mpc.py:256-277) at k = N-1 (V, ey, epsi from (Ux, Uy, ey, epsi),
+//   c from the lateral-force gradient); point-mass Euler Jacobians (dynamic_point_mass.py:
+//   76-100) for k >= N.  s is fixed (s' = 1 in both models); t enters only the terminal
+//   w_time t_{H-1}, a linear stage term through each step's t-row (the switch copies t).
+//   Stage Hessians share one 21-slot pattern; the 12 one-sided rows of a stage touch
+//   (y0..y3, dFx, u1) only (point mass: V >= V_min, Fx <= Peng / V, the trust region).
+// Per SQP iteration: predict (lane 0: RK4, switch, Euler), linearize (one lane per (stage,
+// seed pair), dual numbers), then the Mehrotra predictor-corrector whose Newton steps are LQ
+// problems solved by a backward Riccati recursion over the H stages (O(H) per iteration;
+// the condensed kernel pays O(H^3)) and a forward rollout; lane k owns stage k's rows,
+// slacks and multipliers in registers.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -33,10 +37,9 @@ namespace vc {
 namespace {
 
 constexpr int WTH = 64;
-constexpr int NQ = 20;  // nonzeros of a stage Hessian over v = (Ux, Uy, r, delta, ey, epsi, p, dFx, dw)
+constexpr int NQ = 21;  // nonzeros of a stage Hessian over v = (y0..y5, p, u0, u1)
 constexpr int NR = 12;  // one-sided rows per stage
-// slots of the stage Hessian's nonzeros (block {Ux, Uy, r, delta, dFx} + five diagonal-ish)
-enum { Q00, Q01, Q02, Q03, Q07, Q11, Q12, Q13, Q17, Q22, Q23, Q27, Q33, Q37, Q77, Q44, Q55, Q66, Q67, Q88 };
+enum { Q00, Q01, Q02, Q03, Q07, Q11, Q12, Q13, Q17, Q22, Q23, Q27, Q33, Q37, Q77, Q44, Q55, Q66, Q67, Q88, Q38 };
 
 __host__ __device__ constexpr int qslot(int i, int j) {
   if (i > j) { const int t = i; i = j; j = t; }
@@ -51,31 +54,34 @@ __host__ __device__ constexpr int qslot(int i, int j) {
   if (i == 6 && j == 6) return Q66;
   if (i == 6 && j == 7) return Q67;
   if (i == 8 && j == 8) return Q88;
+  if (i == 3 && j == 8) return Q38;
   return -1;
 }
 // stage vector index -> column of [A6 | B6] (-1 for p: no dynamics enters through it)
 __host__ __device__ constexpr int vcol(int i) { return i < 6 ? i : (i == 6 ? -1 : i - 1); }
 
-template <int N>
-struct StSmem {
-  double xs[N][8];    // prediction (N columns, dynamics for k < N-1)
-  double ub[N][2];    // current ubar
-  double kap[N], dsv[N];
-  double J[N][6][8];  // [A6 | B6 diag(S, 1)] of step k (rows/cols Ux, Uy, r, delta, ey, epsi | dFx, dw)
+template <int N, int M>
+struct CrSmem {
+  static constexpr int H = N + M;
+  double xs[H][8];    // prediction: single-track states k < N, point-mass (V, s, ey, epsi, t) k >= N
+  double ub[H][2];    // current ubar
+  double kap[H], dsv[H];
+  double J[H][6][8];  // [A6 | B6 diag(S, 1 or S)] of the transition out of stage k
   union {
     struct {
-      double Qt[N][NQ];  // stage Hessian + barrier, this iteration
-      double gr[N][9];   // stage gradient Q v + q + C' lam
-      double h[N][9];    // linear term of the current LQ solve
-      double v[N][9];    // QP iterate (xt, u)
-      double dv[N][9];   // Newton direction
-      double K[N][2][7];
-      double Hi[N][3];   // Huu^-1 (00, 01, 11)
-      double kk[N][2];
+      double Qt[H][NQ];  // stage Hessian + barrier, this iteration
+      double gr[H][9];   // stage gradient Q v + q + C' lam
+      double h[H][9];    // linear term of the current LQ solve
+      double v[H][9];    // QP iterate (xt, u)
+      double dv[H][9];   // Newton direction
+      double K[H][2][7];
+      double Hi[H][3];   // Huu^-1 (00, 01, 11)
+      double kk[H][2];
     } q;
     struct {
-      double trow[N][8];     // t-row of step k over (y | dFx, dw)
-      double st[N][7][6];    // stage functions: value + gradient over (Ux, Uy, r, delta, Fx)
+      double trow[H][8];     // t-row of the transition out of stage k over (y | u)
+      double st[N][7][6];    // single-track stage functions: value + gradient over (Ux, Uy, r, delta, Fx)
+      double gfy[6];         // Fy_f + Fy_r at stage N-1: value + gradient over (Ux, Uy, r, delta, Fx)
     } l;
   } u;
   double P[7][7];
@@ -84,9 +90,6 @@ struct StSmem {
   int flag[4];
 };
 
-// Workgroup = one wavefront: LDS operations of a wave execute in order, so a sync only has to
-// stop the compiler from moving memory operations across it (no s_barrier, and no wait for
-// outstanding loads other than the ones actually used).
 #define WSYNC()                          \
   do {                                   \
     asm volatile("" ::: "memory");       \
@@ -116,29 +119,11 @@ __device__ __forceinline__ double wsum(double v) {
 }
 __device__ __forceinline__ double step_to_bound(double x, double dx) { return dx < 0.0 ? -x / dx : 1e300; }
 
-// Section timing (debug builds only, -DVC_TIMING, `make timing`): lane 0's s_memtime stamps,
-// accumulated per section and written to diag[b][4 + slot] (scripts/st_section_timing.py).
-enum { ST_PRED = 0, ST_LIN, ST_SETUP, ST_RESID, ST_DUAL, ST_FACT, ST_SOLVE, ST_STEP, ST_TOTAL, ST_NSLOT };
-#ifdef VC_TIMING
-#define ST_STAMP(var)                                \
-  __builtin_amdgcn_sched_barrier(0);                 \
-  const uint64_t var = __builtin_amdgcn_s_memtime(); \
-  __builtin_amdgcn_sched_barrier(0);
-#define ST_ACC(slot, t0)                               \
-  {                                                    \
-    __builtin_amdgcn_sched_barrier(0);                 \
-    tacc[slot] += __builtin_amdgcn_s_memtime() - (t0); \
-    __builtin_amdgcn_sched_barrier(0);                 \
-  }
-#else
-#define ST_STAMP(var)
-#define ST_ACC(slot, t0)
-#endif
-
 // Stage k's one-sided rows C v <= d (lane-owned):
-//   0: -Ux <= Ux - Ux_min          1: delta <= delta_max - delta   2: -delta <= delta - delta_min
-//   3..7: c_r . (Ux, Uy, r, delta, dFx) <= d_r   (power limit, tyre force bounds front / rear)
-//   8: dw <= ..   9: -dw <= ..   10: dFx <= trust   11: -dFx <= trust
+//   0: -y0 <= ..   (Ux >= Ux_min, point mass V >= V_min)
+//   1: y3 <= ..   2: -y3 <= ..   (delta bounds, single track)
+//   3..7: c_r . (y0, y1, y2, y3, u0) <= d_r   (power limit, tyre force bounds; point mass: Peng / V)
+//   8: u1 <= ..   9: -u1 <= ..   (w box, point mass: the Fy trust region)   10, 11: |u0| trust
 struct Rows {
   double c[5][5];
   double d[NR];
@@ -172,44 +157,46 @@ __device__ __forceinline__ void row_adjoint(const Rows& R, const double* y, doub
   out[8] += y[8] - y[9];
   out[7] += y[10] - y[11];
 }
-// out = Q v (symmetric, 20 slots)
+// out = Q v (symmetric, 21 slots)
 __device__ __forceinline__ void qmul(const double* Q, const double* v, double* o) {
   o[0] = Q[Q00] * v[0] + Q[Q01] * v[1] + Q[Q02] * v[2] + Q[Q03] * v[3] + Q[Q07] * v[7];
   o[1] = Q[Q01] * v[0] + Q[Q11] * v[1] + Q[Q12] * v[2] + Q[Q13] * v[3] + Q[Q17] * v[7];
   o[2] = Q[Q02] * v[0] + Q[Q12] * v[1] + Q[Q22] * v[2] + Q[Q23] * v[3] + Q[Q27] * v[7];
-  o[3] = Q[Q03] * v[0] + Q[Q13] * v[1] + Q[Q23] * v[2] + Q[Q33] * v[3] + Q[Q37] * v[7];
+  o[3] = Q[Q03] * v[0] + Q[Q13] * v[1] + Q[Q23] * v[2] + Q[Q33] * v[3] + Q[Q37] * v[7] + Q[Q38] * v[8];
   o[4] = Q[Q44] * v[4];
   o[5] = Q[Q55] * v[5];
   o[6] = Q[Q66] * v[6] + Q[Q67] * v[7];
   o[7] = Q[Q07] * v[0] + Q[Q17] * v[1] + Q[Q27] * v[2] + Q[Q37] * v[3] + Q[Q67] * v[6] + Q[Q77] * v[7];
-  o[8] = Q[Q88] * v[8];
+  o[8] = Q[Q88] * v[8] + Q[Q38] * v[3];
 }
 
-template <int N, int TYRE>
-__global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
-  static_assert(N >= 2 && N <= WTH, "one lane per stage");
-  __shared__ StSmem<N> s;
+template <int N, int M, int TYRE>
+__global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
+  constexpr int H = N + M;
+  static_assert(N >= 2 && M >= 2 && H <= WTH, "one lane per stage");
+  __shared__ CrSmem<N, M> s;
   const int l = threadIdx.x;
   const int b = blockIdx.x;
   DynCoef<double> c = A.car;
   c.tyre = TYRE;
   const vc_dyn_mpc& W = A.w;
+  const vc_casc_mpc& CW = A.cw;
   const double S = W.fx_scale;
-  const bool stl = l < N;
+  const bool stl = l < H;
   const int k = stl ? l : 0;  // this lane's stage
+  const bool pm = k >= N;     // point-mass stage
 
-  for (int i = l; i < N; i += WTH) {
-    s.kap[i] = A.kappa[(size_t)b * N + i];
-    s.dsv[i] = A.ds[(size_t)b * N + i];
-    s.ub[i][0] = A.ubar[((size_t)b * N + i) * 2];
-    s.ub[i][1] = A.ubar[((size_t)b * N + i) * 2 + 1];
+  for (int i = l; i < H; i += WTH) {
+    s.kap[i] = A.kappa[(size_t)b * H + i];
+    s.dsv[i] = A.ds[(size_t)b * H + i];
+    s.ub[i][0] = A.ubar[((size_t)b * H + i) * 2];
+    s.ub[i][1] = A.ubar[((size_t)b * H + i) * 2 + 1];
   }
   if (l < 8) s.xs[0][l] = A.x0[(size_t)b * 8 + l];
+  if (l >= N && l < H) {  // point-mass slots 5..7 are reported as 0 (free in the reference's NLP)
+    s.xs[l][5] = s.xs[l][6] = s.xs[l][7] = 0.0;
+  }
   if (l == 0) s.flag[0] = VC_SOLVED;
-#ifdef VC_TIMING
-  uint64_t tacc[ST_NSLOT] = {};
-  const uint64_t t_start = __builtin_amdgcn_s_memtime();
-#endif
   WSYNC();
 
   // Riccati lane roles (fixed per lane): H entry (hi, hj), hi <= hj, for lanes < 45
@@ -221,7 +208,6 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     hj = i + q;
   }
   const int hslot = qslot(hi, hj), hci = vcol(hi), hcj = vcol(hj);
-  // P entry (pi, pj) for lanes < 28
   int pi = 0, pj = 0;
   {
     int q = l < 28 ? l : 0, i = 0;
@@ -229,7 +215,6 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     pi = i;
     pj = i + q;
   }
-  const int sc = l < 9 ? vcol(l) : -1;  // sweep lanes 0..8: column of [A6 | B6] of v index l
 
   int it_total = 0, it_max = 0;
   bool all_conv = true, any_fail = false;
@@ -237,8 +222,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
   const double tol_r = 1e-10, tol_mu = 1e-13;
 
   for (int sq = 0;; ++sq) {
-    // ---------------- predict (lane 0, serial RK4) ----------------
-    ST_STAMP(t_p0)
+    // ---------------- predict (lane 0: RK4, switch, point-mass Euler) ----------------
     if (l == 0) {
       double x[8];
 #pragma unroll
@@ -256,21 +240,37 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
           fin = fin && isfinite(xn[i]);
         }
       }
+      double p[5];
+      st_to_pm<double>(x, p);  // cascaded_mpc.py:256-277
+#pragma unroll
+      for (int i = 0; i < 5; ++i) s.xs[N][i] = p[i];
+      for (int j = N; j < H - 1; ++j) {  // dynamic_point_mass.py:76-100, Euler
+        const double u2[2] = {s.ub[j][0], s.ub[j][1]};
+        double f[5];
+        pm_spatial_ode<double, double>(p, u2, s.kap[j], c, f);
+        const double h = s.dsv[j];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+          p[i] = p[i] + h * f[i];
+          s.xs[j + 1][i] = p[i];
+          fin = fin && isfinite(p[i]);
+        }
+      }
       if (!fin) s.flag[0] = VC_NONFINITE;
     }
     WSYNC();
-    ST_ACC(ST_PRED, t_p0)
     if (sq == W.sqp_iters || s.flag[0] == VC_NONFINITE) break;
 
     // ---------------- linearize + stage functions ----------------
-    ST_STAMP(t_l0)
     {
-      constexpr int NLIN = 4 * (N - 1), NTASK = NLIN + 5 * N;
+      constexpr int NLIN = 4 * (N - 1), NSTF = 5 * N, NPM = 3 * (M - 1);
       using D2 = Dual<2, double>;
       using D1 = Dual<1, double>;
+      // three task loops (one kind of work per loop: no divergent mix of the dual-number
+      // evaluations in one iteration)
 #pragma unroll 1
-      for (int task = l; task < NTASK; task += WTH) {
-        if (task < NLIN) {
+      for (int task = l; task < NLIN; task += WTH) {
+        {  // single-track RK4 step k -> k + 1 (k < N - 1): two columns of [A6 | B6]
           const int kk = task >> 2, pr = task & 3;
           // seed pairs: (Ux, Uy), (r, delta), (ey, epsi), (Fx, w)
           const int a0 = pr == 0 ? 0 : (pr == 1 ? 2 : (pr == 2 ? 5 : -1));
@@ -288,7 +288,6 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
           u2[1].d[1] = pr == 3 ? 1.0 : 0.0;
           const D2 kp(s.kap[kk]);
           rk4_apply<D2, 8>(x, D2(s.dsv[kk]), [&](const D2* xx, D2* f) { dyn_spatial_ode_alg<D2, double>(xx, u2, kp, c, f); }, xn);
-          // columns of [A6 | B6] (y index of the seeds) and the t-row
           const int c0 = pr < 3 ? 2 * pr : 6, c1 = c0 + 1;
           const double s0 = pr == 3 ? S : 1.0;
           const int yr[6] = {0, 1, 2, 3, 5, 6};
@@ -299,8 +298,12 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
           }
           s.u.l.trow[kk][c0] = xn[7].d[0] * s0;
           s.u.l.trow[kk][c1] = xn[7].d[1];
-        } else {
-          const int q = task - NLIN, kk = q / 5, j = q % 5;
+        }
+      }
+#pragma unroll 1
+      for (int task = l; task < NSTF; task += WTH) {
+        {  // single-track stage functions (cascaded_mpc.py:110-128,155-165)
+          const int q = task, kk = q / 5, j = q % 5;
           D1 X5[5], o[7];
 #pragma unroll
           for (int i = 0; i < 4; ++i) X5[i] = D1(s.xs[kk][i]);
@@ -315,10 +318,96 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
           }
         }
       }
+#pragma unroll 1
+      for (int task = l; task < NPM; task += WTH) {
+        {  // point-mass Euler step j -> j + 1: seed pairs (V, ey), (epsi, -), (Fx, Fy)
+          const int q = task, j = N + q / 3, pr = q % 3;
+          D2 x[5], u2[2], f[5];
+          const int a0 = pr == 0 ? 0 : (pr == 1 ? 3 : -1), a1 = pr == 0 ? 2 : -1;
+#pragma unroll
+          for (int i = 0; i < 5; ++i) {
+            x[i] = D2(s.xs[j][i]);
+            x[i].d[0] = i == a0 ? 1.0 : 0.0;
+            x[i].d[1] = i == a1 ? 1.0 : 0.0;
+          }
+          u2[0] = D2(s.ub[j][0]);
+          u2[1] = D2(s.ub[j][1]);
+          u2[0].d[0] = pr == 2 ? 1.0 : 0.0;
+          u2[1].d[1] = pr == 2 ? 1.0 : 0.0;
+          pm_spatial_ode<D2, double>(x, u2, D2(s.kap[j]), c, f);
+          const double h = s.dsv[j];
+          // rows (V, ey, epsi) of I + h df/dx at y slots (0, 1, 2); inputs scaled by S; the
+          // Fy slew's c row (3) = e_u1; t-row over (V, ey, epsi)
+          const int yi[3] = {0, 2, 3};
+          if (pr == 0) {
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+              s.J[j][r][0] = (r == 0 ? 1.0 : 0.0) + h * f[yi[r]].d[0];
+              s.J[j][r][1] = (r == 1 ? 1.0 : 0.0) + h * f[yi[r]].d[1];
+            }
+            s.u.l.trow[j][0] = h * f[4].d[0];
+            s.u.l.trow[j][1] = h * f[4].d[1];
+          } else if (pr == 1) {
+#pragma unroll
+            for (int r = 0; r < 3; ++r) s.J[j][r][2] = (r == 2 ? 1.0 : 0.0) + h * f[yi[r]].d[0];
+            s.u.l.trow[j][2] = h * f[4].d[0];
+#pragma unroll
+            for (int cc = 3; cc < 6; ++cc) {
+              s.J[j][0][cc] = s.J[j][1][cc] = s.J[j][2][cc] = 0.0;
+              s.u.l.trow[j][cc] = 0.0;
+            }
+#pragma unroll
+            for (int r = 3; r < 6; ++r)
+#pragma unroll
+              for (int cc = 0; cc < 8; ++cc) s.J[j][r][cc] = (r == 3 && cc == 7) ? 1.0 : 0.0;
+          } else {
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+              s.J[j][r][6] = h * f[yi[r]].d[0] * S;
+              s.J[j][r][7] = h * f[yi[r]].d[1] * S;
+            }
+            s.u.l.trow[j][6] = h * f[4].d[0] * S;
+            s.u.l.trow[j][7] = h * f[4].d[1] * S;
+          }
+        }
+      }
     }
     WSYNC();
-    ST_ACC(ST_LIN, t_l0)
-    ST_STAMP(t_s0)
+    // the switching map out of stage N - 1 (cascaded_mpc.py:241-277): lanes 0..4 the lateral
+    // tyre forces Fy_f + Fy_r and their gradient (one dual seed each), lane 5 the Jacobian rows
+    // (V, ey, epsi); t passes through unchanged
+    if (l < 5) {
+      using D1 = Dual<1, double>;
+      D1 X5[5];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) X5[i] = D1(s.xs[N - 1][i]);
+      X5[4] = D1(s.ub[N - 1][0]);
+#pragma unroll
+      for (int i = 0; i < 5; ++i) X5[i].d[0] = i == l ? 1.0 : 0.0;
+      const D1 fy = dyn_lateral_sum<D1, double>(X5, c);
+      s.u.l.gfy[1 + l] = fy.d[0];
+      if (l == 0) s.u.l.gfy[0] = fy.v;
+    } else if (l == 5) {
+      const double Ux = s.xs[N - 1][0], Uy = s.xs[N - 1][1];
+      const double q2 = Ux * Ux + Uy * Uy, V = sqrt(q2);
+#pragma unroll
+      for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int cc = 0; cc < 8; ++cc) s.J[N - 1][r][cc] = 0.0;
+      s.J[N - 1][0][0] = Ux / V;
+      s.J[N - 1][0][1] = Uy / V;
+      s.J[N - 1][1][4] = 1.0;
+      s.J[N - 1][2][0] = -Uy / q2;
+      s.J[N - 1][2][1] = Ux / q2;
+      s.J[N - 1][2][5] = 1.0;
+#pragma unroll
+      for (int cc = 0; cc < 8; ++cc) s.u.l.trow[N - 1][cc] = 0.0;
+    }
+    WSYNC();
+    // the switch's c row: the lateral-force gradient over (Ux, Uy, r, delta | dFx / S)
+    if (l < 4) s.J[N - 1][3][l] = s.u.l.gfy[1 + l];
+    if (l == 4) s.J[N - 1][3][6] = s.u.l.gfy[5] * S;
+    WSYNC();
 
     // ---------------- stage QP data (lane k, registers) ----------------
     double Qc[NQ], qc[9];
@@ -329,40 +418,50 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     for (int e = 0; e < 9; ++e) qc[e] = 0.0;
     {
       const double ds = s.dsv[k];
-      const double ey = s.xs[k][5];
-      // boundary + deviation (cascaded_mpc.py:139-151), obstacle barrier (:173-176) in ey
-      const double cdev = W.w_dev * ds;
-      const double blo = ey < W.ey_min ? W.w_b * ds : 0.0, bhi = ey > W.ey_max ? W.w_b * ds : 0.0;
-      Qc[Q44] += 2.0 * (cdev + blo + bhi);
-      qc[4] += 2.0 * (cdev * ey + blo * (ey - W.ey_min) + bhi * (ey - W.ey_max));
-      if (A.obs.n > 0) {
-        double po, qo;
-        obstacle_ey_model<double>(A.obs, s.xs[k][4], ey, W.w_obs * ds, po, qo);
-        Qc[Q44] += qo;
-        qc[4] += po;
+      // ey / s slots of this stage's state
+      const double ey = pm ? s.xs[k][2] : s.xs[k][5], sa = pm ? s.xs[k][1] : s.xs[k][4];
+      const double wdev = pm ? CW.w_dev_pm : W.w_dev, eylo = pm ? CW.ey_min_pm : W.ey_min,
+                   eyhi = pm ? CW.ey_max_pm : W.ey_max;
+      // boundary + deviation (cascaded_mpc.py:139-151, point mass :204-219), obstacles (:173-176)
+      const double cdev = wdev * ds;
+      const double blo = ey < eylo ? W.w_b * ds : 0.0, bhi = ey > eyhi ? W.w_b * ds : 0.0;
+      const double cey = 2.0 * (cdev + blo + bhi), qey = 2.0 * (cdev * ey + blo * (ey - eylo) + bhi * (ey - eyhi));
+      double po = 0.0, qo = 0.0;
+      if (A.obs.n > 0) obstacle_ey_model<double>(A.obs, sa, ey, W.w_obs * ds, po, qo);
+      if (pm) {
+        Qc[Q11] += cey + qo;
+        qc[1] += qey + po;
+      } else {
+        Qc[Q44] += cey + qo;
+        qc[4] += qey + po;
       }
-      // w^2 (:153), prox on the scaled step
-      Qc[Q88] += 2.0 * W.w_w + 2.0 * A.qp.prox;
-      qc[8] += 2.0 * W.w_w * s.ub[k][1];
+      // prox on the scaled step, w^2 on the single track (:153)
       Qc[Q77] += 2.0 * A.qp.prox;
-      // slip-angle penalties when active at the prediction (:155-165)
+      Qc[Q88] += 2.0 * A.qp.prox;
+      if (!pm) {
+        Qc[Q88] += 2.0 * W.w_w;
+        qc[8] += 2.0 * W.w_w * s.ub[k][1];
+        // slip-angle penalties when active at the prediction (:155-165)
 #pragma unroll
-      for (int sr = 0; sr < 2; ++sr) {
-        const double fv = s.u.l.st[k][sr][0];
-        const double wsl = fv >= 0.0 ? 2.0 * W.w_slip : 0.0;
-        const double a5[5] = {s.u.l.st[k][sr][1], s.u.l.st[k][sr][2], s.u.l.st[k][sr][3], s.u.l.st[k][sr][4],
-                              s.u.l.st[k][sr][5] * S};
-        constexpr int ix[5] = {0, 1, 2, 3, 7};
+        for (int sr = 0; sr < 2; ++sr) {
+          const double fv = s.u.l.st[k][sr][0];
+          const double wsl = fv >= 0.0 ? 2.0 * W.w_slip : 0.0;
+          const double a5[5] = {s.u.l.st[k][sr][1], s.u.l.st[k][sr][2], s.u.l.st[k][sr][3], s.u.l.st[k][sr][4],
+                                s.u.l.st[k][sr][5] * S};
+          constexpr int ix[5] = {0, 1, 2, 3, 7};
 #pragma unroll
-        for (int a = 0; a < 5; ++a) {
-          qc[ix[a]] += wsl * fv * a5[a];
+          for (int a = 0; a < 5; ++a) {
+            qc[ix[a]] += wsl * fv * a5[a];
 #pragma unroll
-          for (int e = a; e < 5; ++e) Qc[qslot(ix[a], ix[e])] += wsl * a5[a] * a5[e];
+            for (int e = a; e < 5; ++e) Qc[qslot(ix[a], ix[e])] += wsl * a5[a] * a5[e];
+          }
         }
       }
-      // Fx slew with the previous stage (:167-171): c (dFx_k - p_k + (Fx_k - Fx_{k-1}) / S)^2 S^2
+      // Fx slew with the previous stage (:167-171, point mass :226-232), the switching Fx term at
+      // k = N (:244-249): c (dFx_k - p_k + (Fx_k - Fx_{k-1}) / S)^2 S^2, c = w / ds_{k-1}
       if (k >= 1) {
-        const double cs = 2.0 * W.w_Fx / s.dsv[k - 1] * S * S;
+        const double wfx = k == N ? CW.w_switch : W.w_Fx;
+        const double cs = 2.0 * wfx / s.dsv[k - 1] * S * S;
         const double r0 = (s.ub[k][0] - s.ub[k - 1][0]) / S;
         Qc[Q66] += cs;
         Qc[Q67] -= cs;
@@ -370,48 +469,90 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
         qc[6] -= cs * r0;
         qc[7] += cs * r0;
       }
-      // w_time t_{N-1} = sum_k t-row_k . (y_k, u_k): linear stage terms (:292)
-      if (k < N - 1) {
+      if (k == N) {  // switching lateral term (:250-255): csw (dFy S - c + Fy_N - (Fy_f + Fy_r))^2
+        const double csw = 2.0 * CW.w_switch / s.dsv[N - 1];
+        const double r1 = s.ub[N][1] - s.u.l.gfy[0];
+        Qc[Q33] += csw;
+        Qc[Q38] -= csw * S;
+        Qc[Q88] += csw * S * S;
+        qc[3] -= csw * r1;
+        qc[8] += csw * r1 * S;
+      } else if (k > N) {  // Fy slew (:233-239): c (dFy_k - c_k + (Fy_k - Fy_{k-1}) / S)^2 S^2
+        const double cf = 2.0 * CW.w_Fy / s.dsv[k - 1] * S * S;
+        const double r0 = (s.ub[k][1] - s.ub[k - 1][1]) / S;
+        Qc[Q33] += cf;
+        Qc[Q38] -= cf;
+        Qc[Q88] += cf;
+        qc[3] -= cf * r0;
+        qc[8] += cf * r0;
+      }
+      // w_time t_{H-1} = sum_k t-row_k . (y_k, u_k): linear stage terms (:292)
+      if (k < H - 1) {
         constexpr int iy[8] = {0, 1, 2, 3, 4, 5, 7, 8};
 #pragma unroll
         for (int a = 0; a < 8; ++a) qc[iy[a]] += W.w_time * s.u.l.trow[k][a];
       }
-      // terminal (:290-303)
-      if (k == N - 1) {
-        const double Ux = s.xs[k][0];
-        if (Ux >= W.max_speed) {
+      // terminal on the last point-mass state (:279-304)
+      if (k == H - 1) {
+        const double V = s.xs[k][0];
+        if (V >= W.max_speed) {
           Qc[Q00] += 2.0 * W.w_speed;
-          qc[0] += 2.0 * W.w_speed * (Ux - W.max_speed);
+          qc[0] += 2.0 * W.w_speed * (V - W.max_speed);
         }
-        Qc[Q44] += 2.0 * W.w_ey;
-        qc[4] += 2.0 * W.w_ey * ey;
-        Qc[Q55] += 2.0 * W.w_epsi;
-        qc[5] += 2.0 * W.w_epsi * s.xs[k][6];
+        Qc[Q11] += 2.0 * W.w_ey;
+        qc[1] += 2.0 * W.w_ey * ey;
+        Qc[Q22] += 2.0 * W.w_epsi;
+        qc[2] += 2.0 * W.w_epsi * s.xs[k][3];
       }
-      // rows (:101-128, trust region)
-      const double mk = (stl && k >= 1) ? 1.0 : 0.0;
-      R.d[0] = s.xs[k][0] - W.Ux_min;
-      R.d[1] = W.delta_max - s.xs[k][3];
-      R.d[2] = s.xs[k][3] - W.delta_min;
-      R.m[0] = R.m[1] = R.m[2] = mk;
+      // rows (:101-128, point mass :190-195, trust region)
+      const double on = stl ? 1.0 : 0.0;
 #pragma unroll
-      for (int r = 0; r < 5; ++r) {
-        const int fn = 2 + r;
+      for (int r = 0; r < 5; ++r)
 #pragma unroll
-        for (int a = 0; a < 4; ++a) R.c[r][a] = s.u.l.st[k][fn][1 + a] / S;
-        R.c[r][4] = s.u.l.st[k][fn][5];
-        R.d[3 + r] = -s.u.l.st[k][fn][0] / S;
-        R.m[3 + r] = stl ? 1.0 : 0.0;
+        for (int a = 0; a < 5; ++a) R.c[r][a] = 0.0;
+      if (!pm) {
+        const double mk = (stl && k >= 1) ? 1.0 : 0.0;
+        R.d[0] = s.xs[k][0] - W.Ux_min;
+        R.d[1] = W.delta_max - s.xs[k][3];
+        R.d[2] = s.xs[k][3] - W.delta_min;
+        R.m[0] = R.m[1] = R.m[2] = mk;
+#pragma unroll
+        for (int r = 0; r < 5; ++r) {
+          const int fn = 2 + r;
+#pragma unroll
+          for (int a = 0; a < 4; ++a) R.c[r][a] = s.u.l.st[k][fn][1 + a] / S;
+          R.c[r][4] = s.u.l.st[k][fn][5];
+          R.d[3 + r] = -s.u.l.st[k][fn][0] / S;
+          R.m[3 + r] = on;
+        }
+        const double wv = s.ub[k][1];
+        double up = W.w_max - wv, dn = wv - W.w_min;
+        if (A.qp.trust_w > 0) {
+          up = fmin(up, A.qp.trust_w);
+          dn = fmin(dn, A.qp.trust_w);
+        }
+        R.d[8] = up;
+        R.d[9] = dn;
+        R.m[8] = R.m[9] = on;
+      } else {
+        const double V = s.xs[k][0];
+        R.d[0] = V - CW.V_min;
+        R.m[0] = on;
+        R.d[1] = R.d[2] = 1.0;
+        R.m[1] = R.m[2] = 0.0;
+        // Fx - Peng / V <= 0 (divided by S), linearised in (V, Fx)
+        R.c[0][0] = c.Peng / (V * V) / S;
+        R.c[0][4] = 1.0;
+        R.d[3] = -(s.ub[k][0] - c.Peng / V) / S;
+        R.m[3] = on;
+#pragma unroll
+        for (int r = 4; r < 8; ++r) {
+          R.d[r] = 1.0;
+          R.m[r] = 0.0;
+        }
+        R.d[8] = R.d[9] = W.trust_Fx / S;
+        R.m[8] = R.m[9] = (stl && W.trust_Fx > 0) ? 1.0 : 0.0;
       }
-      const double wv = s.ub[k][1];
-      double up = W.w_max - wv, dn = wv - W.w_min;
-      if (A.qp.trust_w > 0) {
-        up = fmin(up, A.qp.trust_w);
-        dn = fmin(dn, A.qp.trust_w);
-      }
-      R.d[8] = up;
-      R.d[9] = dn;
-      R.m[8] = R.m[9] = stl ? 1.0 : 0.0;
       R.d[10] = R.d[11] = W.trust_Fx / S;
       R.m[10] = R.m[11] = (stl && W.trust_Fx > 0) ? 1.0 : 0.0;
 #pragma unroll
@@ -440,26 +581,14 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       for (int e = 0; e < 9; ++e) s.u.q.v[k][e] = 0.0;
     }
     WSYNC();
-    ST_ACC(ST_SETUP, t_s0)
 
-    // ---- LQ machinery -----------------------------------------------------------------
-    // Every stage loop below is branch-free in its lanes (clamped addresses, 0/1 masks) and
-    // loads the next stage's operands before the current stage's dependent chain, so LDS
-    // latency stays off the recursion; cross-lane values move by v_readlane.
-    //
-    // Riccati factorisation of the stage Hessians s.u.q.Qt (backward): K, Hi per stage.
-    //   T = P [A6 B6 ; 0 e_Fx]      lanes 0..55  (a, j) = (l / 8, l % 8)
-    //   H = Qt + [..]' T            lanes 0..44  (hi, hj)
-    //   P' = Hxx - Hux' Huu^-1 Hux  lanes 0..27, K = -Huu^-1 Hux lanes 28..41, Huu^-1 lane 42
+    // ---- LQ machinery (st_sqp.hip's, over H stages) -----------------------------------
     const int ta = l < 56 ? (l >> 3) : 0, tj = l & 7;
     const double tpm = tj == 6 ? 1.0 : 0.0;
     const int hcic = hci < 0 ? 0 : hci, hcjc = hcj < 0 ? 0 : hcj;
     const double hdyn = (l < 45 && hci >= 0 && hcj >= 0) ? 1.0 : 0.0, hpm = hci == 6 ? 1.0 : 0.0;
     const int hsc = hslot < 0 ? 0 : hslot;
     const double hq = (l < 45 && hslot >= 0) ? 1.0 : 0.0;
-    // The stage loops are unrolled by two with ping-pong operand buffers (A for kk, B for
-    // the next stage): no register rotation at the loop latch, so the next stage's loads
-    // stay in flight across the current stage's chain.
     struct FacOps {
       double JT[6], JH[6], qv;
     };
@@ -473,7 +602,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     };
     auto fac_stage = [&](int kk, const FacOps& o) -> bool {
       double hv = hq * o.qv;
-      if (kk < N - 1) {  // uniform
+      if (kk < H - 1) {  // uniform
         double acc = tpm * s.P[ta][6];
 #pragma unroll
         for (int e = 0; e < 6; ++e) acc += s.P[ta][e] * o.JT[e];
@@ -491,13 +620,11 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       WSYNC();
       const double h00 = s.Hm[7][7], h01 = s.Hm[7][8], h11 = s.Hm[8][8];
       const double det = h00 * h11 - h01 * h01;
-      // 1 / det: v_rcp_f64 + two Newton steps (full fp64 accuracy, no IEEE divide sequence)
       double id = __builtin_amdgcn_rcp(det);
       id = id * (2.0 - det * id);
       id = id * (2.0 - det * id);
       const double i00 = h11 * id, i01 = -h01 * id, i11 = h00 * id;
       {
-        // lanes 0..27: P entry (pi, pj); lanes 28..41: K entry; lane 42: Huu^-1
         const int kc = l >= 28 && l < 42 ? (l - 28) / 7 : 0, ki = l >= 28 && l < 42 ? (l - 28) % 7 : 0;
         const int ci = l < 28 ? pi : ki;
         const double x0 = s.Hm[7][ci], x1 = s.Hm[8][ci], y0 = s.Hm[7][pj], y1 = s.Hm[8][pj];
@@ -517,13 +644,12 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       WSYNC();
       return h00 > 0.0 && det > 0.0;
     };
-    // Riccati factorisation of the stage Hessians s.u.q.Qt (backward): K, Hi per stage.
     auto factor = [&]() -> bool {
       bool ok = true;
       FacOps A0, B0;
-      fac_load(N - 1, A0);
+      fac_load(H - 1, A0);
 #pragma unroll 1
-      for (int kk = N - 1; kk >= 0; kk -= 2) {
+      for (int kk = H - 1; kk >= 0; kk -= 2) {
         const int k1 = kk >= 1 ? kk - 1 : 0, k2 = kk >= 2 ? kk - 2 : 0;
         fac_load(k1, B0);
         ok = fac_stage(kk, A0) && ok;
@@ -535,37 +661,29 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       return ok;
     };
 
-    // Sweep lanes 0..8 own the stage-vector components v = (y0..y5, p, dFx, dw).
     const int sl9 = l < 9 ? l : 8;
-    const int scol = vcol(sl9) < 0 ? 0 : vcol(sl9);                 // column of [A6 | B6]
-    const double smsk = (l < 9 && vcol(sl9) >= 0) ? 1.0 : 0.0;      // p (l = 6) has no dynamics column
-    const double spm = (l < 9 && vcol(sl9) == 6) ? 1.0 : 0.0;       // dFx picks up the p costate
-    // backward pass extras: lanes 0..6 read K[kk][0][l], K[kk][1][l]; lanes 7, 8 read the
-    // Huu^-1 pair of their kk component -> one formula t = a gu0 + b gu1 for both
+    const int scol = vcol(sl9) < 0 ? 0 : vcol(sl9);
+    const double smsk = (l < 9 && vcol(sl9) >= 0) ? 1.0 : 0.0;
+    const double spm = (l < 9 && vcol(sl9) == 6) ? 1.0 : 0.0;
     const int bl7 = l < 7 ? l : 0;
-    // forward pass: lanes 0..5 read J row l; lanes 7, 8 read K row (l - 7) and kk
     const int fr = l < 6 ? l : 0, fc = l == 8 ? 1 : 0;
     const bool fk = l == 7 || l == 8;
 
     struct BwdOps {
       double J6[6], h, a, b;
     };
-    // vec: s.u.q.h (solve) or s.u.q.gr (dual residual)
     auto bwd_load = [&](int kk, const double (*vec)[9], BwdOps& o) {
 #pragma unroll
       for (int e = 0; e < 6; ++e) o.J6[e] = s.J[kk][e][scol];
       o.h = vec[kk][sl9];
-      // lane-selected addresses, one unconditional load each (a value select would make
-      // the compiler predicate the loads and wait on the whole prefetch)
       const double* pa = l < 7 ? &s.u.q.K[kk][0][bl7] : &s.u.q.Hi[kk][l == 7 ? 0 : 1];
       const double* pb = l < 7 ? &s.u.q.K[kk][1][bl7] : &s.u.q.Hi[kk][l == 7 ? 1 : 2];
       o.a = *pa;
       o.b = *pb;
     };
-    // g = vec_k + [A6 | B6 ; 0 e_Fx]' p_{k+1} on lanes 0..8
     auto bwd_g = [&](int kk, const BwdOps& o, double pv) -> double {
       double g = o.h;
-      if (kk < N - 1) {  // uniform
+      if (kk < H - 1) {  // uniform
         double pb[7];
 #pragma unroll
         for (int a = 0; a < 7; ++a) pb[a] = bcast(pv, a);
@@ -586,7 +704,6 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       for (int e = 0; e < 7; ++e) o.w[e] = src[e];
       o.w[7] = *src7;
     };
-    // one forward stage: writes dv[kk], returns xt_{k+1} (lanes 0..6)
     auto fwd_stage = [&](int kk, const FwdOps& o, double X) -> double {
       double xb[7];
 #pragma unroll
@@ -594,19 +711,16 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       double acc = 0.0;
 #pragma unroll
       for (int e = 0; e < 6; ++e) acc += o.w[e] * xb[e];
-      const double uk = acc + o.w[6] * xb[6] + o.w[7];  // lanes 7, 8: u_c = K_c xt + kk_c
+      const double uk = acc + o.w[6] * xb[6] + o.w[7];
       const double u0 = bcast(uk, 7), u1 = bcast(uk, 8);
       if (l < 9) s.u.q.dv[kk][l] = fk ? uk : X;
-      const double xn = acc + o.w[6] * u0 + o.w[7] * u1;  // lanes 0..5
+      const double xn = acc + o.w[6] * u0 + o.w[7] * u1;
       return l < 6 ? xn : (l == 6 ? u0 : 0.0);
     };
-
-    // LQ solve with linear terms s.u.q.h -> direction s.u.q.dv (backward vector pass with the
-    // factor, then the forward rollout u = K xt + kk)
     auto lq_solve = [&]() {
       BwdOps A1, B1;
-      bwd_load(N - 1, s.u.q.h, A1);
-      double pv = 0.0;  // lanes 0..6: p_{k+1}
+      bwd_load(H - 1, s.u.q.h, A1);
+      double pv = 0.0;
       auto bstage = [&](int kk, const BwdOps& o) {
         const double g = bwd_g(kk, o, pv);
         const double gu0 = bcast(g, 7), gu1 = bcast(g, 8);
@@ -615,7 +729,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
         if (fk) s.u.q.kk[kk][l - 7] = -t2;
       };
 #pragma unroll 1
-      for (int kk = N - 1; kk >= 0; kk -= 2) {
+      for (int kk = H - 1; kk >= 0; kk -= 2) {
         const int k1 = kk >= 1 ? kk - 1 : 0, k2 = kk >= 2 ? kk - 2 : 0;
         bwd_load(k1, s.u.q.h, B1);
         bstage(kk, A1);
@@ -627,24 +741,22 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       WSYNC();
       FwdOps A2, B2;
       fwd_load(0, A2);
-      double X = 0.0;  // lanes 0..6: xt_k
+      double X = 0.0;
 #pragma unroll 1
-      for (int kk = 0; kk < N; kk += 2) {
-        const int k1 = kk + 1 < N ? kk + 1 : kk, k2 = kk + 2 < N ? kk + 2 : kk;
+      for (int kk = 0; kk < H; kk += 2) {
+        const int k1 = kk + 1 < H ? kk + 1 : kk, k2 = kk + 2 < H ? kk + 2 : kk;
         fwd_load(k1, B2);
         X = fwd_stage(kk, A2, X);
-        if (kk + 1 < N) {
+        if (kk + 1 < H) {
           fwd_load(k2, A2);
           X = fwd_stage(kk + 1, B2, X);
         }
       }
       WSYNC();
     };
-
-    // condensed dual residual max |d/du (sum_k gr_k . v_k)| through the dynamics (adjoint sweep)
     auto dual_residual = [&]() -> double {
       BwdOps A3, B3;
-      bwd_load(N - 1, s.u.q.gr, A3);
+      bwd_load(H - 1, s.u.q.gr, A3);
       double rho = 0.0, rmax = 0.0;
       auto rstage = [&](int kk, const BwdOps& o) {
         const double g = bwd_g(kk, o, rho);
@@ -652,7 +764,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
         rho = g;
       };
 #pragma unroll 1
-      for (int kk = N - 1; kk >= 0; kk -= 2) {
+      for (int kk = H - 1; kk >= 0; kk -= 2) {
         const int k1 = kk >= 1 ? kk - 1 : 0, k2 = kk >= 2 ? kk - 2 : 0;
         bwd_load(k1, s.u.q.gr, B3);
         rstage(kk, A3);
@@ -669,8 +781,6 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     bool conv = false, fail = false;
 #pragma unroll 1
     for (; it < A.qp.max_iter; ++it) {
-      // (a) residuals, stage gradients, barrier-augmented stage Hessians
-      ST_STAMP(t_r0)
       double vk[9], rp[NR], wg[NR], grk[9], val[NR];
       double rpm = 0.0, mus = 0.0;
 #pragma unroll
@@ -718,19 +828,13 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       WSYNC();
       rpm = wmax(rpm);
       const double mu = wsum(mus) / mcount;
-      ST_ACC(ST_RESID, t_r0)
-      ST_STAMP(t_d0)
       const double rdm = dual_residual();
-      ST_ACC(ST_DUAL, t_d0)
       last_res = fmax(rdm, rpm);
       last_mu = mu;
       if (!(last_res == last_res) || !(mu == mu) || last_res > 1e300) { fail = true; break; }
       if (last_res <= rtol && mu <= tol_mu) { conv = true; break; }
 
-      // (b) Riccati factorisation of H + C'WC
-      ST_STAMP(t_f0)
       const bool fok = factor();
-      ST_ACC(ST_FACT, t_f0)
       if (!fok) {
         // the barrier-augmented recursion lost definiteness at the numerical floor (weights
         // ~1e13, cancellation in P = Hxx - Hxu Huu^-1 Hux): a near-converged iterate stands
@@ -739,7 +843,6 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
         break;
       }
 
-      // (c) predictor: h = gr + C'(W rp - lam)
       auto set_h = [&](const double* rc_over_s) {
         if (stl) {
           double y[NR], hk[9];
@@ -753,13 +856,8 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
         }
         WSYNC();
       };
-      ST_STAMP(t_q0)
       set_h(la);
-      ST_ACC(ST_STEP, t_q0)
-      ST_STAMP(t_q1)
       lq_solve();
-      ST_ACC(ST_SOLVE, t_q1)
-      ST_STAMP(t_q2)
       double dsa[NR], dla[NR], cdv[NR], dvk[9];
       double amin = 1.0;
 #pragma unroll
@@ -781,16 +879,11 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       const double ratio = mu > 0.0 ? fmin(1.0, ms / mu) : 0.0;
       const double smu = ratio * ratio * ratio * mu;
 
-      // (d) corrector: rc = s lam + ds_a dl_a - sigma mu
       double rcs[NR];
 #pragma unroll
       for (int i = 0; i < NR; ++i) rcs[i] = R.m[i] * (sl[i] * la[i] + dsa[i] * dla[i] - smu) / sl[i];
       set_h(rcs);
-      ST_ACC(ST_STEP, t_q2)
-      ST_STAMP(t_q3)
       lq_solve();
-      ST_ACC(ST_SOLVE, t_q3)
-      ST_STAMP(t_q4)
 #pragma unroll
       for (int e = 0; e < 9; ++e) dvk[e] = s.u.q.dv[k][e];
       row_values(R, dvk, cdv);
@@ -814,34 +907,32 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
         for (int e = 0; e < 9; ++e) s.u.q.v[k][e] = vk[e] + alpha * dvk[e];
       }
       WSYNC();
-      ST_ACC(ST_STEP, t_q4)
     }
     it_total += it;
     it_max = max(it_max, it);
     all_conv = all_conv && conv;
     any_fail = any_fail || fail;
 
-    // ---------------- SQP update: ubar += dz ----------------
-    // w is projected onto its box: exact at a converged QP (|violation| <= tol_r), and it
-    // keeps a non-converged iterate (infeasible-start interior point) from leaving it
+    // ---------------- SQP update: ubar += dz (Fx, and the point mass's Fy, scaled by S) ----------------
     if (stl) {
       s.ub[k][0] += s.u.q.v[k][7] * S;
-      s.ub[k][1] = fmin(fmax(s.ub[k][1] + s.u.q.v[k][8], W.w_min), W.w_max);
+      if (pm) s.ub[k][1] += s.u.q.v[k][8] * S;
+      else s.ub[k][1] = fmin(fmax(s.ub[k][1] + s.u.q.v[k][8], W.w_min), W.w_max);
     }
     WSYNC();
   }
 
   // ---------------- outputs: u*, x* = rollout(u*), u0, status ----------------
   bool finite = true;
-  for (int e = l; e < 2 * N; e += WTH) {
+  for (int e = l; e < 2 * H; e += WTH) {
     const double v = s.ub[e >> 1][e & 1];
     finite = finite && isfinite(v);
-    A.u_out[(size_t)b * 2 * N + e] = v;
+    A.u_out[(size_t)b * 2 * H + e] = v;
   }
-  for (int e = l; e < 8 * N; e += WTH) {
+  for (int e = l; e < 8 * H; e += WTH) {
     const double v = s.xs[e >> 3][e & 7];
     finite = finite && isfinite(v);
-    A.x_out[(size_t)b * 8 * N + e] = v;
+    A.x_out[(size_t)b * 8 * H + e] = v;
   }
   finite = __all(finite ? 1 : 0) != 0;
   if (l < 2) A.u0[(size_t)b * 2 + l] = s.ub[0][l];
@@ -854,9 +945,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     A.iters[b] = it_total;
     if (A.diag) {
 #ifdef VC_TIMING
-      constexpr size_t DS = 4 + ST_NSLOT;
-      tacc[ST_TOTAL] = __builtin_amdgcn_s_memtime() - t_start;
-      for (int i = 0; i < ST_NSLOT; ++i) A.diag[(size_t)b * DS + 4 + i] = double(tacc[i]);
+      constexpr size_t DS = 4 + 9;
 #else
       constexpr size_t DS = 4;
 #endif
@@ -871,33 +960,29 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
 }  // namespace
 
 // ---- host launcher ---------------------------------------------------------------
-#define VC_ST_HORIZONS(X) X(20) X(30) X(40) X(50) X(60)
+// N = 20 single-track stages (cascaded.yaml) x the recorded tails M = 15, 25, 35, 40
+#define VC_CR_SHAPES(X) X(20, 15) X(20, 25) X(20, 35) X(20, 40)
 
-bool st_sqp_built(int N) {
-  switch (N) {
-#define VC_CASE(n) case n:
-    VC_ST_HORIZONS(VC_CASE)
+bool casc_ric_built(int N, int M) {
+#define VC_CASE(n, m) \
+  if (N == n && M == m) return true;
+  VC_CR_SHAPES(VC_CASE)
 #undef VC_CASE
-    return true;
-    default:
-      return false;
-  }
+  return false;
 }
 
-hipError_t launch_st_sqp(const StSqpArgs& a, int N, hipStream_t stream) {
+hipError_t launch_casc_ric(const CascSqpArgs& a, int N, int M, hipStream_t stream) {
   if (a.B <= 0) return hipSuccess;
   const bool lin = a.car.tyre == VC_TYRE_LINEAR;
-  switch (N) {
-#define VC_CASE(n)                                                                                          \
-  case n:                                                                                                  \
-    if (lin) hipLaunchKernelGGL((st_sqp_kernel<n, VC_TYRE_LINEAR>), dim3(a.B), dim3(WTH), 0, stream, a);  \
-    else hipLaunchKernelGGL((st_sqp_kernel<n, VC_TYRE_FIALA>), dim3(a.B), dim3(WTH), 0, stream, a);       \
-    return hipGetLastError();
-    VC_ST_HORIZONS(VC_CASE)
-#undef VC_CASE
-    default:
-      return hipErrorInvalidValue;
+#define VC_CASE(n, m)                                                                                         \
+  if (N == n && M == m) {                                                                                    \
+    if (lin) hipLaunchKernelGGL((casc_ric_kernel<n, m, VC_TYRE_LINEAR>), dim3(a.B), dim3(WTH), 0, stream, a); \
+    else hipLaunchKernelGGL((casc_ric_kernel<n, m, VC_TYRE_FIALA>), dim3(a.B), dim3(WTH), 0, stream, a);      \
+    return hipGetLastError();                                                                                \
   }
+  VC_CR_SHAPES(VC_CASE)
+#undef VC_CASE
+  return hipErrorInvalidValue;
 }
 
 }  // namespace vc

@@ -162,6 +162,10 @@ hipError_t launch_kin_ric(const KinLtvArgs& a, int N, hipStream_t stream);
 bool kin_ric_built(int N);
 hipError_t launch_dyn_sqp(const DynSqpArgs& a, int N, hipStream_t stream);
 hipError_t launch_casc_sqp(const CascSqpArgs& a, int N, int M, hipStream_t stream);
+// Stagewise-Riccati cascaded SQP step (casc_ric.hip): the same contract (CascSqpArgs.mode /
+// H_out / g_out are not read), N + M <= 64.
+hipError_t launch_casc_ric(const CascSqpArgs& a, int N, int M, hipStream_t stream);
+bool casc_ric_built(int N, int M);
 hipError_t launch_st_sqp(const StSqpArgs& a, int N, hipStream_t stream);
 bool st_sqp_built(int N);
 bool casc_sqp_built(int N, int M);

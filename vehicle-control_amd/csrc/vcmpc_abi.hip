@@ -142,8 +142,14 @@ bool dyn_solve_built(const vc_ctx* c) {
   if (c->dtype == VC_F32) return vc::dyn_sqp_smem_bytes(c->N) > 0;
   return vc::st_sqp_built(c->N);
 }
+// Cascaded: the stagewise Riccati kernel (casc_ric.hip; M = 15, 25, 35, 40) unless
+// qp.solver = 2 asks for the condensed one (casc_sqp.hip, M = 40).
+bool casc_stagewise(const vc_ctx* c) {
+  return c->p.qp.solver != 2 && vc::casc_ric_built(c->N, c->p.casc.horizon_pm);
+}
 bool casc_solve_built(const vc_ctx* c) {
-  return c->model == VC_MODEL_CASCADED && c->dtype == VC_F64 && vc::casc_sqp_built(c->N, c->p.casc.horizon_pm);
+  return c->model == VC_MODEL_CASCADED && c->dtype == VC_F64 &&
+         (casc_stagewise(c) || vc::casc_sqp_built(c->N, c->p.casc.horizon_pm));
 }
 
 // Cascaded single-track + point-mass SQP (casc_sqp.hip), fp64: arrays span H = N + M stages.
@@ -215,7 +221,8 @@ int casc_solve(vc_ctx* c, int B, const void* x0, const void* kappa, const void* 
     a.H_out = (double*)H_out;
     a.g_out = (double*)g_out;
   }
-  VC_HIP(c, vc::launch_casc_sqp(a, c->N, c->p.casc.horizon_pm, c->stream));
+  if (mode == 0 && casc_stagewise(c)) VC_HIP(c, vc::launch_casc_ric(a, c->N, c->p.casc.horizon_pm, c->stream));
+  else VC_HIP(c, vc::launch_casc_sqp(a, c->N, c->p.casc.horizon_pm, c->stream));
   if (flags == VC_HOST_PTRS) return unstage(c, slots);
   return 0;
 }
@@ -517,7 +524,9 @@ int vc_debug_stride(void) { return vc::dyn_sqp_debug_stride(); }
 int vc_condense(vc_ctx* c, int B, const void* x0, const void* ubar, const void* kappa, const void* ds, void* H,
                 void* g, int flags) {
   if (int r = check_common(c, B, flags)) return r;
-  if (!(kin_solve_built(c) && kin_condensed(c)) && !casc_solve_built(c))
+  const bool casc_cond = c->model == VC_MODEL_CASCADED && c->dtype == VC_F64 &&
+                         vc::casc_sqp_built(c->N, c->p.casc.horizon_pm);
+  if (!(kin_solve_built(c) && kin_condensed(c)) && !casc_cond)
     return fail(c, VC_E_UNSUPPORTED, "vc_condense: model=%d dtype=%d N=%d not built", c->model, c->dtype, c->N);
   if (!x0 || !kappa || !ds || !ubar || !H || !g) return fail(c, VC_E_ARG, "null pointer");
   if (B == 0) return 0;
