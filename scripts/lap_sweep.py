@@ -45,23 +45,26 @@ def lap(cfg, x0, steps, track, car):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=520)
+    ap.add_argument("--cascaded", action="store_true", help="the recorded cascaded laps (point-mass tail M)")
     args = ap.parse_args()
     from vcmpc.config import load_config
     from vcmpc.environment import Track
     from vcmpc.models import DynamicCar
     track = Track.load("ippodromo")
     car = DynamicCar(load_config("dynamic_car"), track, tyre="fiala")
+    ctl = "cascaded" if args.cascaded else "singletrack"
     with open(os.path.join(ROOT, "tests", "golden", "closed_loop_bands.json")) as f:
-        runs = [r for r in json.load(f)["runs"] if r["controller"] == "singletrack" and r["complete"]]
+        runs = [r for r in json.load(f)["runs"] if r["controller"] == ctl and r["complete"]]
     rec = {}
     for r in runs:
-        rec.setdefault((r["horizon"], r["max_speed"]), r)
-    for (N, vmax), r in sorted(rec.items()):
-        print(f"== N={N} vmax={vmax}: recorded steps={r['steps']} Ux_median={r['Ux_median']:.2f} "
+        rec.setdefault((r["horizon"], r["horizon_pm"], r["max_speed"]), r)
+    for (N, M, vmax), r in sorted(rec.items()):
+        print(f"== N={N} M={M} vmax={vmax}: recorded steps={r['steps']} Ux_median={r['Ux_median']:.2f} "
               f"Fx=[{r['Fx_min']:.0f},{r['Fx_max']:.0f}] |ey|max={r['ey_absmax']:.2f}", flush=True)
         for v in VARIANTS:
-            cfg = load_config("singletrack_mpc")
+            cfg = load_config("cascaded_mpc" if args.cascaded else "singletrack_mpc")
             cfg["horizon"] = N
+            cfg["horizon_pm"] = M
             cfg["state_constraints"]["max_speed"] = vmax
             cfg["qp"] = dict(cfg["qp"], **v)
             res = lap(cfg, r["x0"], args.steps, track, car)

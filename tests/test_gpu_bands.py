@@ -1,4 +1,4 @@
-"""GPU: closed-loop laps of the single-track NMPC against the reference's recorded laps
+"""GPU: closed-loop laps of the single-track and the cascaded NMPC against the reference's recorded laps
 ("closed-loop sanity bands"; fixture tests/golden/closed_loop_bands.json,
 made by tests/golden/make_st_bands.py from experiments/data/*_ippodromo).
 
@@ -33,17 +33,19 @@ LAP_REL = 0.03
 UX_MED_ABS = 0.3
 
 
-def _recorded():
+def _recorded(ctl="singletrack"):
     with open(os.path.join(GOLDEN, "closed_loop_bands.json")) as f:
         runs = json.load(f)["runs"]
     out = {}
     for r in runs:
-        if r["controller"] == "singletrack" and r["complete"]:
-            out.setdefault((r["horizon"], r["max_speed"]), r)
+        if r["controller"] == ctl and r["complete"]:
+            key = (r["horizon"], r["max_speed"]) if ctl == "singletrack" else (r["horizon_pm"], r["max_speed"])
+            out.setdefault(key, r)
     return out
 
 
 REC = _recorded()
+REC_CASC = _recorded("cascaded")
 
 
 @pytest.mark.parametrize("N,vmax", sorted(REC))
@@ -76,5 +78,43 @@ def test_singletrack_lap_within_recorded_bands(N, vmax):
     assert -7876 * 1.05 <= stats["Fx_min"] and stats["Fx_max"] <= 6055 * 1.05
     assert np.abs(Ul[:, 1]).max() <= 0.4 + 1e-9
     # on the track, or no further off it than the recorded lap (N = 50 / max_speed 20: 5.06 m)
+    assert stats["ey_absmax"] < max(track.width / 2, 1.1 * rec["ey_absmax"])
+    assert stats["nfail"] <= 1
+
+
+@pytest.mark.parametrize("M,vmax", sorted(REC_CASC))
+def test_cascaded_lap_within_recorded_bands(M, vmax):
+    """The reference's headline controller (CascadedMPC with a point-mass tail,
+    config/controllers/cascaded.yaml) on the device: N = 20 single-track + M point-mass stages
+    (csrc/casc_ric.hip, fp64, 5 SQP iterations per step -- the closed-loop setting of
+    singletrack_mpc.yaml), against every recorded cascaded lap config on ippodromo
+    (M = 15 / 25 / 35 / 40 x max_speed 18 .. 30; recorded 418 .. 432 steps)."""
+    from vcmpc.config import load_config
+    from vcmpc.environment import Track
+    from vcmpc.models import DynamicCar
+    from vcmpc.simulation import BatchedRacingSimulator
+    rec = REC_CASC[(M, vmax)]
+    track = Track.load("ippodromo")
+    cfg = load_config("cascaded_mpc")
+    cfg["horizon"], cfg["horizon_pm"] = rec["horizon"], M
+    cfg["state_constraints"]["max_speed"] = vmax
+    cfg["qp"] = dict(cfg["qp"], sqp_iters=5)
+    car = DynamicCar(load_config("dynamic_car"), track, tyre="fiala")
+    sim = BatchedRacingSimulator(car, cfg, track, batch=1)
+    K = int(rec["steps"] * (1 + 2 * LAP_REL))
+    out = sim.reset(np.array([rec["x0"]])).run(K)
+    X, U = out["state_traj"][:, 0], out["action_traj"][:, 0]
+    done = np.nonzero(X[:, 4] > track.length - 0.1)[0]
+    assert len(done), f"no lap in {K} steps: s = {X[-1, 4]:.1f} of {track.length:.1f}"
+    lap = int(done[0])
+    Xl, Ul = X[:lap], U[:lap]
+    stats = dict(steps=lap, Ux_median=float(np.median(Xl[:, 0])), Fx_min=float(Ul[:, 0].min()),
+                 Fx_max=float(Ul[:, 0].max()), ey_absmax=float(np.abs(Xl[:, 5]).max()), nfail=int(out["nfail"].sum()))
+    print(f"M={M} vmax={vmax}: build {stats} | recorded steps={rec['steps']} Ux_median={rec['Ux_median']:.2f} "
+          f"Fx=[{rec['Fx_min']:.0f},{rec['Fx_max']:.0f}] |ey|max={rec['ey_absmax']:.2f}")
+    assert abs(lap - rec["steps"]) <= LAP_REL * rec["steps"], (lap, rec["steps"])
+    assert abs(stats["Ux_median"] - rec["Ux_median"]) <= UX_MED_ABS
+    assert -7876 * 1.05 <= stats["Fx_min"] and stats["Fx_max"] <= 6055 * 1.05
+    assert np.abs(Ul[:, 1]).max() <= 0.4 + 1e-9
     assert stats["ey_absmax"] < max(track.width / 2, 1.1 * rec["ey_absmax"])
     assert stats["nfail"] <= 1

@@ -42,14 +42,15 @@ __global__ void track_k_kernel(TrackTable tt, int B, const T* s, T* k) {
 // _init_horizon.  XT is the type of x0 (double inside vc_simulate, where the kernel
 // also emits the context-dtype copy x0_out for the solve).
 template <typename T, typename XT, int MODEL>
-__global__ void horizon_kernel(TrackTable tt, int B, int N, const XT* x0, const T* xbar, double mpc_dt, T* kappa,
-                               T* ds, T* x0_out) {
+__global__ void horizon_kernel(TrackTable tt, int B, int N, int M, double ds_pm, const XT* x0, const T* xbar,
+                               double mpc_dt, T* kappa, T* ds, T* x0_out) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   constexpr int NX = MODEL == VC_MODEL_KINEMATIC ? KIN_NX : DYN_NX;
   constexpr int IS = MODEL == VC_MODEL_KINEMATIC ? 2 : 4;  // s  (kinematic_car.py:81, dynamic_car.py:209)
   constexpr int IV = 0;                                     // v / Ux
-  const int NS = MODEL == VC_MODEL_KINEMATIC ? N + 1 : N;
+  const int H = N + (MODEL == VC_MODEL_CASCADED ? M : 0);   // stages of the kappa / ds arrays
+  const int NS = MODEL == VC_MODEL_KINEMATIC ? N + 1 : H;
   const XT* xb0 = x0 + (size_t)b * NX;
   const double s0 = double(xb0[IS]);
   if (x0_out) {
@@ -57,8 +58,8 @@ __global__ void horizon_kernel(TrackTable tt, int B, int N, const XT* x0, const 
     for (int i = 0; i < NX; ++i) x0_out[(size_t)b * NX + i] = T(xb0[i]);
   }
   const T* xp = xbar + (size_t)b * NS * NX;
-  T* kap = kappa + (size_t)b * N;
-  T* dsb = ds + (size_t)b * N;
+  T* kap = kappa + (size_t)b * H;
+  T* dsb = ds + (size_t)b * H;
   if (MODEL == VC_MODEL_KINEMATIC) {
     // ds_traj = mpc_dt * v + 0.5 (N+1 values); ds = ds_traj[:N]; ds_traj[0] = 0;
     // s = cumsum(ds_traj) + s0; kappa = k(s[:N])   (kinematic_mpc.py:178-187)
@@ -83,6 +84,17 @@ __global__ void horizon_kernel(TrackTable tt, int B, int N, const XT* x0, const 
       }
       kap[k] = T(track_k(tt, (c - d0) + s0));
     }
+    if (MODEL == VC_MODEL_CASCADED) {
+      // point mass: ds = ds_pm, s = cumsum(ds_pm) - ds[N-1] + s_traj[N-1]  (cascaded_mpc.py:332-338)
+      const double d_last = mpc_dt * double(xp[(size_t)(N - 1) * NX + IV]);
+      const double s_last = (c - d0) + s0;
+      double cp = 0.0;
+      for (int j = 0; j < M; ++j) {
+        cp = cp + ds_pm;
+        dsb[N + j] = T(ds_pm);
+        kap[N + j] = T(track_k(tt, (cp - d_last) + s_last));
+      }
+    }
   }
 }
 
@@ -90,7 +102,8 @@ __global__ void horizon_kernel(TrackTable tt, int B, int N, const XT* x0, const 
 // closed-loop bookkeeping of vc_simulate (failure restart, logging).
 template <typename T, int MODEL>
 __global__ void drive_kernel(ModelArgs m, TrackTable tt, double* x64, const T* u0, double dt, T* x_ctx,
-                             const int32_t* status, T* xbar, T* ubar, int32_t* nfail, double* log_x, T* log_u) {
+                             const int32_t* status, T* xbar, T* ubar, int32_t* nfail, double* log_x, T* log_u,
+                             const T* kappa) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= m.B) return;
   constexpr int NX = MODEL == VC_MODEL_KINEMATIC ? KIN_NX : DYN_NX;
@@ -126,8 +139,18 @@ __global__ void drive_kernel(ModelArgs m, TrackTable tt, double* x64, const T* u
   }
   if (failed) {
     if (nfail) nfail[b] += 1;
-    const int N = m.N, NS = MODEL == VC_MODEL_KINEMATIC ? N + 1 : N;
-    for (int k = 0; k < N; ++k) ubar[((size_t)b * N + k) * 2] = ubar[((size_t)b * N + k) * 2 + 1] = T(0);
+    const int N = m.N, H = N + (MODEL == VC_MODEL_CASCADED ? m.M : 0), NS = MODEL == VC_MODEL_KINEMATIC ? N + 1 : H;
+    for (int k = 0; k < H; ++k) ubar[((size_t)b * H + k) * 2] = ubar[((size_t)b * H + k) * 2 + 1] = T(0);
+    if (MODEL == VC_MODEL_CASCADED && kappa) {
+      // the neutral point-mass tail (controllers/cascaded_mpc.py BatchedCascadedMPC._neutral):
+      // Fx = the drag at the current speed, Fy = m V^2 kappa (steady cornering)
+      const DynCoef<double>& c = m.dyn64;
+      const double V = fmax(sqrt(x[0] * x[0] + x[1] * x[1]), 3.0);
+      for (int k = N; k < H; ++k) {
+        ubar[((size_t)b * H + k) * 2] = T(c.Frr + c.Cd * (V * V));
+        ubar[((size_t)b * H + k) * 2 + 1] = T(c.m * (V * V) * double(kappa[(size_t)b * H + k]));
+      }
+    }
     for (int k = 0; k < NS; ++k)
 #pragma unroll
       for (int i = 0; i < NX; ++i) xbar[((size_t)b * NS + k) * NX + i] = T(xn[i]);
@@ -148,46 +171,49 @@ hipError_t launch_track_k(const TrackTable& tt, int dtype, int B, const void* s,
 }
 
 template <typename T, typename XT>
-hipError_t launch_horizon_t(const TrackTable& tt, int model, int B, int N, const void* x0, const void* xbar,
-                            double mpc_dt, void* kappa, void* ds, void* x0_out, hipStream_t st) {
-  if (model == VC_MODEL_KINEMATIC)
-    hipLaunchKernelGGL((horizon_kernel<T, XT, VC_MODEL_KINEMATIC>), grid1(B, 128), dim3(128), 0, st, tt, B, N,
-                       (const XT*)x0, (const T*)xbar, mpc_dt, (T*)kappa, (T*)ds, (T*)x0_out);
-  else
-    hipLaunchKernelGGL((horizon_kernel<T, XT, VC_MODEL_DYNAMIC>), grid1(B, 128), dim3(128), 0, st, tt, B, N,
-                       (const XT*)x0, (const T*)xbar, mpc_dt, (T*)kappa, (T*)ds, (T*)x0_out);
+hipError_t launch_horizon_t(const TrackTable& tt, int model, int B, int N, int M, double ds_pm, const void* x0,
+                            const void* xbar, double mpc_dt, void* kappa, void* ds, void* x0_out, hipStream_t st) {
+#define VC_HZ(MD)                                                                                                   \
+  hipLaunchKernelGGL((horizon_kernel<T, XT, MD>), grid1(B, 128), dim3(128), 0, st, tt, B, N, M, ds_pm, (const XT*)x0, \
+                     (const T*)xbar, mpc_dt, (T*)kappa, (T*)ds, (T*)x0_out)
+  if (model == VC_MODEL_KINEMATIC) VC_HZ(VC_MODEL_KINEMATIC);
+  else if (model == VC_MODEL_CASCADED) VC_HZ(VC_MODEL_CASCADED);
+  else VC_HZ(VC_MODEL_DYNAMIC);
+#undef VC_HZ
   return hipGetLastError();
 }
 
-hipError_t launch_horizon(const TrackTable& tt, int model, int dtype, int B, int N, const void* x0, bool x0_fp64,
-                          const void* xbar, double mpc_dt, void* kappa, void* ds, void* x0_out, hipStream_t st) {
+hipError_t launch_horizon(const TrackTable& tt, int model, int dtype, int B, int N, int M, double ds_pm,
+                          const void* x0, bool x0_fp64, const void* xbar, double mpc_dt, void* kappa, void* ds,
+                          void* x0_out, hipStream_t st) {
   if (B <= 0) return hipSuccess;
   if (dtype == VC_F32)
-    return x0_fp64 ? launch_horizon_t<float, double>(tt, model, B, N, x0, xbar, mpc_dt, kappa, ds, x0_out, st)
-                   : launch_horizon_t<float, float>(tt, model, B, N, x0, xbar, mpc_dt, kappa, ds, x0_out, st);
-  return launch_horizon_t<double, double>(tt, model, B, N, x0, xbar, mpc_dt, kappa, ds, x0_out, st);
+    return x0_fp64 ? launch_horizon_t<float, double>(tt, model, B, N, M, ds_pm, x0, xbar, mpc_dt, kappa, ds, x0_out, st)
+                   : launch_horizon_t<float, float>(tt, model, B, N, M, ds_pm, x0, xbar, mpc_dt, kappa, ds, x0_out, st);
+  return launch_horizon_t<double, double>(tt, model, B, N, M, ds_pm, x0, xbar, mpc_dt, kappa, ds, x0_out, st);
 }
 
 template <typename T>
 hipError_t launch_drive_t(const ModelArgs& m, const TrackTable& tt, double* x64, const void* u0, double dt,
                           void* x_ctx, const int32_t* status, void* xbar, void* ubar, int32_t* nfail, double* log_x,
-                          void* log_u, hipStream_t st) {
-  if (m.model == VC_MODEL_KINEMATIC)
-    hipLaunchKernelGGL((drive_kernel<T, VC_MODEL_KINEMATIC>), grid1(m.B, 128), dim3(128), 0, st, m, tt, x64,
-                       (const T*)u0, dt, (T*)x_ctx, status, (T*)xbar, (T*)ubar, nfail, log_x, (T*)log_u);
-  else
-    hipLaunchKernelGGL((drive_kernel<T, VC_MODEL_DYNAMIC>), grid1(m.B, 128), dim3(128), 0, st, m, tt, x64,
-                       (const T*)u0, dt, (T*)x_ctx, status, (T*)xbar, (T*)ubar, nfail, log_x, (T*)log_u);
+                          void* log_u, const void* kappa, hipStream_t st) {
+#define VC_DR(MD)                                                                                                   \
+  hipLaunchKernelGGL((drive_kernel<T, MD>), grid1(m.B, 128), dim3(128), 0, st, m, tt, x64, (const T*)u0, dt,      \
+                     (T*)x_ctx, status, (T*)xbar, (T*)ubar, nfail, log_x, (T*)log_u, (const T*)kappa)
+  if (m.model == VC_MODEL_KINEMATIC) VC_DR(VC_MODEL_KINEMATIC);
+  else if (m.model == VC_MODEL_CASCADED) VC_DR(VC_MODEL_CASCADED);
+  else VC_DR(VC_MODEL_DYNAMIC);
+#undef VC_DR
   return hipGetLastError();
 }
 
 hipError_t launch_drive(const ModelArgs& m, int dtype, const TrackTable& tt, double* x64, const void* u0, double dt,
                         void* x_ctx, const int32_t* status, void* xbar, void* ubar, int32_t* nfail, double* log_x,
-                        void* log_u, hipStream_t st) {
+                        void* log_u, const void* kappa, hipStream_t st) {
   if (m.B <= 0) return hipSuccess;
   return dtype == VC_F32
-             ? launch_drive_t<float>(m, tt, x64, u0, dt, x_ctx, status, xbar, ubar, nfail, log_x, log_u, st)
-             : launch_drive_t<double>(m, tt, x64, u0, dt, x_ctx, status, xbar, ubar, nfail, log_x, log_u, st);
+             ? launch_drive_t<float>(m, tt, x64, u0, dt, x_ctx, status, xbar, ubar, nfail, log_x, log_u, kappa, st)
+             : launch_drive_t<double>(m, tt, x64, u0, dt, x_ctx, status, xbar, ubar, nfail, log_x, log_u, kappa, st);
 }
 
 }  // namespace vc

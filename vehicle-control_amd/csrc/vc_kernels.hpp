@@ -130,6 +130,7 @@ struct CascSqpArgs {
 struct ModelArgs {
   int model;  // vc_model
   int B, N;
+  int M;      // point-mass stages of a cascaded context (0 otherwise)
   double L;   // kinematic wheelbase
   DynCoef<double> dyn64;
   DynCoef<float> dyn32;
@@ -150,11 +151,14 @@ struct TrackTable {
 };
 
 hipError_t launch_track_k(const TrackTable& tt, int dtype, int B, const void* s, void* k, hipStream_t st);
-hipError_t launch_horizon(const TrackTable& tt, int model, int dtype, int B, int N, const void* x0, bool x0_fp64,
-                          const void* xbar, double mpc_dt, void* kappa, void* ds, void* x0_out, hipStream_t st);
+// M, ds_pm: the point-mass tail of a cascaded context (M = 0 otherwise)
+hipError_t launch_horizon(const TrackTable& tt, int model, int dtype, int B, int N, int M, double ds_pm,
+                          const void* x0, bool x0_fp64, const void* xbar, double mpc_dt, void* kappa, void* ds,
+                          void* x0_out, hipStream_t st);
+// kappa: this step's horizon curvature (cascaded restart: the neutral point-mass tail), may be null
 hipError_t launch_drive(const ModelArgs& m, int dtype, const TrackTable& tt, double* x64, const void* u0, double dt,
                         void* x_ctx, const int32_t* status, void* xbar, void* ubar, int32_t* nfail, double* log_x,
-                        void* log_u, hipStream_t st);
+                        void* log_u, const void* kappa, hipStream_t st);
 hipError_t launch_kin_ltv(const KinLtvArgs& a, int N, hipStream_t stream);
 // Stagewise-Riccati kinematic LTV-MPC step (kin_ric.hip): the same contract, any built N
 // (KinLtvArgs.mode / H_out / g_out are not read).

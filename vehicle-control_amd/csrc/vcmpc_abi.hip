@@ -119,13 +119,17 @@ vc::ModelArgs model_args(const vc_ctx* c, int B) {
   m.model = c->model;
   m.B = B;
   m.N = c->N;
+  m.M = c->model == VC_MODEL_CASCADED ? c->p.casc.horizon_pm : 0;
   m.L = c->p.kin_car.l;
   m.dyn64 = vc::make_dyn_coef<double>(c->p.dyn_car);
   m.dyn32 = vc::make_dyn_coef<float>(c->p.dyn_car);
   return m;
 }
 
-int ns_of(const vc_ctx* c) { return c->model == VC_MODEL_KINEMATIC ? c->N + 1 : c->N; }
+// stages of the solve arrays: kappa / ds / ubar span H (= N, or N + horizon_pm for a
+// cascaded context); xbar has N + 1 (kinematic) or H state columns
+int nh_of(const vc_ctx* c) { return c->N + (c->model == VC_MODEL_CASCADED ? c->p.casc.horizon_pm : 0); }
+int ns_of(const vc_ctx* c) { return c->model == VC_MODEL_KINEMATIC ? c->N + 1 : nh_of(c); }
 size_t al256(size_t b) { return (b + 255) & ~size_t(255); }
 vc::TrackTable track_table(const vc_ctx* c) {
   return vc::TrackTable{static_cast<const double*>(c->track), c->track_n, c->track_h, c->track_len};
@@ -702,23 +706,22 @@ int vc_horizon(vc_ctx* c, int B, const void* x0, const void* xbar, double mpc_dt
   if (int r = check_common(c, B, flags)) return r;
   if (!x0 || !xbar || !kappa || !ds) return fail(c, VC_E_ARG, "null pointer");
   if (!c->track) return fail(c, VC_E_ARG, "vc_horizon: no track table (vc_track_set)");
-  if (c->model == VC_MODEL_CASCADED)
-    return fail(c, VC_E_UNSUPPORTED, "vc_horizon: cascaded contexts build their horizon on the host");
   if (B == 0) return 0;
-  const int N = c->N, nx = nx_of(c), NS = ns_of(c);
+  const int N = c->N, nx = nx_of(c), NS = ns_of(c), NH = nh_of(c), M = NH - N;
+  const double ds_pm = c->p.casc.ds_pm;
   const size_t es = esize(c);
   if (flags == VC_HOST_PTRS) {
     std::vector<Slot> slots = {{x0, nullptr, (size_t)B * nx * es, nullptr},
                                {xbar, nullptr, (size_t)B * NS * nx * es, nullptr},
-                               {nullptr, kappa, (size_t)B * N * es, nullptr},
-                               {nullptr, ds, (size_t)B * N * es, nullptr}};
+                               {nullptr, kappa, (size_t)B * NH * es, nullptr},
+                               {nullptr, ds, (size_t)B * NH * es, nullptr}};
     if (int r = stage(c, slots)) return r;
-    VC_HIP(c, vc::launch_horizon(track_table(c), c->model, c->dtype, B, N, slots[0].dev, c->dtype == VC_F64,
+    VC_HIP(c, vc::launch_horizon(track_table(c), c->model, c->dtype, B, N, M, ds_pm, slots[0].dev, c->dtype == VC_F64,
                                  slots[1].dev, mpc_dt, slots[2].dev, slots[3].dev, nullptr, c->stream));
     return unstage(c, slots);
   }
-  VC_HIP(c, vc::launch_horizon(track_table(c), c->model, c->dtype, B, N, x0, c->dtype == VC_F64, xbar, mpc_dt, kappa,
-                               ds, nullptr, c->stream));
+  VC_HIP(c, vc::launch_horizon(track_table(c), c->model, c->dtype, B, N, M, ds_pm, x0, c->dtype == VC_F64, xbar,
+                               mpc_dt, kappa, ds, nullptr, c->stream));
   return 0;
 }
 
@@ -737,11 +740,11 @@ int vc_drive(vc_ctx* c, int B, double* x64, const void* u0, double dt, void* x_c
     if (int r = stage(c, slots)) return r;
     VC_HIP(c, vc::launch_drive(m, c->dtype, track_table(c), (double*)slots[0].dev, slots[1].dev, dt,
                                x_ctx ? slots[2].dev : nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-                               c->stream));
+                               nullptr, c->stream));
     return unstage(c, slots);
   }
   VC_HIP(c, vc::launch_drive(m, c->dtype, track_table(c), x64, u0, dt, x_ctx, nullptr, nullptr, nullptr, nullptr,
-                             nullptr, nullptr, c->stream));
+                             nullptr, nullptr, nullptr, c->stream));
   return 0;
 }
 
@@ -751,11 +754,12 @@ int vc_simulate(vc_ctx* c, int B, int steps, double mpc_dt, double dt, double* x
   if (!x64 || !xbar || !ubar) return fail(c, VC_E_ARG, "null pointer");
   if (steps < 0) return fail(c, VC_E_ARG, "steps %d < 0", steps);
   if (!c->track) return fail(c, VC_E_ARG, "vc_simulate: no track table (vc_track_set)");
-  if (!kin_solve_built(c) && !dyn_solve_built(c))
+  if (!kin_solve_built(c) && !dyn_solve_built(c) && !casc_solve_built(c))
     return fail(c, VC_E_UNSUPPORTED, "vc_simulate: model=%d dtype=%d N=%d has no built vc_solve", c->model, c->dtype,
                 c->N);
   if (B == 0 || steps == 0) return 0;
-  const int N = c->N, nx = nx_of(c), NS = ns_of(c);
+  const int N = c->N, nx = nx_of(c), NS = ns_of(c), NH = nh_of(c), M = NH - N;
+  const double ds_pm = c->p.casc.ds_pm;
   const size_t es = esize(c);
   std::vector<Slot> slots;
   double* dx = x64;
@@ -765,7 +769,7 @@ int vc_simulate(vc_ctx* c, int B, int steps, double mpc_dt, double dt, double* x
   if (flags == VC_HOST_PTRS) {
     slots = {{x64, x64, (size_t)B * nx * 8, nullptr},
              {xbar, xbar, (size_t)B * NS * nx * es, nullptr},
-             {ubar, ubar, (size_t)B * N * 2 * es, nullptr},
+             {ubar, ubar, (size_t)B * NH * 2 * es, nullptr},
              {nullptr, log_x, log_x ? (size_t)(steps + 1) * B * nx * 8 : 0, nullptr},
              {nullptr, log_u, log_u ? (size_t)steps * B * 2 * es : 0, nullptr},
              {nfail, nfail, nfail ? (size_t)B * 4 : 0, nullptr}};
@@ -777,8 +781,8 @@ int vc_simulate(vc_ctx* c, int B, int steps, double mpc_dt, double dt, double* x
     dlu = log_u ? slots[4].dev : nullptr;
     dnf = nfail ? (int32_t*)slots[5].dev : nullptr;
   }
-  // scratch: kappa[B][N], ds[B][N], x[B][nx], u0[B][2] (context dtype), status[B], iters[B]
-  const size_t o_kap = 0, o_ds = o_kap + al256((size_t)B * N * es), o_x = o_ds + al256((size_t)B * N * es),
+  // scratch: kappa[B][NH], ds[B][NH], x[B][nx], u0[B][2] (context dtype), status[B], iters[B]
+  const size_t o_kap = 0, o_ds = o_kap + al256((size_t)B * NH * es), o_x = o_ds + al256((size_t)B * NH * es),
                o_u0 = o_x + al256((size_t)B * nx * es), o_st = o_u0 + al256((size_t)B * 2 * es),
                o_it = o_st + al256((size_t)B * 4), total = o_it + al256((size_t)B * 4);
   if (total > c->sim_bytes) {
@@ -796,11 +800,12 @@ int vc_simulate(vc_ctx* c, int B, int steps, double mpc_dt, double dt, double* x
   vc::ModelArgs m = model_args(c, B);
   if (dlx) VC_HIP(c, hipMemcpyAsync(dlx, dx, (size_t)B * nx * 8, hipMemcpyDeviceToDevice, c->stream));
   for (int step = 0; step < steps; ++step) {
-    VC_HIP(c, vc::launch_horizon(tt, c->model, c->dtype, B, N, dx, true, dxbar, mpc_dt, kap, dsv, xc, c->stream));
+    VC_HIP(c, vc::launch_horizon(tt, c->model, c->dtype, B, N, M, ds_pm, dx, true, dxbar, mpc_dt, kap, dsv, xc,
+                                 c->stream));
     if (int r = vc_solve_diag(c, B, xc, kap, dsv, dxbar, dubar, u0, st, it, nullptr, VC_DEVICE_PTRS)) return r;
     VC_HIP(c, vc::launch_drive(m, c->dtype, tt, dx, u0, dt, nullptr, st, dxbar, dubar, dnf,
                                dlx ? dlx + (size_t)(step + 1) * B * nx : nullptr,
-                               dlu ? (char*)dlu + (size_t)step * B * 2 * es : nullptr, c->stream));
+                               dlu ? (char*)dlu + (size_t)step * B * 2 * es : nullptr, kap, c->stream));
   }
   if (flags == VC_HOST_PTRS) return unstage(c, slots);
   return 0;

@@ -38,7 +38,8 @@ class BatchedRacingSimulator:
 
     ``car`` is a ``KinematicCar`` or ``DynamicCar`` (its config and tyre are used),
     ``controller_config`` the matching controller yaml (``kinematic_mpc`` /
-    ``dynamic_mpc``), ``track`` a ``vcmpc.environment.Track``.  ``dtype`` picks the
+    ``dynamic_mpc`` / ``singletrack_mpc`` / ``cascaded_mpc``: a ``horizon_pm > 0`` config runs
+    the cascaded NMPC with its point-mass tail), ``track`` a ``vcmpc.environment.Track``.  ``dtype`` picks the
     dynamic solve precision (default fp64 where the fp64 kernel is built for N).  Buffers live on
     ``cuda:<device>`` as torch tensors when torch is importable (the fast path),
     else in host numpy arrays staged by every call."""
@@ -46,21 +47,25 @@ class BatchedRacingSimulator:
     def __init__(self, car, controller_config, track, batch: int, device: int = 0, seed: int | None = 31,
                  use_torch: bool = True, dtype: int | None = None):
         cfg = controller_config
-        if int(cfg.get("horizon_pm", 0)) > 0:
-            raise NotImplementedError("the cascaded point-mass tail (cascaded_mpc.py:181-277) is SURVEY 8(f) row 3")
         self.car, self.config, self.track = car, cfg, track
         self.dynamic = _is_dynamic(car)
         self.B, self.N = int(batch), int(cfg["horizon"])
+        # the cascaded controller's point-mass tail (cascaded_mpc.py:181-338): arrays over H stages
+        self.M = int(cfg.get("horizon_pm", 0) or 0) if self.dynamic else 0
+        self.H = self.N + self.M
         self.mpc_dt = float(cfg["mpc_dt"])
         self.dt = float(car.dt)
         if self.dynamic:
             params = make_params(dyn_car=car.config, dyn_mpc=cfg, tyre=getattr(car, "tyre", "fiala"),
                                  obstacles=obstacle_list(track, cfg))
-            # fp64 (csrc/st_sqp.hip, the reference's own precision) where it is built, else
-            # the fp32 condensed kernel (csrc/dyn_sqp.hip, N = 40)
-            model = _abi.VC_MODEL_DYNAMIC
-            if dtype is None:
-                dtype = _abi.VC_F64 if self.N in ST_SQP_HORIZONS else _abi.VC_F32
+            if self.M > 0:  # cascaded SQP, fp64 (csrc/casc_ric.hip)
+                model, dtype = _abi.VC_MODEL_CASCADED, _abi.VC_F64
+            else:
+                # fp64 (csrc/st_sqp.hip, the reference's own precision) where it is built, else
+                # the fp32 condensed kernel (csrc/dyn_sqp.hip, N = 40)
+                model = _abi.VC_MODEL_DYNAMIC
+                if dtype is None:
+                    dtype = _abi.VC_F64 if self.N in ST_SQP_HORIZONS else _abi.VC_F32
         else:
             # the kinematic controller's real-time-iteration trust region (controllers/
             # kinematic_mpc.py RTI_TRUST) unless the config's qp block sets its own
@@ -105,17 +110,18 @@ class BatchedRacingSimulator:
         and cascaded_mpc.py:72-76 (ones, Ux + 3); actions 1 + U[0, 1), projected onto
         the input box (see controllers/*.py)."""
         rng = np.random.RandomState(seed) if seed is not None else np.random
-        B, N, ns, nx = self.B, self.N, self.ns, self.nx
+        B, N, H, ns, nx = self.B, self.N, self.H, self.ns, self.nx
         ic = self.config["input_constraints"]
         if self.dynamic:
             xbar = np.ones((B, ns, nx))
-            xbar[..., IUX] += 3
+            xbar[:, :N, IUX] += 3
         else:
             xbar = np.zeros((B, ns, nx))
             xbar[..., IV_KIN] += 0.1
-        ubar = np.ones((B, N, 2)) + np.swapaxes(rng.random_sample((B, 2, N)), 1, 2)
+        ubar = np.ones((B, H, 2)) + np.swapaxes(rng.random_sample((B, 2, H)), 1, 2)
         if self.dynamic:
-            np.clip(ubar[..., 1], ic["w_min"], ic["w_max"], out=ubar[..., 1])
+            np.clip(ubar[:, :N, 1], ic["w_min"], ic["w_max"], out=ubar[:, :N, 1])
+            self._fresh_tail = self.M > 0  # the point-mass tail gets the neutral guess at reset()
         else:
             np.clip(ubar[..., 0], ic["a_min"], ic["a_max"], out=ubar[..., 0])
             np.clip(ubar[..., 1], ic["w_min"], ic["w_max"], out=ubar[..., 1])
@@ -123,9 +129,26 @@ class BatchedRacingSimulator:
         self.ubar = self._to_dev(ubar.astype(self.np_dtype))
 
     def reset(self, states):
-        """Set the B plant states (fp64 [B, nx], reference FancyVector order)."""
+        """Set the B plant states (fp64 [B, nx], reference FancyVector order).  A cascaded
+        controller's point-mass tail starts from the neutral guess of
+        controllers/cascaded_mpc.py (BatchedCascadedMPC._neutral: drag-level Fx, Fy = m V^2
+        kappa), as the host controller does -- the reference's random first guess would roll
+        the tail off the track in every corner."""
         states = np.asarray(states, np.float64).reshape(self.B, self.nx)
         self.x = self._to_dev(states)
+        if getattr(self, "_fresh_tail", False):
+            from .controllers.cascaded_mpc import casc_horizon_params
+            xb = self._to_host(self.xbar)
+            ds, kappa = casc_horizon_params(states[:, IS_DYN], xb[:, :, IUX], self.mpc_dt, self.N, self.M,
+                                            float(self.config["ds_pm"]), self.track.k)
+            car = self.car.config
+            m, Frr, Cd = float(car["car"]["m"]), float(car["env"]["Frr"]), float(car["env"]["Cd"])
+            V = np.maximum(np.hypot(states[:, 0], states[:, 1]), 3.0)[:, None]
+            ub = self._to_host(self.ubar).copy()
+            ub[:, self.N:, 0] = Frr + Cd * V ** 2
+            ub[:, self.N:, 1] = m * V ** 2 * kappa[:, self.N:]
+            self.ubar = self._to_dev(ub.astype(self.np_dtype))
+            self._fresh_tail = False
         return self
 
     # -- loop ---------------------------------------------------------------------------

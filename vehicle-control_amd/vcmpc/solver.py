@@ -229,7 +229,7 @@ class Context:
     def horizon(self, x0, xbar, mpc_dt):
         """``_init_horizon`` on the device: (kappa[B, N], ds[B, N]) from the state and
         the unshifted warm start xbar[B, NS, nx]."""
-        B, N, nx, f = self._batch(x0), self.N, self.nx, _NP_DT[self.dtype]
+        B, N, nx, f = self._batch(x0), self.NH, self.nx, _NP_DT[self.dtype]
         kappa, ds = self._like(x0, (B, N)), self._like(x0, (B, N))
         ptrs, flags = self._marshal([x0, xbar, kappa, ds], [(B, nx), (B, self.ns_solve, nx), (B, N), (B, N)], [f] * 4)
         self._check(self.lib.vc_horizon(self._h, B, ptrs[0], ptrs[1], float(mpc_dt), ptrs[2], ptrs[3], flags))
@@ -251,7 +251,7 @@ class Context:
         """``vc_simulate``: ``steps`` closed-loop steps (horizon -> solve -> drive) on the
         device.  x64, xbar, ubar are updated in place.  With ``log=True`` returns
         (log_x[steps+1, B, nx] fp64, log_u[steps, B, nu], nfail[B]); else (None, None, nfail)."""
-        B, N, nx, f = self._batch(x64), self.N, self.nx, _NP_DT[self.dtype]
+        B, N, nx, f = self._batch(x64), self.NH, self.nx, _NP_DT[self.dtype]
         steps = int(steps)
         dev = _is_torch(x64)
         if nfail is None:
