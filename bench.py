@@ -51,7 +51,7 @@ FLOP_ITER = (2 * N_DEC * sum(2 * (1 + r % (N_HORIZON - 1)) for r in range(NC_ROW
              + N_DEC ** 3 // 3 + 2 * 2 * N_DEC * N_DEC                                  # Cholesky, 2 solves
              + 4 * (2 * NC_ROWS * N_DEC) + 2 * 2 * N_DEC * N_DEC)                       # mat-vecs
 FP64_VALU_PEAK = 78.6  # TFLOP/s
-PMC_PROFILE = os.path.join(ROOT, "profiles", "r01", "pmc_b1024.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02", "pmc_summary.json")
 
 # ---- C3: dynamic single-track SQP (fp32, N = 40) ------------------------------------
 C3_N, C3_NX = 40, 8
@@ -98,17 +98,16 @@ def c3_flops(pdip_iters_total, sqp_iters=3, polish_rounds=2):
             + C3_N * 4 * 300)
 
 
-def pmc_traffic(batch):
+def pmc_traffic(batch, kernel="kin_ltv_kernel<20>"):
     """HBM bytes per launch from the committed rocprofv3 PMC passes (FETCH_SIZE +
-    WRITE_SIZE, scripts/pmc_profile.sh) when they were taken at this batch."""
+    WRITE_SIZE, scripts/pmc_profile.sh -> scripts/pmc_summary.py) when they were taken at
+    this batch (one 64-lane workgroup per problem: grid = 64 B threads)."""
     try:
-        with open(PMC_PROFILE) as f:
+        with open(PMC_SUMMARY) as f:
             p = json.load(f)
-    except (OSError, ValueError):
+        return p[f"{kernel} grid={64 * batch}"]["derived"]["traffic_bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
         return None
-    if p.get("batch") != batch:
-        return None
-    return p["derived"]["traffic_bytes_per_launch"]
 
 
 def parse():
@@ -162,7 +161,8 @@ def cpu_baseline(batch, sample):
         pass
     return {"value": len(d["x0"]) / dt, "unit": "solves/s", "cores": 1, "kind": "port",
             "sample": f"{len(d['x0'])} problems of the C2 workload, one oracle pass (PDIP + active-set polish, "
-                      f"numpy fp64, 1 thread) in {dt:.2f} s on {cpu}"}
+                      f"numpy fp64, 1 thread) in {dt:.2f} s on {cpu}; a stand-in for the reference's "
+                      f"CasADi/IPOPT path, which cannot run here"}
 
 
 def _oracle_chunk(chunk):
@@ -197,8 +197,11 @@ def cpu_baseline_all_cores(batch, sample, workers=16):
         done = sum(pool.map(_oracle_chunk, chunks, chunksize=1))
         dt = time.perf_counter() - t0
     return {"value": done / dt, "unit": "solves/s", "cores": len(chunks), "kind": "port",
+            "host_cpus_visible": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
             "sample": f"{int(done)} problems of the C2 workload split over {len(chunks)} single-threaded "
-                      f"oracle processes, {dt:.2f} s wall"}
+                      f"oracle processes, {dt:.2f} s wall (the batched numpy oracle stands in for the "
+                      f"reference's CasADi/IPOPT path, which cannot run here; {len(chunks)} = this pool's "
+                      f"CPU share per GPU, the machine shows {os.cpu_count()} CPUs)"}
 
 
 def cpu_baseline_c3(data, sample):
@@ -783,9 +786,12 @@ def main():
             "roofline": {"bound": "mfma", "achieved": flops * B / (kern_ms / 1e3) / 1e12, "peak": FP64_VALU_PEAK,
                          "unit": "TFLOP/s", "frac": flops * B / (kern_ms / 1e3) / 1e12 / FP64_VALU_PEAK,
                          "traffic": pmc_traffic(B),
-                         "traffic_unit": "HBM bytes/launch (rocprofv3 FETCH_SIZE+WRITE_SIZE, profiles/r01)",
+                         "traffic_unit": "HBM bytes/launch (rocprofv3 FETCH_SIZE+WRITE_SIZE, profiles/r02/pmc_summary.json)",
                          "kernel": "kin_ltv_kernel<20>", "kernel_ms": kern_ms, "flops_per_solve": flops,
                          "flops_note": "algorithmic fp64 FLOPs: sweep + (IPM iterations + 1 polish) x iteration",
+                         # SURVEY 8(d)'s dense count F = 0.42 M + iterations x 0.28 M (the VERDICT's basis)
+                         "frac_survey_F": (0.42e6 + (float(it.mean()) + 1.0) * 0.28e6) * B / (kern_ms / 1e3) / 1e12
+                                          / FP64_VALU_PEAK,
                          "hbm": {"achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                  "frac": achieved / HBM_PEAK_GBS, "algorithmic_bytes": BYTES_PER_SOLVE * B,
                                  "bytes_per_solve": BYTES_PER_SOLVE}},

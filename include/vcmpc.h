@@ -119,8 +119,11 @@ typedef struct vc_qp {
   double trust_w;   /* trust region |u_w - ubar_w| <= trust_w (0 = off) */
   int32_t max_iter; /* interior-point iteration cap */
   int32_t polish;   /* active-set polish rounds after the interior point (0 = off) */
-  int32_t solver;   /* kinematic solve kernel: 0 = condensed (kin_ltv.hip) where built (N = 20),
-                       else stagewise Riccati (kin_ric.hip); 1 = stagewise Riccati always */
+  int32_t solver;   /* solve-kernel choice (ABI 5).  Kinematic: 0 = condensed (kin_ltv.hip) where
+                       built (N = 20), else stagewise Riccati (kin_ric.hip); 1 = stagewise
+                       Riccati always.  Cascaded: 0 / 1 = stagewise Riccati (casc_ric.hip),
+                       2 = condensed (casc_sqp.hip, M = 40 only).  Single-track: the dtype
+                       picks the kernel (VC_F32: dyn_sqp.hip, VC_F64: st_sqp.hip). */
   int32_t pad_;
 } vc_qp;
 
@@ -165,11 +168,17 @@ int vc_params_sizeof(void);
 
 /* Create a solve context on `device` for `model` with horizon N and workspace for
  * up to max_batch problems.  Returns NULL on failure (reason: vc_last_error(NULL)).
- * Built combinations: (VC_MODEL_KINEMATIC, VC_F64, N = 20) for vc_solve /
- * vc_condense; (VC_MODEL_DYNAMIC, VC_F32, N = 40) for vc_solve (sequential QP);
- * (VC_MODEL_CASCADED, VC_F64, N = 20 single-track stages, casc.horizon_pm = 40) for
- * vc_solve / vc_condense, whose arrays span H = N + horizon_pm stages;
- * every N >= 1 for vc_rollout / vc_linearize / vc_plant_step / vc_spatial_step. */
+ * Built combinations for vc_solve (and vc_horizon / vc_simulate):
+ *   (VC_MODEL_KINEMATIC, VC_F64, N = 20) condensed (kin_ltv.hip; also vc_condense) and
+ *     N = 10, 20, 30, 40, 50, 60 stagewise Riccati (kin_ric.hip; kinematic.yaml N = 50);
+ *   (VC_MODEL_DYNAMIC, VC_F64, N = 20, 30, 40, 50, 60) single-track SQP, stagewise Riccati
+ *     (st_sqp.hip; singletrack.yaml N = 60, recorded N = 50); (VC_MODEL_DYNAMIC, VC_F32,
+ *     N = 40) the condensed fp32 SQP (dyn_sqp.hip, BASELINE config 3);
+ *   (VC_MODEL_CASCADED, VC_F64, N = 20 single-track stages, casc.horizon_pm = 15, 25, 35,
+ *     40) stagewise Riccati (casc_ric.hip), horizon_pm = 40 also condensed (casc_sqp.hip,
+ *     vc_condense); the arrays span H = N + horizon_pm stages.
+ * Other combinations create a context whose vc_solve returns VC_E_UNSUPPORTED.
+ * vc_rollout / vc_linearize / vc_plant_step / vc_spatial_step: every N >= 1. */
 vc_ctx* vc_create(int device, int model, int N, int max_batch, int dtype, const vc_params* params);
 void vc_destroy(vc_ctx* ctx);
 const char* vc_last_error(const vc_ctx* ctx);

@@ -364,10 +364,37 @@ def test_batched_simulator_laps_ippodromo(tracks):
     assert np.isfinite(X).all() and np.isfinite(U).all()
     assert out["nfail"].sum() <= 0.01 * B * K, out["nfail"].sum()
     on_track = (np.abs(X[:, :, 5]) < pt.width / 2).all(axis=0)
-    assert on_track.mean() >= 0.99, on_track.mean()
+    assert on_track.all(), on_track.mean()   # fp64 solve (st_sqp): every vehicle (round 1 fp32: >= 99 %)
     progress = X[-1, :, 4] - X[0, :, 4]
     assert np.median(progress) > K * DT * 8.0
     assert np.abs(U[..., 1]).max() <= 0.4 + 1e-4
     # a second run continues from the stored state and warm starts
     out2 = sim.run(5)
     np.testing.assert_array_equal(out2["state_traj"][0], X[-1])
+
+
+def test_c5_divergent_vehicles_stay_on_track(tracks):
+    """Regression for round 1's C5 divergence: the four vehicles (ids 801, 2640, 5936, 5986
+    of the bench's 8,192) that left the track at |ey| ~ 240 m under the fp32 solve (non-finite
+    solves from their first step, scripts/c5_divergence.py, fixture c5_divergent_x0.npz).
+    The full 500-step C5 job for them, through the fp64 closed loop: on track throughout,
+    max |ey| < 4.5 m (the bench criterion), and lap progress."""
+    import os
+    from conftest import GOLDEN
+    from vcmpc.config import load_config
+    from vcmpc.models import DynamicCar
+    from vcmpc.simulation import BatchedRacingSimulator
+    pt, _ = tracks
+    x0 = np.load(os.path.join(GOLDEN, "c5_divergent_x0.npz"))["x0"]
+    car = DynamicCar(load_config("dynamic_car"), pt, tyre="fiala")
+    cfg = load_config("dynamic_mpc")
+    cfg["mpc_dt"] = C5_MPC_DT
+    sim = BatchedRacingSimulator(car, cfg, pt, batch=len(x0))
+    out = sim.reset(x0.copy()).run(500)
+    X = out["state_traj"]
+    ey = np.abs(X[:, :, 5]).max(axis=0)
+    print("max |ey| per vehicle:", ey, "non-solved steps:", out["nfail"].sum(axis=0) if out["nfail"].ndim > 1
+          else out["nfail"])
+    assert np.isfinite(X).all()
+    assert (ey < 4.5).all(), ey
+    assert (X[-1, :, 4] - X[0, :, 4] > 250.0).all()

@@ -17,7 +17,7 @@ kernel of BASELINE config 3 (csrc/dyn_sqp.hip, N = 40, ``dtype="f32"``); contrac
 oracle/dyn_sqp.py.  ``BatchedSingleTrackMPC`` is the same controller for B
 vehicles at once.  With ``horizon_pm > 0`` (the cascaded point-mass tail,
 cascaded_mpc.py:181-277) ``CascadedMPC`` / ``BatchedCascadedMPC`` run the fp64 cascaded
-SQP (csrc/casc_sqp.hip, contract oracle/casc_sqp.py); obstacle barrier terms
+SQP (csrc/casc_ric.hip, stagewise Riccati; the condensed csrc/casc_sqp.hip with qp.solver = 2; contract oracle/casc_sqp.py); obstacle barrier terms
 (`obstacles: True`, cascaded_mpc.py:173-176) enter each QP as in DESIGN.md 2c.
 """
 from __future__ import annotations
@@ -122,7 +122,7 @@ def casc_horizon_params(s0, ux_pred, mpc_dt, N, M, ds_pm, k_of_s):
 
 class BatchedCascadedMPC(Controller):
     """B independent cascaded NMPCs (single track N + point mass M = horizon_pm stages)
-    solved in one launch (csrc/casc_sqp.hip, fp64; contract oracle/casc_sqp.py)."""
+    solved in one launch (csrc/casc_ric.hip, fp64; contract oracle/casc_sqp.py)."""
 
     def __init__(self, car, config, batch: int, device: int = 0, seed: int | None = 31):
         Controller.__init__(self)
@@ -195,7 +195,7 @@ class CascadedMPC(BatchedSingleTrackMPC):
     """Single-vehicle drop-in for ``CascadedMPC(car, point_mass, config)`` (cascaded_mpc.py:16-39).
     ``horizon_pm: 0`` runs the single-track SQP (fp64 csrc/st_sqp.hip by default, fp32
     csrc/dyn_sqp.hip with ``dtype="f32"``); ``horizon_pm > 0``
-    returns a :class:`CascadedTailMPC` (point-mass tail, csrc/casc_sqp.hip, fp64)."""
+    returns a :class:`CascadedTailMPC` (point-mass tail, csrc/casc_ric.hip, fp64)."""
 
     def __new__(cls, car, point_mass, config, device: int = 0, dtype: str = "f64"):
         if cls is CascadedMPC and int(config.get("horizon_pm", 0) or 0) > 0:
