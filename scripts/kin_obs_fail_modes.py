@@ -1,0 +1,115 @@
+"""Why does the kinematic closed loop with obstacles end steps non-solved and hit obstacles?
+Runs the loop of tests/test_gpu_obstacles.py::test_kinematic_closed_loop_with_obstacles (64
+vehicles, 400 steps, ippodromo's obstacle field) one step at a time and, for a sample of the
+non-solved steps, re-solves the QP with the oracle (same x0, warm start, horizon parameters,
+obstacle model) to classify it: infeasible linearised QP (primal residual) or a solver
+failure on a feasible one.  Also reports when the non-solved steps happen (first step, near
+an obstacle, elsewhere) and each collision's step and preceding failures.
+
+    python scripts/kin_obs_fail_modes.py [--steps 400] [--sample 40] [--warm zeros|reference]
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "vehicle-control_amd")]
+
+from oracle import ltv_qp as Q  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--sample", type=int, default=40)
+    ap.add_argument("--warm", default="reference", help="initial warm start: the reference's 1 + U[0,1) or zeros")
+    ap.add_argument("--trust", default="rti", help="rti (1.0 / 0.1) or off")
+    ap.add_argument("--no-obstacles", action="store_true", help="the same loop without the barrier terms")
+    ap.add_argument("--horizon", type=int, default=0, help="override the config's N (kin_ric above 20)")
+    args = ap.parse_args()
+    from vcmpc.config import load_config
+    from vcmpc.controllers.kinematic_mpc import RTI_TRUST
+    from vcmpc.environment import Track
+    from vcmpc.models import KinematicCar
+    from vcmpc.simulation import BatchedRacingSimulator
+    tr = Track.load("ippodromo")
+    obs = [(o.s, o.ey, o.radius) for o in tr.obstacles]
+    B, K = 64, args.steps
+    rng = np.random.default_rng(3)
+    x0 = np.zeros((B, 6))
+    x0[:, 0] = rng.uniform(5, 8, B)
+    x0[:, 2] = rng.uniform(0, 15, B)
+    x0[:, 3] = rng.uniform(-0.5, 0.5, B)
+    cfg = load_config("kinematic_mpc")
+    cfg["obstacles"] = not args.no_obstacles
+    if args.horizon:
+        cfg["horizon"] = args.horizon
+    trust = dict(RTI_TRUST) if args.trust == "rti" else {"trust_a": 0.0, "trust_w": 0.0}
+    cfg["qp"] = dict(cfg.get("qp") or {}, **trust)
+    N = cfg["horizon"]
+    car = KinematicCar(load_config("kinematic_car"), tr)
+    sim = BatchedRacingSimulator(car, cfg, tr, batch=B)
+    if args.warm == "zeros":
+        sim.ubar = sim._to_dev(np.zeros((B, N, 2)))
+    sim.reset(x0.copy())
+    W = Q.kin_weights(cfg)
+    W.update(trust)
+    W["obstacles"] = obs
+    X = [x0.copy()]
+    fails = np.zeros((K, B), bool)
+    sample, seen, rs = [], 0, np.random.default_rng(0)
+    for k in range(K):
+        xk = sim.states.copy()
+        xb = sim._to_host(sim.xbar).copy()
+        ub = sim._to_host(sim.ubar).copy()
+        before = sim._to_host(sim.nfail).copy()
+        sim.run(1, log=False)
+        nf = sim._to_host(sim.nfail) - before
+        fails[k] = nf > 0
+        X.append(sim.states.copy())
+        for b in np.nonzero(nf)[0]:   # reservoir sample over all non-solved steps
+            seen += 1
+            item = (k, int(b), xk[b].copy(), xb[b].copy(), ub[b].copy())
+            if len(sample) < args.sample:
+                sample.append(item)
+            elif args.sample and rs.random() < args.sample / seen:
+                sample[rs.integers(args.sample)] = item
+    X = np.array(X)
+    clear = np.min([np.hypot(X[..., 2] - so, X[..., 3] - eo) - r for so, eo, r in obs], axis=0)  # [K+1, B]
+    hit = clear < 0
+    off = np.abs(X[..., 3]) > tr.width / 2
+    print(f"max |ey| per vehicle: median {np.median(np.abs(X[..., 3]).max(0)):.2f} max {np.abs(X[..., 3]).max():.2f}; "
+          f"vehicles ever off track {off.any(0).sum()} of {B}; first off-track step median "
+          f"{np.median([np.argmax(off[:, b]) for b in range(B) if off[:, b].any()]) if off.any() else None}; "
+          f"final s median {np.median(X[-1, :, 2]):.1f}")
+    print(f"warm={args.warm} trust={args.trust}: non-solved steps {fails.sum()} of {K * B} "
+          f"({fails.mean():.3%}); at step 0: {fails[0].sum()}; vehicles ever hitting: {hit.any(0).sum()} of {B}")
+    # failures vs distance to the nearest obstacle
+    near = clear[:-1] < 3.0
+    print(f"  non-solved steps within 3 m of an obstacle: {(fails & near).sum()}, elsewhere: {(fails & ~near).sum()}")
+    firsts = [int(np.argmax(hit[:, b])) for b in range(B) if hit[:, b].any()]
+    pre = [int(fails[max(0, f - 10):f, b].sum()) for f, b in zip(firsts, [b for b in range(B) if hit[:, b].any()])]
+    print(f"  first-hit steps (median) {np.median(firsts) if firsts else None}; non-solved steps in the 10 "
+          f"steps before a first hit: {pre[:20]}")
+    cats = {}
+    W0 = dict(W, trust_a=0.0, trust_w=0.0)
+    dmax = cfg["state_constraints"]["delta_max"]
+    for (k, b, xk, xb, ub) in sorted(sample, key=lambda t: t[0]):
+        ds, kap = Q.kin_horizon_params(xk, xb.T, cfg["mpc_dt"], N, tr.k)
+        ref = Q.kin_ltv_solve(xk[None], ub[None], kap[None], ds[None], 2.5, W)
+        pf = float(ref["kkt"]["pfeas"][0])
+        ref0 = Q.kin_ltv_solve(xk[None], ub[None], kap[None], ds[None], 2.5, W0)
+        pf0 = float(ref0["kkt"]["pfeas"][0])
+        cat = ("infeasible" if pf > 1e-6 else "feasible") + ("; infeasible without trust" if pf0 > 1e-6
+                                                            else "; feasible without trust")
+        cat += "; |delta0| > delta_max" if abs(xk[1]) > dmax else ""
+        cats[cat] = cats.get(cat, 0) + 1
+        print(f"  step {k} vehicle {b}: {cat} (pfeas {pf:.2e} / {pf0:.2e}); x {np.round(xk, 3)}; "
+              f"ubar w [{ub[:, 1].min():.3f}, {ub[:, 1].max():.3f}] a [{ub[:, 0].min():.3f}, {ub[:, 0].max():.3f}]")
+    print("  sampled non-solved steps:", cats)
+
+
+if __name__ == "__main__":
+    main()

@@ -127,7 +127,9 @@ __device__ __forceinline__ double step_to_bound(double x, double dx) { return dx
 struct Rows {
   double c[5][5];
   double d[NR];
-  double m[NR];
+  uint32_t mb;  // bit i: row i is present (a 1.0 / 0.0 mask as 12 doubles would hold 24 VGPRs)
+  __device__ __forceinline__ double m(int i) const { return ((mb >> i) & 1u) ? 1.0 : 0.0; }
+  __device__ __forceinline__ void set(int i, bool on) { mb = on ? (mb | (1u << i)) : (mb & ~(1u << i)); }
 };
 
 __device__ __forceinline__ void row_values(const Rows& R, const double* v, double* o) {
@@ -198,23 +200,6 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
   }
   if (l == 0) s.flag[0] = VC_SOLVED;
   WSYNC();
-
-  // Riccati lane roles (fixed per lane): H entry (hi, hj), hi <= hj, for lanes < 45
-  int hi = 0, hj = 0;
-  {
-    int q = l < 45 ? l : 0, i = 0;
-    while (q >= 9 - i) { q -= 9 - i; ++i; }
-    hi = i;
-    hj = i + q;
-  }
-  const int hslot = qslot(hi, hj), hci = vcol(hi), hcj = vcol(hj);
-  int pi = 0, pj = 0;
-  {
-    int q = l < 28 ? l : 0, i = 0;
-    while (q >= 7 - i) { q -= 7 - i; ++i; }
-    pi = i;
-    pj = i + q;
-  }
 
   int it_total = 0, it_max = 0;
   bool all_conv = true, any_fail = false;
@@ -412,6 +397,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     // ---------------- stage QP data (lane k, registers) ----------------
     double Qc[NQ], qc[9];
     Rows R;
+    R.mb = 0u;
 #pragma unroll
     for (int e = 0; e < NQ; ++e) Qc[e] = 0.0;
 #pragma unroll
@@ -515,7 +501,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
         R.d[0] = s.xs[k][0] - W.Ux_min;
         R.d[1] = W.delta_max - s.xs[k][3];
         R.d[2] = s.xs[k][3] - W.delta_min;
-        R.m[0] = R.m[1] = R.m[2] = mk;
+        R.set(0, mk > 0.0); R.set(1, mk > 0.0); R.set(2, mk > 0.0);
 #pragma unroll
         for (int r = 0; r < 5; ++r) {
           const int fn = 2 + r;
@@ -523,7 +509,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
           for (int a = 0; a < 4; ++a) R.c[r][a] = s.u.l.st[k][fn][1 + a] / S;
           R.c[r][4] = s.u.l.st[k][fn][5];
           R.d[3 + r] = -s.u.l.st[k][fn][0] / S;
-          R.m[3 + r] = on;
+          R.set(3 + r, on > 0.0);
         }
         const double wv = s.ub[k][1];
         double up = W.w_max - wv, dn = wv - W.w_min;
@@ -533,41 +519,41 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
         }
         R.d[8] = up;
         R.d[9] = dn;
-        R.m[8] = R.m[9] = on;
+        R.set(8, on > 0.0); R.set(9, on > 0.0);
       } else {
         const double V = s.xs[k][0];
         R.d[0] = V - CW.V_min;
-        R.m[0] = on;
+        R.set(0, on > 0.0);
         R.d[1] = R.d[2] = 1.0;
-        R.m[1] = R.m[2] = 0.0;
+        R.set(1, false); R.set(2, false);
         // Fx - Peng / V <= 0 (divided by S), linearised in (V, Fx)
         R.c[0][0] = c.Peng / (V * V) / S;
         R.c[0][4] = 1.0;
         R.d[3] = -(s.ub[k][0] - c.Peng / V) / S;
-        R.m[3] = on;
+        R.set(3, on > 0.0);
 #pragma unroll
         for (int r = 4; r < 8; ++r) {
           R.d[r] = 1.0;
-          R.m[r] = 0.0;
+          R.set(r, false);
         }
         R.d[8] = R.d[9] = W.trust_Fx / S;
-        R.m[8] = R.m[9] = (stl && W.trust_Fx > 0) ? 1.0 : 0.0;
+        R.set(8, stl && W.trust_Fx > 0); R.set(9, stl && W.trust_Fx > 0);
       }
       R.d[10] = R.d[11] = W.trust_Fx / S;
-      R.m[10] = R.m[11] = (stl && W.trust_Fx > 0) ? 1.0 : 0.0;
+      R.set(10, stl && W.trust_Fx > 0); R.set(11, stl && W.trust_Fx > 0);
 #pragma unroll
       for (int i = 0; i < NR; ++i)
-        if (R.m[i] == 0.0) R.d[i] = 1.0;
+        if (R.m(i) == 0.0) R.d[i] = 1.0;
     }
     double sl[NR], la[NR];
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
-      sl[i] = R.m[i] > 0.0 ? fmax(R.d[i], 1.0) : 1.0;
-      la[i] = R.m[i];
+      sl[i] = R.m(i) > 0.0 ? fmax(R.d[i], 1.0) : 1.0;
+      la[i] = R.m(i);
     }
     double mc = 0.0;
 #pragma unroll
-    for (int i = 0; i < NR; ++i) mc += R.m[i];
+    for (int i = 0; i < NR; ++i) mc += R.m(i);
     const double mcount = wsum(mc);
     // the residual floor grows with the data (|q| up to ~1e3 in the scaled units): the
     // stopping test is relative to it
@@ -583,6 +569,24 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     WSYNC();
 
     // ---- LQ machinery (st_sqp.hip's, over H stages) -----------------------------------
+    // Riccati lane roles: H entry (hi, hj), hi <= hj, for lanes < 45; P entry (pi, pj) for
+    // lanes < 28.  Recomputed here each SQP iteration (a few integer ops) rather than held
+    // across the linearisation, whose dual-number evaluations need every register.
+    int hi = 0, hj = 0;
+    {
+      int q = l < 45 ? l : 0, i = 0;
+      while (q >= 9 - i) { q -= 9 - i; ++i; }
+      hi = i;
+      hj = i + q;
+    }
+    const int hslot = qslot(hi, hj), hci = vcol(hi), hcj = vcol(hj);
+    int pi = 0, pj = 0;
+    {
+      int q = l < 28 ? l : 0, i = 0;
+      while (q >= 7 - i) { q -= 7 - i; ++i; }
+      pi = i;
+      pj = i + q;
+    }
     const int ta = l < 56 ? (l >> 3) : 0, tj = l & 7;
     const double tpm = tj == 6 ? 1.0 : 0.0;
     const int hcic = hci < 0 ? 0 : hci, hcjc = hcj < 0 ? 0 : hcj;
@@ -788,10 +792,10 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       row_values(R, vk, val);
 #pragma unroll
       for (int i = 0; i < NR; ++i) {
-        rp[i] = R.m[i] * (val[i] + sl[i] - R.d[i]);
-        wg[i] = R.m[i] * la[i] / sl[i];
+        rp[i] = R.m(i) * (val[i] + sl[i] - R.d[i]);
+        wg[i] = R.m(i) * la[i] / sl[i];
         rpm = fmax(rpm, fabs(rp[i]));
-        mus += R.m[i] * sl[i] * la[i];
+        mus += R.m(i) * sl[i] * la[i];
       }
       qmul(Qc, vk, grk);
 #pragma unroll
@@ -799,7 +803,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       {
         double ml[NR];
 #pragma unroll
-        for (int i = 0; i < NR; ++i) ml[i] = R.m[i] * la[i];
+        for (int i = 0; i < NR; ++i) ml[i] = R.m(i) * la[i];
         row_adjoint(R, ml, grk);
       }
       if (stl) {
@@ -847,7 +851,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
         if (stl) {
           double y[NR], hk[9];
 #pragma unroll
-          for (int i = 0; i < NR; ++i) y[i] = R.m[i] * (wg[i] * rp[i] - rc_over_s[i]);
+          for (int i = 0; i < NR; ++i) y[i] = R.m(i) * (wg[i] * rp[i] - rc_over_s[i]);
 #pragma unroll
           for (int e = 0; e < 9; ++e) hk[e] = grk[e];
           row_adjoint(R, y, hk);
@@ -865,15 +869,15 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       row_values(R, dvk, cdv);
 #pragma unroll
       for (int i = 0; i < NR; ++i) {
-        dsa[i] = R.m[i] * (-rp[i] - cdv[i]);
-        dla[i] = R.m[i] * (wg[i] * (cdv[i] + rp[i]) - la[i]);
-        if (stl && R.m[i] > 0.0) amin = fmin(amin, fmin(step_to_bound(sl[i], dsa[i]), step_to_bound(la[i], dla[i])));
+        dsa[i] = R.m(i) * (-rp[i] - cdv[i]);
+        dla[i] = R.m(i) * (wg[i] * (cdv[i] + rp[i]) - la[i]);
+        if (stl && R.m(i) > 0.0) amin = fmin(amin, fmin(step_to_bound(sl[i], dsa[i]), step_to_bound(la[i], dla[i])));
       }
       amin = wmin(amin);
       double ms = 0.0;
       if (stl) {
 #pragma unroll
-        for (int i = 0; i < NR; ++i) ms += R.m[i] * (sl[i] + amin * dsa[i]) * (la[i] + amin * dla[i]);
+        for (int i = 0; i < NR; ++i) ms += R.m(i) * (sl[i] + amin * dsa[i]) * (la[i] + amin * dla[i]);
       }
       ms = wsum(ms) / mcount;
       const double ratio = mu > 0.0 ? fmin(1.0, ms / mu) : 0.0;
@@ -881,7 +885,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
 
       double rcs[NR];
 #pragma unroll
-      for (int i = 0; i < NR; ++i) rcs[i] = R.m[i] * (sl[i] * la[i] + dsa[i] * dla[i] - smu) / sl[i];
+      for (int i = 0; i < NR; ++i) rcs[i] = R.m(i) * (sl[i] * la[i] + dsa[i] * dla[i] - smu) / sl[i];
       set_h(rcs);
       lq_solve();
 #pragma unroll
@@ -890,15 +894,15 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       amin = 1.0;
 #pragma unroll
       for (int i = 0; i < NR; ++i) {
-        dsa[i] = R.m[i] * (-rp[i] - cdv[i]);
-        dla[i] = R.m[i] * (wg[i] * (cdv[i] + rp[i]) - rcs[i]);
-        if (stl && R.m[i] > 0.0) amin = fmin(amin, fmin(step_to_bound(sl[i], dsa[i]), step_to_bound(la[i], dla[i])));
+        dsa[i] = R.m(i) * (-rp[i] - cdv[i]);
+        dla[i] = R.m(i) * (wg[i] * (cdv[i] + rp[i]) - rcs[i]);
+        if (stl && R.m(i) > 0.0) amin = fmin(amin, fmin(step_to_bound(sl[i], dsa[i]), step_to_bound(la[i], dla[i])));
       }
       const double alpha = fmin(1.0, 0.99 * wmin(amin));
       if (stl) {
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
-          if (R.m[i] > 0.0) {
+          if (R.m(i) > 0.0) {
             sl[i] = fmax(sl[i] + alpha * dsa[i], 1e-300);
             la[i] = fmax(la[i] + alpha * dla[i], 1e-300);
           }
