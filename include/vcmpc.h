@@ -58,7 +58,7 @@
 extern "C" {
 #endif
 
-#define VCMPC_ABI_VERSION 5
+#define VCMPC_ABI_VERSION 6
 #define VC_MAX_OBSTACLES 16
 
 typedef struct vc_ctx vc_ctx;
@@ -120,11 +120,14 @@ typedef struct vc_qp {
   int32_t max_iter; /* interior-point iteration cap */
   int32_t polish;   /* active-set polish rounds after the interior point (0 = off) */
   int32_t solver;   /* solve-kernel choice (ABI 5).  Kinematic: 0 = condensed (kin_ltv.hip) where
-                       built (N = 20), else stagewise Riccati (kin_ric.hip); 1 = stagewise
-                       Riccati always.  Cascaded: 0 / 1 = stagewise Riccati (casc_ric.hip),
+                       built (N = 20) and kin_sqp == 0, else stagewise Riccati (kin_ric.hip);
+                       1 = stagewise Riccati always.  Cascaded: 0 / 1 = stagewise Riccati (casc_ric.hip),
                        2 = condensed (casc_sqp.hip, M = 40 only).  Single-track: the dtype
                        picks the kernel (VC_F32: dyn_sqp.hip, VC_F64: st_sqp.hip). */
-  int32_t pad_;
+  int32_t kin_sqp;  /* kinematic (ABI 6): 0 = one LTV-QP step (the C2 contract); k > 0 = k SQP
+                       steps, each QP step followed by an Armijo line search on the exact NLP cost
+                       + an L1 state-row penalty (kin_merit.hip, oracle/kin_sqp.py) -- the
+                       globalised step for the obstacle barrier (kinematic_mpc.py:130-133) */
 } vc_qp;
 
 /* Cascaded controller: single-track stages followed by a point-mass tail

@@ -1,0 +1,122 @@
+"""Oracle restatement of the kinematic SQP step with a merit line search (TEST INFRASTRUCTURE
+ONLY).
+
+The kinematic LTV-QP contract (oracle/ltv_qp.py) takes one convexified QP step per control
+step.  With the obstacle barrier of kinematic_mpc.py:130-133 that is not enough: the QP's
+second-order barrier model at a prediction that passes close to (or through) an obstacle
+extrapolates the barrier's steep slope, and successive control steps keep steering away long
+after the trajectory is clear, off the track.  The reference avoids this
+because IPOPT solves the NLP with the exact barrier.  The build's globalised step:
+
+    repeat sqp_iters times:
+        dz    = the LTV-QP step at ubar (oracle/ltv_qp.py, trust region included)
+        alpha = the first of 1, 1/2, ..., 2^-(LS_STEPS-1) with
+                phi(ubar + alpha dz) <= phi(ubar) + ARMIJO * alpha * D,
+                D = (phi(ubar + EPS_FD dz) - phi(ubar)) / EPS_FD  (one-sided derivative),
+                and no step at all (alpha = 0) if none qualifies or D >= 0
+        ubar += alpha dz
+
+phi is the exact NLP cost of the QP contract (the same terms, each `if_else` evaluated on
+the trial rollout instead of frozen at the prediction, no proximal term) plus an exact L1
+penalty on the state rows:
+
+    sum_{n=1}^{N-1} [ w_b ds_n (ey_n - ey_min)^2 [ey_n < ey_min] + w_b ds_n (ey_n - ey_max)^2 [ey_n > ey_max]
+                      + w_dev ds_n ey_n^2 + w_obs ds_n sum_j b(dist_nj - (r_j + 0.1)) ]
+  + sum_{n=0}^{N-1} w_w w_n^2 + sum_{n=0}^{N-2} w_a (a_{n+1} - a_n)^2
+  + w_v (v_N - v_max)^2 [v_N >= v_max] + w_time t_N + w_ey ey_N^2 + w_epsi epsi_N^2
+  + RHO sum_{n=1}^{N-1} [ (v_min - v_n)_+ + (delta_n - delta_max)_+ + (delta_min - delta_n)_+ ]
+
+with b(m) = 1/m for m >= m0 = margin_min (the reference's barrier) and its second-order
+Taylor extension 1/m0 - (m - m0)/m0^2 + (m - m0)^2/m0^3 below (finite, convex and decreasing
+through the obstacle, so a trajectory that passes through one is pushed out rather than
+rewarded by the reference's negative values inside).  The device code is
+csrc/kin_merit.hip; the operation order below is the same.  Parity unpinned by the
+reference (IPOPT cannot run here; no recorded kinematic run exists).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import ltv_qp as Q
+
+LS_STEPS = 8        # alpha = 1 .. 2^-7
+ARMIJO = 1e-4
+EPS_FD = 1e-7
+RHO = 1e3           # L1 penalty on the state rows (above every multiplier seen in the contract's QPs)
+IV, ID, IS, IEY, IEP, IT = Q.IV, Q.ID, Q.IS, Q.IEY, Q.IEP, Q.IT
+IA, IW = Q.IA, Q.IW
+
+
+def barrier_ext(m, m0):
+    """b(m): 1/m above m0, the quadratic Taylor extension of 1/m at m0 below."""
+    m = np.asarray(m, np.float64)
+    dm = m - m0
+    ext = 1.0 / m0 - dm / (m0 * m0) + dm * dm / (m0 * m0 * m0)
+    return np.where(m >= m0, 1.0 / np.maximum(m, m0), ext)
+
+
+def merit(x0, u, kappa, ds, L, W):
+    """phi(u) per problem: x0[B,6], u[B,N,2], kappa/ds[B,N] -> [B]."""
+    x = Q.kin_predict(np.asarray(x0, np.float64), np.asarray(u, np.float64), kappa, ds, L)  # [B, N+1, 6]
+    u = np.asarray(u, np.float64)
+    B, N = u.shape[:2]
+    ds = np.asarray(ds, np.float64)
+    ey = x[:, 1:N, IEY]
+    dsn = ds[:, 1:N]
+    phi = np.zeros(B)
+    lo = ey < W["ey_min"]
+    hi = ey > W["ey_max"]
+    phi += np.sum(np.where(lo, W["w_b"] * dsn * (ey - W["ey_min"]) ** 2, 0.0), axis=1)
+    phi += np.sum(np.where(hi, W["w_b"] * dsn * (ey - W["ey_max"]) ** 2, 0.0), axis=1)
+    phi += np.sum(W["w_dev"] * dsn * ey * ey, axis=1)
+    if W.get("obstacles"):
+        m0 = W.get("obs_margin_min", 0.05)
+        sa = x[:, 1:N, IS]
+        for so, eo, r in W["obstacles"]:
+            d = np.sqrt((sa - so) ** 2 + (ey - eo) ** 2)
+            phi += np.sum(W["w_obs"] * dsn * barrier_ext(d - (r + 0.1), m0), axis=1)
+    phi += np.sum(W["w_w"] * u[:, :, IW] ** 2, axis=1)
+    phi += np.sum(W["w_a"] * (u[:, 1:, IA] - u[:, :-1, IA]) ** 2, axis=1)
+    vN = x[:, N, IV]
+    phi += np.where(vN >= W["v_max"], W["w_v"] * (vN - W["v_max"]) ** 2, 0.0)
+    phi += W["w_time"] * x[:, N, IT] + W["w_ey"] * x[:, N, IEY] ** 2 + W["w_epsi"] * x[:, N, IEP] ** 2
+    v, dl = x[:, 1:N, IV], x[:, 1:N, ID]
+    viol = (np.maximum(W["v_min"] - v, 0.0) + np.maximum(dl - W["delta_max"], 0.0)
+            + np.maximum(W["delta_min"] - dl, 0.0))
+    phi += RHO * np.sum(viol, axis=1)
+    return phi
+
+
+def line_search(x0, ubar, dz, kappa, ds, L, W):
+    """(alpha[B], phi0[B], phi_alpha[B], D[B]) of the rule in the module docstring."""
+    ubar = np.asarray(ubar, np.float64)
+    phi0 = merit(x0, ubar, kappa, ds, L, W)
+    D = (merit(x0, ubar + EPS_FD * dz, kappa, ds, L, W) - phi0) / EPS_FD
+    B = len(phi0)
+    alpha = np.zeros(B)
+    phia = phi0.copy()
+    done = D >= 0.0
+    a = 1.0
+    for _ in range(LS_STEPS):
+        pa = merit(x0, ubar + a * dz, kappa, ds, L, W)
+        ok = ~done & (pa <= phi0 + ARMIJO * a * D)
+        alpha[ok] = a
+        phia[ok] = pa[ok]
+        done |= ok
+        a *= 0.5
+    return alpha, phi0, phia, D
+
+
+def kin_sqp_solve(x0, ubar, kappa, ds, L, W, sqp_iters, **qp_kw):
+    """The globalised step: u_star[B,N,2], x_star[B,N+1,6] (x at u_star), per-iteration
+    (alpha, phi0, phi, D, QP certificates)."""
+    u = np.array(ubar, np.float64, copy=True)
+    hist = []
+    for _ in range(sqp_iters):
+        sol = Q.kin_ltv_solve(x0, u, kappa, ds, L, W, **qp_kw)
+        dz = sol["u_star"] - u
+        alpha, phi0, phia, D = line_search(x0, u, dz, kappa, ds, L, W)
+        hist.append(dict(alpha=alpha, phi0=phi0, phi=phia, D=D, kkt=sol["kkt"], polished=sol["polished"]))
+        u = u + alpha[:, None, None] * dz
+    x_star = Q.kin_predict(np.asarray(x0, np.float64), u, kappa, ds, L)
+    return dict(u_star=u, x_star=x_star, u0=u[:, 0].copy(), hist=hist)

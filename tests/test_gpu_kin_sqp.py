@@ -1,0 +1,100 @@
+"""GPU parity of the kinematic globalised SQP step (vc_qp.kin_sqp > 0: QP step through
+kin_ltv.hip / kin_ric.hip, then the merit line search of csrc/kin_merit.hip) through the C ABI,
+against the oracle (oracle/kin_sqp.py) on the obstacle golden problems
+(tests/golden/obs_golden.npz), whose predictions pass close to or through ippodromo's obstacles.
+
+Tolerance: the north star's 1e-5 on u* (m/s^2, rad/s); the line search is a discrete choice,
+so the accepted step sizes must agree exactly.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from oracle import kin_sqp as KS
+from oracle import ltv_qp as Q
+
+pytestmark = pytest.mark.gpu
+
+U_TOL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def golden():
+    return dict(np.load(os.path.join(GOLDEN, "obs_golden.npz")))
+
+
+def _obs(g):
+    return [tuple(float(v) for v in o) for o in g["obstacles"]]
+
+
+def _cfg(kin_sqp, solver=0, N=20):
+    from vcmpc.config import load_config
+    cfg = load_config("kinematic_mpc")
+    cfg["horizon"] = N
+    cfg["qp"] = dict(cfg["qp"], kin_sqp=kin_sqp, solver=solver)
+    return cfg
+
+
+def _ctx(cfg, obstacles, B, N=20):
+    from vcmpc import Context, _abi
+    from vcmpc.config import load_config, make_params
+    p = make_params(kin_car=load_config("kinematic_car"), kin_mpc=cfg, obstacles=obstacles)
+    return Context(model=_abi.VC_MODEL_KINEMATIC, N=N, max_batch=B, dtype=_abi.VC_F64, params=p)
+
+
+@pytest.mark.parametrize("solver", [0, 1], ids=["kin_ltv", "kin_ric"])
+def test_kin_sqp_obstacles_vs_oracle(golden, solver):
+    g = golden
+    obs = _obs(g)
+    S = 3
+    cfg = _cfg(S, solver)
+    W = Q.kin_weights(cfg)
+    W["obstacles"] = obs
+    x0, ub, kap, ds = (g[k].astype(np.float64) for k in ("kin_x0", "kin_ubar", "kin_kappa", "kin_ds"))
+    ref = KS.kin_sqp_solve(x0, ub, kap, ds, 2.5, W, S)
+    with _ctx(cfg, obs, len(x0)) as c:
+        u0, xs, us, st, it = c.solve(x0, kap, ds, ub.copy())
+    err = np.abs(us - ref["u_star"]).max(axis=(1, 2))
+    alphas = np.array([h["alpha"] for h in ref["hist"]])
+    print(f"solver {solver}: |u* - u*_oracle| max {err.max():.2e}; oracle step sizes per iteration "
+          f"{[np.unique(a).tolist() for a in alphas]}; status {np.bincount(st)}")
+    assert (st == 0).all(), st
+    assert err.max() < U_TOL, np.argsort(err)[-5:]
+    np.testing.assert_array_equal(u0, us[:, 0])
+    x_own = Q.kin_predict(x0, us, kap, ds, 2.5)     # x* = rollout(u*) of the kernel's own u*
+    dx = np.abs(xs - x_own)
+    print("x* vs rollout(u*): max %.2e at %s" % (dx.max(), np.unravel_index(dx.argmax(), dx.shape)))
+    assert dx.max() < 1e-9
+    # the merit of the final iterate never exceeds the start's
+    phi_start = KS.merit(x0, ub, kap, ds, 2.5, W)
+    phi_end = KS.merit(x0, us, kap, ds, 2.5, W)
+    assert (phi_end <= phi_start + 1e-9 * np.abs(phi_start)).all()
+
+
+def test_kin_sqp_without_obstacles_is_descent(golden):
+    """kin_sqp = 2 on the plain C2 sampler: every accepted iterate lowers the merit, and the
+    first SQP iteration's full QP step is taken where the merit allows it (oracle agrees)."""
+    from vcmpc.workload import kinematic_batch
+    d = kinematic_batch(64, seed=5)
+    cfg = _cfg(2)
+    W = Q.kin_weights(cfg)
+    ref = KS.kin_sqp_solve(d["x0"], d["ubar"], d["kappa"], d["ds"], 2.5, W, 2)
+    with _ctx(cfg, [], 64) as c:
+        u0, xs, us, st, it = c.solve(d["x0"], d["kappa"], d["ds"], d["ubar"].copy())
+    assert (st == 0).all()
+    assert np.abs(us - ref["u_star"]).max() < U_TOL
+    phi0 = KS.merit(d["x0"], d["ubar"], d["kappa"], d["ds"], 2.5, W)
+    assert (KS.merit(d["x0"], us, d["kappa"], d["ds"], 2.5, W) <= phi0 + 1e-9 * np.abs(phi0)).all()
+
+
+def test_kin_sqp_zero_is_the_ltv_contract(golden):
+    """kin_sqp = 0 keeps the one-step LTV-QP contract bit for bit (the C2 hot path)."""
+    from vcmpc.workload import kinematic_batch
+    d = kinematic_batch(32, seed=6)
+    with _ctx(_cfg(0), [], 32) as c:
+        r0 = c.solve(d["x0"], d["kappa"], d["ds"], d["ubar"].copy())
+    W = Q.kin_weights(_cfg(0))
+    ref = Q.kin_ltv_solve(d["x0"], d["ubar"], d["kappa"], d["ds"], 2.5, W)
+    assert np.abs(r0[2] - ref["u_star"]).max() < U_TOL

@@ -111,11 +111,12 @@ def _min_clearance(X, obstacles, i_s, i_ey):
 def test_kinematic_closed_loop_with_obstacles():
     """BatchedRacingSimulator with the kinematic controller and ``obstacles: True`` on
     ippodromo (the reference's kinematic default, config/controllers/kinematic.yaml:4),
-    vehicles starting on the centre line ahead of the obstacle field.  Without the
-    barrier terms every vehicle drives through an obstacle; with them the clearance
-    improves but the kinematic contract -- one LTV-QP per control step over a 20-stage
-    (~15 m) preview, the reference file has 50 -- does not keep every vehicle clear
-    (the dynamic NMPC below does)."""
+    vehicles starting on the centre line ahead of the obstacle field.  Without the barrier
+    terms every vehicle drives through an obstacle; with them the controller takes the
+    globalised step (10 SQP steps with the merit line search per control step,
+    controllers/kinematic_mpc.py KIN_OBS_SQP, csrc/kin_merit.hip): no vehicle touches an
+    obstacle, every vehicle stays on the track, <= 2 % non-solved steps (measured 0.04 %;
+    round 1's one convexified QP per step: 39 of 64 hit, 21 % non-solved)."""
     from vcmpc.config import load_config
     from vcmpc.environment import Track
     from vcmpc.models import KinematicCar
@@ -140,17 +141,15 @@ def test_kinematic_closed_loop_with_obstacles():
         res[flag] = (_min_clearance(X, obs, 2, 3), X, out["nfail"])
     clear_on, X_on, nfail_on = res[True]
     clear_off, _, _ = res[False]
-    print("clearance with obstacles: median %.3f, %d/%d clear; without: median %.3f, %d/%d clear"
-          % (np.median(clear_on), int((clear_on > 0).sum()), B, np.median(clear_off), int((clear_off > 0).sum()), B))
+    print("clearance with obstacles: median %.3f, %d/%d clear; without: median %.3f, %d/%d clear; "
+          "non-solved steps %d of %d; max |ey| %.2f"
+          % (np.median(clear_on), int((clear_on > 0).sum()), B, np.median(clear_off), int((clear_off > 0).sum()), B,
+             int(nfail_on.sum()), B * K, np.abs(X_on[:, :, 3]).max()))
     assert (clear_off < 0).sum() >= B // 2          # the obstacle field is in the way
-    assert np.median(clear_on) > np.median(clear_off) + 0.5   # measured: -0.48 vs -1.85 m
-    assert (clear_on > 0).sum() >= B // 4                      # measured: 25 of 64 (0 without)
-    assert np.median(X_on[-1, :, 2]) > 100.0        # into the field (measured median 116 m; obstacles up to s = 185)
-    # measured 5,383 of 25,600 vehicle-steps (21 %) end at max_iter: with the floored margin
-    # the barrier curvature reaches ~1e5 and the kinematic interior point (max_iter 40) does
-    # not reach tol on those QPs; the simulator restarts them from the neutral warm start
-    # (DESIGN.md 2c).  The bar guards against a regression, not the known weakness.
-    assert nfail_on.sum() <= 0.25 * B * K, nfail_on.sum()
+    assert (clear_on > 0).all()                      # no vehicle touches an obstacle
+    assert (np.abs(X_on[:, :, 3]) < tr.width / 2).all()
+    assert np.median(X_on[-1, :, 2]) > 200.0         # through the field (obstacles up to s = 185)
+    assert nfail_on.sum() <= 0.02 * B * K, nfail_on.sum()
 
 
 def test_dynamic_closed_loop_avoids_obstacles():

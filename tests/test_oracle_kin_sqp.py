@@ -1,0 +1,63 @@
+"""CPU checks of the kinematic globalised-step oracle (oracle/kin_sqp.py): the merit is the
+contract's cost evaluated on the nonlinear rollout, its barrier extension is C1 at the floor,
+and the line search only accepts sufficient decrease."""
+import numpy as np
+
+from oracle import kin_sqp as KS
+from oracle import ltv_qp as Q
+from oracle import obstacles as OB
+
+
+def _W(obstacles=()):
+    from vcmpc.config import load_config
+    W = Q.kin_weights(load_config("kinematic_mpc"))
+    W["obstacles"] = list(obstacles)
+    return W
+
+
+def test_barrier_extension_is_c1_at_the_floor():
+    m0 = OB.MARGIN_MIN
+    h = 1e-7
+    b = lambda m: KS.barrier_ext(np.array([m]), m0)[0]
+    assert abs(b(m0 + h) - b(m0 - h)) < 1e-4                      # continuous
+    d_hi = (b(m0 + 2 * h) - b(m0 + h)) / h
+    d_lo = (b(m0 - h) - b(m0 - 2 * h)) / h
+    assert abs(d_hi - d_lo) / abs(d_hi) < 1e-4                    # slope continuous
+    m = np.linspace(-3.0, 2.0, 501)
+    v = KS.barrier_ext(m, m0)
+    assert (np.diff(v) < 0).all() and (v > 0).all()              # decreasing, positive through the obstacle
+    np.testing.assert_allclose(KS.barrier_ext(m[m > m0], m0), 1.0 / m[m > m0])
+
+
+def test_merit_matches_the_qp_cost_at_the_prediction():
+    """At dz = 0 the QP's model equals the exact cost (no obstacle): phi(ubar) minus the
+    constant parts = 0 model value; checked as phi(ubar + eps dz) - phi(ubar) ~ eps g.dz."""
+    from vcmpc.workload import kinematic_batch
+    d = kinematic_batch(6, seed=3)
+    W = _W()
+    Qd = Q.kin_qp(d["x0"], d["ubar"], d["kappa"], d["ds"], 2.5, W)
+    rng = np.random.default_rng(0)
+    dz = rng.normal(size=Qd["g"].shape) * 1e-3
+    eps = 1e-4
+    phi0 = KS.merit(d["x0"], d["ubar"], d["kappa"], d["ds"], 2.5, W)
+    phi1 = KS.merit(d["x0"], d["ubar"] + eps * dz.reshape(d["ubar"].shape), d["kappa"], d["ds"], 2.5, W)
+    # the QP gradient g is the exact cost gradient at the prediction (Gauss-Newton model)
+    pen = np.zeros(6)  # the sampler's predictions satisfy the state rows (no penalty slope)
+    np.testing.assert_allclose((phi1 - phi0) / eps, np.einsum("bi,bi->b", Qd["g"], dz) + pen, rtol=1e-3, atol=1e-6)
+
+
+def test_line_search_accepts_only_sufficient_decrease():
+    from vcmpc.workload import kinematic_batch
+    d = kinematic_batch(16, seed=4)
+    W = _W([(30.0, 0.0, 1.0), (60.0, 0.0, 2.0)])
+    d["x0"][:, 2] = np.linspace(10.0, 50.0, 16)
+    sol = Q.kin_ltv_solve(d["x0"], d["ubar"], d["kappa"], d["ds"], 2.5, W)
+    dz = sol["u_star"] - d["ubar"]
+    alpha, phi0, phia, D = KS.line_search(d["x0"], d["ubar"], dz, d["kappa"], d["ds"], 2.5, W)
+    ok = alpha > 0
+    assert (phia[ok] <= phi0[ok] + KS.ARMIJO * alpha[ok] * D[ok]).all()
+    assert (D[ok] < 0).all()
+    np.testing.assert_array_equal(phia[~ok], phi0[~ok])
+    r = KS.kin_sqp_solve(d["x0"], d["ubar"], d["kappa"], d["ds"], 2.5, W, 3)
+    phis = np.array([h["phi"] for h in r["hist"]])
+    assert (np.diff(np.vstack([phi0, phis]), axis=0) <= 1e-9 * np.abs(phi0)).all()   # monotone merit

@@ -1,0 +1,156 @@
+// kin_merit.hip -- merit line search of the kinematic SQP step (fp64), one wavefront per problem.
+//
+// The kinematic LTV-QP contract takes one convexified QP step per control step; with the
+// obstacle barrier of kinematic_mpc.py:130-133 the build globalises it (vc_qp.kin_sqp > 0):
+// kin_sqp times { QP step dz at ubar (kin_ltv.hip / kin_ric.hip); this kernel: Armijo
+// backtracking on the exact NLP cost + an L1 penalty on the state rows; ubar += alpha dz }.
+// Contract and operation order: oracle/kin_sqp.py (merit, line_search).
+//
+// Lanes 0..LS-1 evaluate phi(u_prev + 2^-j dz), lane LS phi(u_prev + EPS dz) (the one-sided
+// directional derivative), lane LS+1 phi(u_prev); each lane rolls its candidate out with the
+// spatial Euler model (kinematic_car.py:47-64) and sums the cost terms stage by stage -- a few
+// thousand flops per lane, negligible next to the QP.  Lane 0 picks the first candidate with
+// sufficient decrease (none, or a failed QP: alpha = 0), then the wavefront writes the
+// accepted inputs, lane 0 their rollout x* and u0, and the solve status / iteration count
+// accumulate over the SQP iterations (status: the first non-solved QP's; iterations: summed).
+#include <hip/hip_runtime.h>
+
+#include "vc_kernels.hpp"
+#include "vc_models.hpp"
+#include "vcmpc.h"
+
+namespace vc {
+namespace {
+
+constexpr int LS = 8;            // alpha = 1 .. 2^-7  (oracle/kin_sqp.py LS_STEPS)
+constexpr double ARMIJO = 1e-4;  // sufficient-decrease constant
+constexpr double EPS_FD = 1e-7;  // directional-derivative step
+constexpr double RHO = 1e3;      // L1 penalty on the state rows
+
+__device__ __forceinline__ double bcast(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+
+// b(m): 1/m above m0, the quadratic Taylor extension of 1/m at m0 below (oracle barrier_ext)
+__device__ __forceinline__ double barrier_ext(double m, double m0) {
+  if (m >= m0) return 1.0 / m;
+  const double dm = m - m0;
+  return 1.0 / m0 - dm / (m0 * m0) + dm * dm / (m0 * m0 * m0);
+}
+
+// phi(u), u = up + alpha (uq - up), for one problem (oracle/kin_sqp.py merit)
+__device__ double merit(const KinMeritArgs& A, int b, double alpha) {
+  const int N = A.N;
+  const vc_kin_mpc& W = A.w;
+  const double* x0 = A.x0 + (size_t)b * KIN_NX;
+  const double* kap = A.kappa + (size_t)b * N;
+  const double* dsv = A.ds + (size_t)b * N;
+  const double* up = A.u_prev + (size_t)b * N * 2;
+  const double* uq = A.ubar + (size_t)b * N * 2;
+  double x[KIN_NX];
+#pragma unroll
+  for (int i = 0; i < KIN_NX; ++i) x[i] = x0[i];
+  double blo = 0.0, bhi = 0.0, dev = 0.0, obs = 0.0, ww = 0.0, wa = 0.0, pen = 0.0, a_prev = 0.0;
+  const double m0 = A.obs.margin_min;
+  for (int n = 0; n < N; ++n) {
+    const double u[2] = {up[2 * n] + alpha * (uq[2 * n] - up[2 * n]),
+                         up[2 * n + 1] + alpha * (uq[2 * n + 1] - up[2 * n + 1])};
+    const double ds = dsv[n];
+    if (n >= 1) {  // stage terms on x_n (n = 0 is the fixed initial state)
+      const double ey = x[3];
+      if (ey < W.ey_min) blo += W.w_b * ds * (ey - W.ey_min) * (ey - W.ey_min);
+      if (ey > W.ey_max) bhi += W.w_b * ds * (ey - W.ey_max) * (ey - W.ey_max);
+      dev += W.w_dev * ds * ey * ey;
+      for (int j = 0; j < A.obs.n; ++j) {
+        const double a = x[2] - A.obs.s[j], e = ey - A.obs.ey[j];
+        const double d = sqrt(a * a + e * e);
+        obs += W.w_obs * ds * barrier_ext(d - (A.obs.radius[j] + 0.1), m0);
+      }
+      pen += fmax(W.v_min - x[0], 0.0) + fmax(x[1] - W.delta_max, 0.0) + fmax(W.delta_min - x[1], 0.0);
+      wa += W.w_a * (u[0] - a_prev) * (u[0] - a_prev);
+    }
+    ww += W.w_w * u[1] * u[1];
+    a_prev = u[0];
+    double f[KIN_NX];
+    kin_spatial_ode<double>(x, u, kap[n], A.L, f);
+#pragma unroll
+    for (int i = 0; i < KIN_NX; ++i) x[i] = x[i] + ds * f[i];
+  }
+  double phi = blo + bhi + dev + obs + ww + wa;
+  if (x[0] >= W.v_max) phi += W.w_v * (x[0] - W.v_max) * (x[0] - W.v_max);
+  phi += W.w_time * x[5] + W.w_ey * x[3] * x[3] + W.w_epsi * x[4] * x[4];
+  return phi + RHO * pen;
+}
+
+__global__ __launch_bounds__(64) void kin_merit_kernel(KinMeritArgs A) {
+  const int b = blockIdx.x;
+  const int l = threadIdx.x;
+  const int N = A.N;
+  // candidate of this lane
+  double alpha = 0.0;
+  if (l < LS) alpha = ldexp(1.0, -l);
+  else if (l == LS) alpha = EPS_FD;
+  double phi = 0.0;
+  if (l <= LS + 1) phi = merit(A, b, alpha);
+  const double phi0 = bcast(phi, LS + 1);
+  const double D = (bcast(phi, LS) - phi0) / EPS_FD;
+  const bool qp_ok = A.qp_status[b] == VC_SOLVED;
+  // lane 0..LS-1: sufficient decrease?  the first such lane (largest alpha) wins
+  const bool good = l < LS && qp_ok && D < 0.0 && isfinite(phi) && phi <= phi0 + ARMIJO * alpha * D;
+  const uint64_t mask = __ballot(good);
+  const int pick = mask ? __builtin_ctzll(mask) : -1;
+  const double al = pick >= 0 ? ldexp(1.0, -pick) : 0.0;
+  const double phia = pick >= 0 ? bcast(phi, pick) : phi0;
+  const double* up = A.u_prev + (size_t)b * N * 2;
+  double* ub = A.ubar + (size_t)b * N * 2;
+  if (l == 0) {  // rollout of the accepted inputs (read before the wavefront overwrites u*)
+    double x[KIN_NX];
+    double* xo = A.x_out + (size_t)b * (N + 1) * KIN_NX;
+#pragma unroll
+    for (int i = 0; i < KIN_NX; ++i) {
+      x[i] = A.x0[(size_t)b * KIN_NX + i];
+      xo[i] = x[i];
+    }
+    for (int n = 0; n < N; ++n) {
+      const double u[2] = {up[2 * n] + al * (ub[2 * n] - up[2 * n]), up[2 * n + 1] + al * (ub[2 * n + 1] - up[2 * n + 1])};
+      if (n == 0) {
+        A.u0[(size_t)b * 2] = u[0];
+        A.u0[(size_t)b * 2 + 1] = u[1];
+      }
+      double f[KIN_NX];
+      kin_spatial_ode<double>(x, u, A.kappa[(size_t)b * N + n], A.L, f);
+#pragma unroll
+      for (int i = 0; i < KIN_NX; ++i) {
+        x[i] = x[i] + A.ds[(size_t)b * N + n] * f[i];
+        xo[(n + 1) * KIN_NX + i] = x[i];
+      }
+    }
+    const int32_t st_prev = A.first ? VC_SOLVED : A.st_acc[b];
+    const int32_t st = st_prev != VC_SOLVED ? st_prev : A.qp_status[b];
+    const int32_t it = (A.first ? 0 : A.it_acc[b]) + A.qp_iters[b];
+    A.st_acc[b] = st;
+    A.it_acc[b] = it;
+    A.status[b] = st;
+    A.iters[b] = it;
+    if (A.ls_diag) {
+      A.ls_diag[(size_t)b * 4 + 0] = al;
+      A.ls_diag[(size_t)b * 4 + 1] = phi0;
+      A.ls_diag[(size_t)b * 4 + 2] = phia;
+      A.ls_diag[(size_t)b * 4 + 3] = D;
+    }
+  }
+  __syncthreads();  // lane 0's reads of u* have completed
+  for (int e = l; e < 2 * N; e += 64) ub[e] = up[e] + al * (ub[e] - up[e]);
+}
+
+}  // namespace
+
+hipError_t launch_kin_merit(const KinMeritArgs& a, hipStream_t stream) {
+  if (a.B <= 0) return hipSuccess;
+  hipLaunchKernelGGL(kin_merit_kernel, dim3(a.B), dim3(64), 0, stream, a);
+  return hipGetLastError();
+}
+
+}  // namespace vc

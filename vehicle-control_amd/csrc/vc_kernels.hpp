@@ -64,6 +64,29 @@ struct KinLtvArgs {
   vc_obstacles obs;
 };
 
+// Merit line search of the kinematic SQP step (kin_merit.hip; vc_qp.kin_sqp > 0).
+struct KinMeritArgs {
+  const double* x0;        // [B][6]
+  const double* kappa;     // [B][N]
+  const double* ds;        // [B][N]
+  const double* u_prev;    // [B][N][2]  iterate before this QP step
+  double* ubar;            // [B][N][2]  in: the QP's u*; out: u_prev + alpha (u* - u_prev)
+  double* x_out;           // [B][N+1][6] rollout of the accepted iterate
+  double* u0;              // [B][2]
+  const int32_t* qp_status;  // [B] this iteration's QP status (aliases status)
+  const int32_t* qp_iters;   // [B] this iteration's QP iterations (aliases iters)
+  int32_t* status;         // [B] accumulated: the first non-solved QP's status
+  int32_t* iters;          // [B] accumulated interior-point iterations
+  int32_t* st_acc;         // [B] scratch accumulators
+  int32_t* it_acc;         // [B]
+  double* ls_diag;         // [B][4] optional: alpha, phi(u_prev), phi(accepted), directional derivative
+  int B, N;
+  int first;               // 1 on the first SQP iteration
+  double L;
+  vc_kin_mpc w;
+  vc_obstacles obs;
+};
+
 // Fused dynamic-bicycle SQP step (dyn_sqp.hip), fp32.
 struct DynSqpArgs {
   const float* x0;     // [B][8]
@@ -163,6 +186,7 @@ hipError_t launch_kin_ltv(const KinLtvArgs& a, int N, hipStream_t stream);
 // Stagewise-Riccati kinematic LTV-MPC step (kin_ric.hip): the same contract, any built N
 // (KinLtvArgs.mode / H_out / g_out are not read).
 hipError_t launch_kin_ric(const KinLtvArgs& a, int N, hipStream_t stream);
+hipError_t launch_kin_merit(const KinMeritArgs& a, hipStream_t stream);
 bool kin_ric_built(int N);
 hipError_t launch_dyn_sqp(const DynSqpArgs& a, int N, hipStream_t stream);
 hipError_t launch_casc_sqp(const CascSqpArgs& a, int N, int M, hipStream_t stream);

@@ -28,6 +28,21 @@ IV, IS = 0, 2
 # step linearised around a far-off warm start can otherwise overshoot into a
 # region where the linearisation is meaningless (cos(epsi) -> 0).
 RTI_TRUST = {"trust_a": 1.0, "trust_w": 0.1}
+# With the obstacle barrier (``obstacles: True``, kinematic_mpc.py:130-133) one convexified
+# QP per control step is not enough: the controller takes KIN_OBS_SQP SQP steps, each with a
+# merit line search on the exact NLP cost (vc_qp.kin_sqp, csrc/kin_merit.hip, oracle/kin_sqp.py;
+# 0 of 64 vehicles touch an obstacle on ippodromo with 10 steps).
+KIN_OBS_SQP = 10
+
+
+def kin_qp_block(config) -> dict:
+    """The kinematic controller's `qp` block: RTI_TRUST, the globalised step when obstacles
+    are on, then the config's own `qp` entries."""
+    qp = dict(RTI_TRUST)
+    if config.get("obstacles"):
+        qp["kin_sqp"] = KIN_OBS_SQP
+    qp.update(config.get("qp") or {})
+    return qp
 
 
 def horizon_params(s0, v_pred, mpc_dt, k_of_s):
@@ -55,10 +70,8 @@ class BatchedKinematicMPC(Controller):
         self.dt = float(config["mpc_dt"])
         self.ns, self.na = len(car.state), len(car.input)
         self.B = int(batch)
-        qp = dict(RTI_TRUST)
-        qp.update(config.get("qp") or {})
         cfg = dict(config)
-        cfg["qp"] = qp
+        cfg["qp"] = kin_qp_block(config)
         self.ctx = Context(model=_abi.VC_MODEL_KINEMATIC, N=self.N, max_batch=self.B, dtype=_abi.VC_F64,
                            device=device, params=make_params(kin_car=car.config, kin_mpc=cfg,
                                                              obstacles=obstacle_list(car, config)))

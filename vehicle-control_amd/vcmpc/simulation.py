@@ -67,13 +67,12 @@ class BatchedRacingSimulator:
                 if dtype is None:
                     dtype = _abi.VC_F64 if self.N in ST_SQP_HORIZONS else _abi.VC_F32
         else:
-            # the kinematic controller's real-time-iteration trust region (controllers/
-            # kinematic_mpc.py RTI_TRUST) unless the config's qp block sets its own
-            from .controllers.kinematic_mpc import RTI_TRUST
-            qp = dict(RTI_TRUST)
-            qp.update(cfg.get("qp") or {})
+            # the kinematic controller's real-time-iteration trust region and, with obstacles,
+            # its globalised SQP step (controllers/kinematic_mpc.py kin_qp_block) unless the
+            # config's qp block sets its own
+            from .controllers.kinematic_mpc import kin_qp_block
             kcfg = dict(cfg)
-            kcfg["qp"] = qp
+            kcfg["qp"] = kin_qp_block(cfg)
             params = make_params(kin_car=car.config, kin_mpc=kcfg, obstacles=obstacle_list(track, cfg))
             model, dtype = _abi.VC_MODEL_KINEMATIC, _abi.VC_F64
         self.ctx = Context(model=model, N=self.N, max_batch=self.B, dtype=dtype, device=device, params=params)
@@ -107,8 +106,9 @@ class BatchedRacingSimulator:
 
     def _init_warm_start(self, seed):
         """The controllers' initial predictions: kinematic_mpc.py:64-68 (zeros, v = 0.1)
-        and cascaded_mpc.py:72-76 (ones, Ux + 3); actions 1 + U[0, 1), projected onto
-        the input box (see controllers/*.py)."""
+        and cascaded_mpc.py:72-76 (ones, Ux + 3); actions: the dynamic controller's
+        1 + U[0, 1) projected onto the input box (controllers/*.py), the kinematic
+        controller's neutral guess (see below)."""
         rng = np.random.RandomState(seed) if seed is not None else np.random
         B, N, H, ns, nx = self.B, self.N, self.H, self.ns, self.nx
         ic = self.config["input_constraints"]
@@ -123,8 +123,11 @@ class BatchedRacingSimulator:
             np.clip(ubar[:, :N, 1], ic["w_min"], ic["w_max"], out=ubar[:, :N, 1])
             self._fresh_tail = self.M > 0  # the point-mass tail gets the neutral guess at reset()
         else:
-            np.clip(ubar[..., 0], ic["a_min"], ic["a_max"], out=ubar[..., 0])
-            np.clip(ubar[..., 1], ic["w_min"], ic["w_max"], out=ubar[..., 1])
+            # the neutral guess (a = w = 0, the restart value of a failed step): the reference's
+            # 1 + U[0, 1) (kinematic_mpc.py:64-68) puts w at its bound on every stage, so the
+            # predicted steering leaves the delta box and the trust-region QP of the first step
+            # is infeasible for every vehicle (IPOPT has no trust region and recovers)
+            ubar[:] = 0.0
         self.xbar = self._to_dev(xbar.astype(self.np_dtype))
         self.ubar = self._to_dev(ubar.astype(self.np_dtype))
 
