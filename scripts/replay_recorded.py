@@ -1,0 +1,99 @@
+"""Open-loop replay of the reference's recorded closed-loop runs through the drop-in
+controllers (tests/golden/replay_kat.npz, make_replay_kat.py): at every recorded control step
+the controller gets the recorded state (and its own previous solution as the unshifted warm
+start, as the reference's controller does), and its first input is compared with the input
+IPOPT computed there (action_traj[n + 1]: racing.py:77-84 logs a zero action first and then
+the command made from state_traj[n] at :230-237), its plan with IPOPT's recorded plan (global x, y per stage).
+
+If the build's SQP converges to the same local optimum of the NLP as IPOPT, the two agree
+to solver tolerance; the script sweeps the SQP iteration count.
+
+    python scripts/replay_recorded.py [--sqp 3 5 10 20] [--runs cascaded7_ippodromo]
+"""
+import argparse
+import copy
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "vehicle-control_amd")]
+
+
+def config_for(run, rec):
+    """The build's config (its `qp` block) with the recorded run's horizons, weights and bounds."""
+    from vcmpc.config import load_config
+    cfg = copy.deepcopy(load_config("cascaded_mpc" if rec.get("horizon_pm", 0) else "singletrack_mpc"))
+    for k in ("horizon", "mpc_dt", "horizon_pm", "ds_pm"):
+        if k in rec:
+            cfg[k] = rec[k]
+    for k in ("cost_weights", "input_constraints", "state_constraints", "state_pm_constraints"):
+        if k in rec:
+            cfg[k] = dict(cfg.get(k) or {}, **rec[k])
+    return cfg
+
+
+def replay(run, g, rec, sqp, skip=5):
+    from vcmpc.config import load_config
+    from vcmpc.controllers.cascaded_mpc import BatchedCascadedMPC, BatchedSingleTrackMPC
+    from vcmpc.environment import Track
+    from vcmpc.models import DynamicCar
+    track = Track.load("ippodromo")
+    car = DynamicCar(load_config("dynamic_car"), track, tyre="fiala")
+    cfg = config_for(run, rec)
+    cfg["qp"] = dict(cfg["qp"], sqp_iters=sqp)
+    X, U, P = g[f"{run}/state_traj"], g[f"{run}/action_traj"], g[f"{run}/preds"]
+    ctl = (BatchedCascadedMPC if cfg.get("horizon_pm", 0) else BatchedSingleTrackMPC)(car, cfg, batch=1)
+    N = int(cfg["horizon"])
+    T = min(len(X), len(U))
+    du, dplan, nfail, us, dbg = [], [], 0, [], None
+    for n in range(T):
+        u = ctl.command(X[n][None])[0]
+        us.append(u)
+        nfail += int(ctl.status[0] != 0)
+        if n < skip:
+            continue
+        if n + 1 < len(U):   # racing.py:230-241: action_traj[n + 1] is the command at state_traj[n]
+            du.append(u - U[n + 1])
+        if n < len(P):
+            sp = ctl.state_prediction[0]
+            xy = np.array([track.rel2glob(sp[4, i], sp[5, i], sp[6, i])[:2] for i in range(min(N, 20))])
+            dplan.append(np.hypot(*(xy - P[n, :len(xy)]).T).max())
+            if dbg is None and n == 50:
+                dbg = dict(ours=xy[:3].tolist(), recorded=P[n, :3].tolist())
+    du, dplan = np.abs(np.array(du)), np.array(dplan)
+    us = np.array(us)
+    rel = du / np.maximum(np.abs(U[skip + 1:skip + 1 + len(du)]), [100.0, 0.01])
+    return dict(run=run, sqp=sqp, steps=T - skip, nonsolved=nfail,
+                dFx_median=float(np.median(du[:, 0])), dFx_p90=float(np.percentile(du[:, 0], 90)),
+                dFx_max=float(du[:, 0].max()), dw_median=float(np.median(du[:, 1])),
+                dw_p90=float(np.percentile(du[:, 1], 90)), dw_max=float(du[:, 1].max()),
+                plan_dev_median_m=float(np.nanmedian(dplan)), plan_dev_p90_m=float(np.nanpercentile(dplan, 90)),
+                plan_nan_steps=int(np.isnan(dplan).sum()),
+                Fx_scale=float(np.abs(U[:, 0]).max()), w_scale=float(np.abs(U[:, 1]).max()),
+                frac_within_1pct=float(np.mean((rel < 0.01).all(axis=1))), example_plan=dbg)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sqp", type=int, nargs="+", default=[3, 5, 10, 20])
+    ap.add_argument("--runs", nargs="+", default=["cascaded7_ippodromo", "singletrack_ippodromo"])
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    g = dict(np.load(os.path.join(ROOT, "tests", "golden", "replay_kat.npz"), allow_pickle=False))
+    recs = json.loads(str(g["configs"]))
+    res = []
+    for run in args.runs:
+        for sqp in args.sqp:
+            r = replay(run, g, recs[run], sqp)
+            res.append(r)
+            print(json.dumps(r), flush=True)
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,63 @@
+"""GPU: the build's SQP against the reference's own IPOPT solutions.  Open-loop replay of
+recorded closed-loop runs (tests/golden/replay_kat.npz, make_replay_kat.py): at every
+recorded control step the drop-in controller gets the recorded state (its own previous
+solution as the unshifted warm start, cascaded_mpc.py:320-321), and its first input is
+compared with the command IPOPT produced from that state (action_traj[n + 1]: racing.py:77-84
+logs a zero action first, then the command from state_traj[n] at :230-237), its plan with
+IPOPT's recorded plan (get_state_prediction, racing.py:239-240).
+
+The SQP's fixed point is a KKT point of the reference NLP (the Gauss-Newton model and the
+proximal term vanish at a fixed point, the frozen if_else branches match), so with enough
+SQP iterations the two solvers agree wherever they find the same local optimum.  Measured
+(scripts/replay_recorded.py, profiles/r02/replay.json): single-track N = 60 with 40 SQP
+iterations, median |dFx| 2e-5 N of |Fx| <= 6055 N and median |dw| < 1e-6; cascaded 20 + 40
+converges more slowly (median |dFx| 241 / 109 / 63 / 24 N at 5 / 10 / 20 / 40 iterations).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def data():
+    return dict(np.load(os.path.join(GOLDEN, "replay_kat.npz"), allow_pickle=False))
+
+
+def _replay(data, run, sqp):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(GOLDEN), "..", "scripts"))
+    from replay_recorded import replay
+    recs = json.loads(str(data["configs"]))
+    return replay(run, data, recs[run], sqp)
+
+
+def test_singletrack_replay_matches_ipopt(data):
+    """singletrack_ippodromo (config/controllers/singletrack.yaml: N = 60), 428 steps."""
+    r = _replay(data, "singletrack_ippodromo", 40)
+    print(json.dumps({k: v for k, v in r.items() if k != "example_plan"}))
+    assert r["nonsolved"] == 0
+    assert r["dFx_median"] < 0.01          # N (measured 2e-5)
+    assert r["dw_median"] < 1e-5           # rad/s
+    assert r["frac_within_1pct"] > 0.8      # measured 0.88
+    assert r["plan_dev_median_m"] < 1e-4    # global x, y over the first 20 stages
+    assert r["plan_dev_p90_m"] < 0.02
+
+
+def test_cascaded_replay_converges_to_ipopt(data):
+    """cascaded7_ippodromo (cascaded.yaml's N = 20 + M = 40 shape and weights), 413 steps:
+    the distance to IPOPT's commands shrinks with the SQP iterations."""
+    r10 = _replay(data, "cascaded7_ippodromo", 10)
+    r40 = _replay(data, "cascaded7_ippodromo", 40)
+    for r in (r10, r40):
+        print(json.dumps({k: v for k, v in r.items() if k != "example_plan"}))
+    assert r10["nonsolved"] == 0 and r40["nonsolved"] == 0
+    assert r40["dFx_median"] < 0.5 * r10["dFx_median"]
+    assert r40["dFx_median"] < 50.0         # N (measured 24 of |Fx| <= 6055)
+    assert r40["dw_median"] < 2e-3          # measured 4.5e-4
+    assert r40["plan_dev_median_m"] < 0.01  # measured 2e-3 m
