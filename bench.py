@@ -272,6 +272,7 @@ def run_c3(args, dev, stream, rank, dist, steps, f64=False, N=C3_N, cfg_name="dy
     st, it = status.cpu().numpy(), iters.cpu().numpy()
     solves, elapsed_max, kern_ms_max = dist.aggregate(float(B * steps), elapsed, kern_ms, dev)
     ctx.close()
+    sqp = int(load_config(cfg_name)["qp"]["sqp_iters"])
     if f64:
         flops = st_flops(float(it.mean()), N, sqp)
         word, kern, peak, bpsolve = 8, f"st_sqp_kernel<{N}, linear>", FP64_VALU_PEAK, c3_bytes(N, 8)
@@ -279,7 +280,6 @@ def run_c3(args, dev, stream, rank, dist, steps, f64=False, N=C3_N, cfg_name="dy
         flops = c3_flops(float(it.mean()))
         word, kern, peak, bpsolve = 4, "dyn_sqp_kernel<40, linear>", FP32_PEAK_TFS, C3_BYTES_PER_SOLVE
     dname = "fp64" if f64 else "fp32"
-    sqp = int(load_config(cfg_name)["qp"]["sqp_iters"])
     out = {"metric": f"MPC solves/sec (batched, N={N}, {sqp} SQP iterations)", "value": solves / elapsed_max,
            "unit": "solves/s", "steps": steps, "ms_per_step": elapsed_max / steps * 1e3,
            "dtype": "f64" if f64 else "f32",
