@@ -248,41 +248,35 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
 
     // ---------------- linearize + stage functions ----------------
     {
-      constexpr int NLIN = 4 * (N - 1), NSTF = 5 * N, NPM = 3 * (M - 1);
+      constexpr int NLIN = 8 * (N - 1), NSTF = 5 * N, NPM = 3 * (M - 1);
       using D2 = Dual<2, double>;
       using D1 = Dual<1, double>;
       // three task loops (one kind of work per loop: no divergent mix of the dual-number
       // evaluations in one iteration)
 #pragma unroll 1
       for (int task = l; task < NLIN; task += WTH) {
-        {  // single-track RK4 step k -> k + 1 (k < N - 1): two columns of [A6 | B6]
-          const int kk = task >> 2, pr = task & 3;
-          // seed pairs: (Ux, Uy), (r, delta), (ey, epsi), (Fx, w)
-          const int a0 = pr == 0 ? 0 : (pr == 1 ? 2 : (pr == 2 ? 5 : -1));
-          const int a1 = pr == 0 ? 1 : (pr == 1 ? 3 : (pr == 2 ? 6 : -1));
-          D2 x[8], u2[2], xn[8];
+        {  // single-track RK4 step k -> k + 1 (k < N - 1): one column of [A6 | B6] per task
+          // (one dual seed: half the registers of a seed pair, which made the Fiala build spill)
+          const int kk = task >> 3, col = task & 7;
+          // column -> seeded variable: (Ux, Uy, r, delta, ey, epsi | Fx, w)
+          const int a0 = col < 4 ? col : (col < 6 ? col + 1 : -1);
+          D1 x[8], u2[2], xn[8];
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
-            x[i] = D2(s.xs[kk][i]);
+            x[i] = D1(s.xs[kk][i]);
             x[i].d[0] = i == a0 ? 1.0 : 0.0;
-            x[i].d[1] = i == a1 ? 1.0 : 0.0;
           }
-          u2[0] = D2(s.ub[kk][0]);
-          u2[1] = D2(s.ub[kk][1]);
-          u2[0].d[0] = pr == 3 ? 1.0 : 0.0;
-          u2[1].d[1] = pr == 3 ? 1.0 : 0.0;
-          const D2 kp(s.kap[kk]);
-          rk4_apply<D2, 8>(x, D2(s.dsv[kk]), [&](const D2* xx, D2* f) { dyn_spatial_ode_alg<D2, double>(xx, u2, kp, c, f); }, xn);
-          const int c0 = pr < 3 ? 2 * pr : 6, c1 = c0 + 1;
-          const double s0 = pr == 3 ? S : 1.0;
+          u2[0] = D1(s.ub[kk][0]);
+          u2[1] = D1(s.ub[kk][1]);
+          u2[0].d[0] = col == 6 ? 1.0 : 0.0;
+          u2[1].d[0] = col == 7 ? 1.0 : 0.0;
+          const D1 kp(s.kap[kk]);
+          rk4_apply<D1, 8>(x, D1(s.dsv[kk]), [&](const D1* xx, D1* f) { dyn_spatial_ode_alg<D1, double>(xx, u2, kp, c, f); }, xn);
+          const double s0 = col == 6 ? S : 1.0;
           const int yr[6] = {0, 1, 2, 3, 5, 6};
 #pragma unroll
-          for (int r = 0; r < 6; ++r) {
-            s.J[kk][r][c0] = xn[yr[r]].d[0] * s0;
-            s.J[kk][r][c1] = xn[yr[r]].d[1];
-          }
-          s.u.l.trow[kk][c0] = xn[7].d[0] * s0;
-          s.u.l.trow[kk][c1] = xn[7].d[1];
+          for (int r = 0; r < 6; ++r) s.J[kk][r][col] = xn[yr[r]].d[0] * s0;
+          s.u.l.trow[kk][col] = xn[7].d[0] * s0;
         }
       }
 #pragma unroll 1
