@@ -58,7 +58,7 @@
 extern "C" {
 #endif
 
-#define VCMPC_ABI_VERSION 6
+#define VCMPC_ABI_VERSION 7
 #define VC_MAX_OBSTACLES 16
 
 typedef struct vc_ctx vc_ctx;
@@ -128,6 +128,11 @@ typedef struct vc_qp {
                        steps, each QP step followed by an Armijo line search on the exact NLP cost
                        + an L1 state-row penalty (kin_merit.hip, oracle/kin_sqp.py) -- the
                        globalised step for the obstacle barrier (kinematic_mpc.py:130-133) */
+  int32_t shift;    /* ABI 7: vc_simulate shifts a solved vehicle's warm start one stage ahead
+                       (stage k <- k + 1, the last stage kept) before the next step; 0 keeps the
+                       reference's unshifted warm start (kinematic_mpc.py:170-187).  Kinematic and
+                       single-track contexts (ignored for cascaded ones) */
+  int32_t pad_;
 } vc_qp;
 
 /* Cascaded controller: single-track stages followed by a point-mass tail

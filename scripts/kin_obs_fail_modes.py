@@ -106,8 +106,11 @@ def main():
         cat = ("infeasible" if pf > 1e-6 else "feasible") + ("; infeasible without trust" if pf0 > 1e-6
                                                             else "; feasible without trust")
         cat += "; |delta0| > delta_max" if abs(xk[1]) > dmax else ""
+        xr = Q.kin_predict(xk[None], ub[None], kap[None], ds[None], 2.5)[0]   # the warm start's rollout
+        cat += "; rollout |epsi| > pi/2" if np.abs(xr[:, 4]).max() > np.pi / 2 else ""
         cats[cat] = cats.get(cat, 0) + 1
-        print(f"  step {k} vehicle {b}: {cat} (pfeas {pf:.2e} / {pf0:.2e}); x {np.round(xk, 3)}; "
+        print(f"  step {k} vehicle {b}: {cat} (pfeas {pf:.2e} / {pf0:.2e}); rollout max |epsi| "
+              f"{np.abs(xr[:, 4]).max():.2f} max |delta| {np.abs(xr[:, 1]).max():.2f}; x {np.round(xk, 3)}; "
               f"ubar w [{ub[:, 1].min():.3f}, {ub[:, 1].max():.3f}] a [{ub[:, 0].min():.3f}, {ub[:, 0].max():.3f}]")
     print("  sampled non-solved steps:", cats)
 

@@ -154,6 +154,18 @@ __global__ void drive_kernel(ModelArgs m, TrackTable tt, double* x64, const T* u
     for (int k = 0; k < NS; ++k)
 #pragma unroll
       for (int i = 0; i < NX; ++i) xbar[((size_t)b * NS + k) * NX + i] = T(xn[i]);
+  } else if (m.shift && MODEL != VC_MODEL_CASCADED) {
+    // shifted warm start: the plan one stage on (single shooting re-rolls the warm-start inputs
+    // from the new state; unshifted, they lag one step and over a 40 m kinematic horizon the
+    // rollout crosses the spatial model's eps = +-pi/2 singularity, scripts/kin_shift_test.py)
+    const int N = m.N, NS = MODEL == VC_MODEL_KINEMATIC ? N + 1 : N;
+    for (int k = 0; k + 1 < N; ++k) {
+      ubar[((size_t)b * N + k) * 2] = ubar[((size_t)b * N + k + 1) * 2];
+      ubar[((size_t)b * N + k) * 2 + 1] = ubar[((size_t)b * N + k + 1) * 2 + 1];
+    }
+    for (int k = 0; k + 1 < NS; ++k)
+#pragma unroll
+      for (int i = 0; i < NX; ++i) xbar[((size_t)b * NS + k) * NX + i] = xbar[((size_t)b * NS + k + 1) * NX + i];
   }
 }
 

@@ -154,6 +154,7 @@ struct ModelArgs {
   int model;  // vc_model
   int B, N;
   int M;      // point-mass stages of a cascaded context (0 otherwise)
+  int shift;  // vc_qp.shift: advance a solved vehicle's warm start one stage after the step
   double L;   // kinematic wheelbase
   DynCoef<double> dyn64;
   DynCoef<float> dyn32;

@@ -122,6 +122,7 @@ vc::ModelArgs model_args(const vc_ctx* c, int B) {
   m.B = B;
   m.N = c->N;
   m.M = c->model == VC_MODEL_CASCADED ? c->p.casc.horizon_pm : 0;
+  m.shift = c->p.qp.shift;
   m.L = c->p.kin_car.l;
   m.dyn64 = vc::make_dyn_coef<double>(c->p.dyn_car);
   m.dyn32 = vc::make_dyn_coef<float>(c->p.dyn_car);

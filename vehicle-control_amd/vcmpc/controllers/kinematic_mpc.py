@@ -35,12 +35,22 @@ RTI_TRUST = {"trust_a": 1.0, "trust_w": 0.1}
 KIN_OBS_SQP = 10
 
 
+# Shifted warm start from this horizon on (vc_qp.shift): the reference keeps the previous
+# prediction unshifted (kinematic_mpc.py:170-187), harmless for IPOPT's multiple shooting; the
+# build's single-shooting step re-rolls the warm-start inputs from the new state, and over a
+# 40 m horizon the one-step lag makes that rollout cross the spatial model's eps = +-pi/2
+# singularity (N = 50: 52 of 64 vehicles off track unshifted, 0 shifted; scripts/kin_shift_test.py).
+KIN_SHIFT_FROM_N = 30
+
+
 def kin_qp_block(config) -> dict:
     """The kinematic controller's `qp` block: RTI_TRUST, the globalised step when obstacles
-    are on, then the config's own `qp` entries."""
+    are on, the shifted warm start at long horizons, then the config's own `qp` entries."""
     qp = dict(RTI_TRUST)
     if config.get("obstacles"):
         qp["kin_sqp"] = KIN_OBS_SQP
+    if int(config["horizon"]) >= KIN_SHIFT_FROM_N:
+        qp["shift"] = 1
     qp.update(config.get("qp") or {})
     return qp
 
@@ -72,6 +82,7 @@ class BatchedKinematicMPC(Controller):
         self.B = int(batch)
         cfg = dict(config)
         cfg["qp"] = kin_qp_block(config)
+        self.shift = bool(cfg["qp"].get("shift", 0))
         self.ctx = Context(model=_abi.VC_MODEL_KINEMATIC, N=self.N, max_batch=self.B, dtype=_abi.VC_F64,
                            device=device, params=make_params(kin_car=car.config, kin_mpc=cfg,
                                                              obstacles=obstacle_list(car, config)))
@@ -87,7 +98,8 @@ class BatchedKinematicMPC(Controller):
         """states[B, ns] -> actions[B, na] (u*_0 of every problem).
 
         The warm start is the previous solution, unshifted, as in the reference
-        (kinematic_mpc.py:175-176), projected onto the input box first: the LTV-QP
+        (kinematic_mpc.py:175-176) -- shifted one stage at horizons >= KIN_SHIFT_FROM_N
+        (vc_qp.shift) -- projected onto the input box first: the LTV-QP
         linearises around the warm-start rollout, and the reference's initial guess
         1 + U[0, 1) (kinematic_mpc.py:65-67) is far outside w_max = 0.4 (IPOPT
         recovers from that by globalisation; one QP step cannot).  A problem that
@@ -111,6 +123,9 @@ class BatchedKinematicMPC(Controller):
             u0[idx], xbar[idx], ustar[idx], status[idx], iters[idx] = r
         self.action_prediction = np.swapaxes(ustar, 1, 2).copy()
         self.state_prediction = np.swapaxes(xbar, 1, 2).copy()
+        if self.shift:  # vc_qp.shift, as vc_simulate does: the next warm start one stage on
+            self.action_prediction[:, :, :-1] = self.action_prediction[:, :, 1:].copy()
+            self.state_prediction[:, :, :-1] = self.state_prediction[:, :, 1:].copy()
         self.status, self.iters = status, iters
         return u0
 
