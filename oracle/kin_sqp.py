@@ -107,6 +107,32 @@ def line_search(x0, ubar, dz, kappa, ds, L, W):
     return alpha, phi0, phia, D
 
 
+def elastic_qp_step(x0, ubar, kappa, ds, L, W, rho=RHO, eps_t=1e-8, **qp_kw):
+    """The LTV-QP step with *elastic* state rows (v >= v_min, delta bounds): each row gets its own
+    slack t >= 0 with cost rho t (+ eps_t t^2 so the oracle's solver sees a definite Hessian), the
+    QP model of the merit's L1 penalty (Fletcher's Sl1QP).  Always feasible; equal to the plain
+    step whenever that is feasible with multipliers below rho.  Returns (u_star, kkt, t)."""
+    from .qp import solve_qp_batch
+    Qd = Q.kin_qp(x0, ubar, kappa, ds, L, W)
+    H, g, C, d = Qd["H"], Qd["g"], Qd["C"], Qd["d"]
+    B, n = g.shape
+    N = n // 2
+    ne = 3 * (N - 1)
+    nb = C.shape[1] - ne
+    H2 = np.zeros((B, n + ne, n + ne))
+    H2[:, :n, :n] = H
+    H2[:, n:, n:] = 2.0 * eps_t * np.eye(ne)
+    g2 = np.concatenate([g, np.full((B, ne), rho)], axis=1)
+    C2 = np.zeros((B, nb + 2 * ne, n + ne))
+    C2[:, :nb + ne, :n] = C
+    C2[:, nb:nb + ne, n:] = -np.eye(ne)
+    C2[:, nb + ne:, n:] = -np.eye(ne)
+    d2 = np.concatenate([d, np.zeros((B, ne))], axis=1)
+    sol = solve_qp_batch(H2, g2, C2, d2, **qp_kw)
+    dz = sol["z"][:, :n]
+    return np.asarray(ubar, np.float64) + dz.reshape(B, N, 2), sol["kkt"], sol["z"][:, n:]
+
+
 def kin_sqp_solve(x0, ubar, kappa, ds, L, W, sqp_iters, **qp_kw):
     """The globalised step: u_star[B,N,2], x_star[B,N+1,6] (x at u_star), per-iteration
     (alpha, phi0, phi, D, QP certificates)."""

@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--trust", default="rti", help="rti (1.0 / 0.1) or off")
     ap.add_argument("--N", type=int, default=0)
     ap.add_argument("--vehicle", type=int, default=-1, help="run only this vehicle of the 64 and trace it")
+    ap.add_argument("--elastic", action="store_true", help="elastic state rows (oracle/kin_sqp.py elastic_qp_step)")
+    ap.add_argument("--no-obstacles", action="store_true")
     args = ap.parse_args()
     from oracle import kin_sqp as KS
     from oracle import ltv_qp as Q
@@ -44,7 +46,7 @@ def main():
     W = Q.kin_weights(cfg)
     if args.trust == "rti":
         W.update(RTI_TRUST)
-    W["obstacles"] = obs
+    W["obstacles"] = [] if args.no_obstacles else obs
     rng = np.random.default_rng(3)
     B0 = 64
     x0 = np.zeros((B0, 6))
@@ -70,10 +72,14 @@ def main():
         u = ub.copy()
         fail = np.zeros(B, bool)
         for it in range(args.sqp):
-            sol = Q.kin_ltv_solve(x, u, kap, ds, L, W)
-            bad = (sol["kkt"]["pfeas"] > 1e-6) | ~np.isfinite(sol["u_star"]).all(axis=(1, 2))
+            if args.elastic:
+                ustar, kkt, _ = KS.elastic_qp_step(x, u, kap, ds, L, W)
+            else:
+                sol = Q.kin_ltv_solve(x, u, kap, ds, L, W)
+                ustar, kkt = sol["u_star"], sol["kkt"]
+            bad = (kkt["pfeas"] > 1e-6) | ~np.isfinite(ustar).all(axis=(1, 2))
             fail |= bad
-            dz = np.where(bad[:, None, None], 0.0, sol["u_star"] - u)
+            dz = np.where(bad[:, None, None], 0.0, ustar - u)
             if args.no_ls:
                 alpha = np.ones(B)
             else:
@@ -96,7 +102,7 @@ def main():
     X = np.array(X)
     clear = np.min([np.hypot(X[..., 2] - so, X[..., 3] - eo) - r for so, eo, r in obs], axis=0)
     al = np.array(alphas)
-    print(f"N={N} trust={args.trust} sqp={args.sqp} ls={not args.no_ls} B={B} steps={args.steps} ({time.time() - t0:.0f} s): "
+    print(f"N={N} elastic={args.elastic} obstacles={not args.no_obstacles} trust={args.trust} sqp={args.sqp} ls={not args.no_ls} B={B} steps={args.steps} ({time.time() - t0:.0f} s): "
           f"vehicles hitting an obstacle {(clear < 0).any(0).sum()}, min clearance {clear.min(0).round(2).tolist()}, "
           f"max |ey| {np.abs(X[..., 3]).max(0).round(2).tolist()}, failed steps {nfail.tolist()}, "
           f"final s {X[-1, :, 2].round(1).tolist()}, alpha<1 fraction {np.mean(al < 1):.3f}, alpha=0 {np.mean(al == 0):.3f}")
