@@ -58,7 +58,7 @@
 extern "C" {
 #endif
 
-#define VCMPC_ABI_VERSION 7
+#define VCMPC_ABI_VERSION 8
 #define VC_MAX_OBSTACLES 16
 
 typedef struct vc_ctx vc_ctx;
@@ -132,7 +132,10 @@ typedef struct vc_qp {
                        (stage k <- k + 1, the last stage kept) before the next step; 0 keeps the
                        reference's unshifted warm start (kinematic_mpc.py:170-187).  Kinematic and
                        single-track contexts (ignored for cascaded ones) */
-  int32_t pad_;
+  int32_t ms;       /* ABI 8, kinematic stagewise kernel: 1 = multiple shooting -- linearise at the
+                       warm-start states xbar (read from vc_solve's xbar, x0 replacing its first
+                       column) instead of the rollout of ubar; the defects enter as a linear
+                       offset (oracle/ltv_qp.py kin_qp(..., x_ws=)) */
 } vc_qp;
 
 /* Cascaded controller: single-track stages followed by a point-mass tail

@@ -90,18 +90,37 @@ def kin_condense(A, Bm):
     return G
 
 
-def kin_qp(x0, ubar, kappa, ds, L, W):
+def kin_qp(x0, ubar, kappa, ds, L, W, x_ws=None):
     """Steps 1-4.  Returns dict with xbar, G, H[B,n,n], g[B,n], and the inequality
-    system C[B,m,n] dz <= d[B,m] (one-sided rows, m = 4N + 3(N-1))."""
+    system C[B,m,n] dz <= d[B,m] (one-sided rows, m = 4N + 3(N-1)).
+
+    x_ws[B,N+1,6] given: *multiple shooting* (vc_qp.ms, csrc/kin_ric.hip).  The QP is linearised
+    at the warm-start states (x0 in column 0, s = s0 + cumsum ds since s' = 1) instead of the
+    rollout of ubar; the defects c_k = F(x_k, u_k) - x_{k+1} enter through their linear rollout
+    e (e_0 = 0, e_{k+1} = A_k e_k + c_k): dx_k = G_k dz + e_k.  Every `if_else` branch and the
+    obstacle model stay frozen at the warm-start states; the residuals they multiply are taken
+    at x_ws + e (the kernel's q + Q e, d - C e)."""
     x0 = np.asarray(x0, np.float64)
     ubar = np.asarray(ubar, np.float64)
     kappa = np.asarray(kappa, np.float64)
     ds = np.asarray(ds, np.float64)
     B, N = ubar.shape[:2]
     n = 2 * N
-    xbar = kin_predict(x0, ubar, kappa, ds, L)
+    if x_ws is None:
+        xbar = kin_predict(x0, ubar, kappa, ds, L)
+        eo = np.zeros_like(xbar)
+    else:
+        xbar = np.array(x_ws, np.float64, copy=True)
+        xbar[:, 0] = x0
+        xbar[:, 1:, IS] = x0[:, None, IS] + np.cumsum(ds, axis=1)
     A, Bm = kin_linearize(xbar, ubar, kappa, ds, L)
     G = kin_condense(A, Bm)
+    if x_ws is not None:
+        eo = np.zeros_like(xbar)
+        for k in range(N):
+            c = M.kin_spatial_transition(xbar[:, k], ubar[:, k], kappa[:, k], ds[:, k], L) - xbar[:, k + 1]
+            eo[:, k + 1] = np.einsum("bij,bj->bi", A[:, k], eo[:, k]) + c
+    xv = xbar + eo   # the values the residuals are taken at
 
     H = np.zeros((B, n, n))
     g = np.zeros((B, n))
@@ -115,17 +134,18 @@ def kin_qp(x0, ubar, kappa, ds, L, W):
     # stage costs on ey_n (n = 0 is constant: G[:,0] = 0)
     for k in range(1, N):
         ey = xbar[:, k, IEY]
+        eyv = xv[:, k, IEY]
         row = G[:, k, IEY]
-        add_square(W["w_dev"] * ds[:, k], ey, row)
+        add_square(W["w_dev"] * ds[:, k], eyv, row)
         lo = ey < W["ey_min"]
         hi = ey > W["ey_max"]
-        add_square(np.where(lo, W["w_b"] * ds[:, k], 0.0), ey - W["ey_min"], row)
-        add_square(np.where(hi, W["w_b"] * ds[:, k], 0.0), ey - W["ey_max"], row)
+        add_square(np.where(lo, W["w_b"] * ds[:, k], 0.0), eyv - W["ey_min"], row)
+        add_square(np.where(hi, W["w_b"] * ds[:, k], 0.0), eyv - W["ey_max"], row)
         if W.get("obstacles"):  # kinematic_mpc.py:130-133, convexified in ey (obstacles.py)
             p_o, q_o = OB.ey_model(xbar[:, k, IS], ey, W["w_obs"] * ds[:, k], W["obstacles"],
                                    W.get("obs_margin_min", OB.MARGIN_MIN))
             H[:] += q_o[:, None, None] * row[:, :, None] * row[:, None, :]
-            g[:] += p_o[:, None] * row
+            g[:] += (p_o + q_o * (eyv - ey))[:, None] * row
     # input costs: w_w w^2 and slew w_a (a_{n+1}-a_n)^2
     for k in range(N):
         e = np.zeros((B, n)); e[:, 2 * k + IW] = 1.0
@@ -135,10 +155,10 @@ def kin_qp(x0, ubar, kappa, ds, L, W):
         add_square(W["w_a"], ubar[:, k + 1, IA] - ubar[:, k, IA], e)
     # terminal costs
     vN = xbar[:, N, IV]
-    add_square(np.where(vN >= W["v_max"], W["w_v"], 0.0), vN - W["v_max"], G[:, N, IV])
+    add_square(np.where(vN >= W["v_max"], W["w_v"], 0.0), xv[:, N, IV] - W["v_max"], G[:, N, IV])
     g += W["w_time"] * G[:, N, IT]
-    add_square(W["w_ey"], xbar[:, N, IEY], G[:, N, IEY])
-    add_square(W["w_epsi"], xbar[:, N, IEP], G[:, N, IEP])
+    add_square(W["w_ey"], xv[:, N, IEY], G[:, N, IEY])
+    add_square(W["w_epsi"], xv[:, N, IEP], G[:, N, IEP])
     # proximal term prox*||dz||^2
     H += 2.0 * W["prox"] * np.eye(n)
 
@@ -155,25 +175,25 @@ def kin_qp(x0, ubar, kappa, ds, L, W):
             rows.append(e); rhs.append(up)
             rows.append(-e); rhs.append(dn)
     for k in range(1, N):
-        rows.append(-G[:, k, IV]); rhs.append(xbar[:, k, IV] - W["v_min"])
-        rows.append(G[:, k, ID]); rhs.append(W["delta_max"] - xbar[:, k, ID])
-        rows.append(-G[:, k, ID]); rhs.append(xbar[:, k, ID] - W["delta_min"])
+        rows.append(-G[:, k, IV]); rhs.append(xv[:, k, IV] - W["v_min"])
+        rows.append(G[:, k, ID]); rhs.append(W["delta_max"] - xv[:, k, ID])
+        rows.append(-G[:, k, ID]); rhs.append(xv[:, k, ID] - W["delta_min"])
     C = np.stack(rows, axis=1)
     d = np.stack(rhs, axis=1)
-    return dict(xbar=xbar, A=A, Bm=Bm, G=G, H=H, g=g, C=C, d=d)
+    return dict(xbar=xbar, e=eo, A=A, Bm=Bm, G=G, H=H, g=g, C=C, d=d)
 
 
-def kin_ltv_solve(x0, ubar, kappa, ds, L, W, **qp_kw):
+def kin_ltv_solve(x0, ubar, kappa, ds, L, W, x_ws=None, **qp_kw):
     """Steps 1-5 with the exact oracle QP solver.  Returns dict with u_star[B,N,2],
     x_star[B,N+1,6], u0[B,2], dz, lam, kkt (certificate), plus the QP data."""
     from .qp import solve_qp_batch
 
-    Q = kin_qp(x0, ubar, kappa, ds, L, W)
+    Q = kin_qp(x0, ubar, kappa, ds, L, W, x_ws=x_ws)
     B, N = np.asarray(ubar).shape[:2]
     sol = solve_qp_batch(Q["H"], Q["g"], Q["C"], Q["d"], **qp_kw)
     dz = sol["z"]
     u_star = np.asarray(ubar, np.float64) + dz.reshape(B, N, 2)
-    x_star = Q["xbar"] + np.einsum("bkin,bn->bki", Q["G"], dz)
+    x_star = Q["xbar"] + Q["e"] + np.einsum("bkin,bn->bki", Q["G"], dz)
     Q.update(sol)
     Q.update(dz=dz, u_star=u_star, x_star=x_star, u0=u_star[:, 0].copy())
     return Q

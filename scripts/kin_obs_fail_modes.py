@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--no-obstacles", action="store_true", help="the same loop without the barrier terms")
     ap.add_argument("--horizon", type=int, default=0, help="override the config's N (kin_ric above 20)")
     ap.add_argument("--kin-sqp", type=int, default=0, help="vc_qp.kin_sqp: SQP steps with the merit line search")
+    ap.add_argument("--ms", action="store_true", help="vc_qp.ms: multiple-shooting linearisation")
     args = ap.parse_args()
     from vcmpc.config import load_config
     from vcmpc.controllers.kinematic_mpc import RTI_TRUST
@@ -48,7 +49,7 @@ def main():
     if args.horizon:
         cfg["horizon"] = args.horizon
     trust = dict(RTI_TRUST) if args.trust == "rti" else {"trust_a": 0.0, "trust_w": 0.0}
-    cfg["qp"] = dict(cfg.get("qp") or {}, **trust, kin_sqp=args.kin_sqp)
+    cfg["qp"] = dict(cfg.get("qp") or {}, **trust, kin_sqp=args.kin_sqp, ms=int(args.ms))
     N = cfg["horizon"]
     car = KinematicCar(load_config("kinematic_car"), tr)
     sim = BatchedRacingSimulator(car, cfg, tr, batch=B)
@@ -85,7 +86,7 @@ def main():
           f"vehicles ever off track {off.any(0).sum()} of {B}; first off-track step median "
           f"{np.median([np.argmax(off[:, b]) for b in range(B) if off[:, b].any()]) if off.any() else None}; "
           f"final s median {np.median(X[-1, :, 2]):.1f}")
-    print(f"N={N} kin_sqp={args.kin_sqp} warm={args.warm} trust={args.trust}: non-solved steps {fails.sum()} of {K * B} "
+    print(f"N={N} kin_sqp={args.kin_sqp} ms={int(args.ms)} warm={args.warm} trust={args.trust}: non-solved steps {fails.sum()} of {K * B} "
           f"({fails.mean():.3%}); at step 0: {fails[0].sum()}; vehicles ever hitting: {hit.any(0).sum()} of {B}")
     # failures vs distance to the nearest obstacle
     near = clear[:-1] < 3.0

@@ -183,3 +183,41 @@ def test_kinematic_closed_loop_reference_horizon():
     assert (np.abs(X[:, :, 3]) < tr.width / 2).all()
     assert out["nfail"].sum() <= 0.01 * B * K
     assert np.median(X[-1, :, 2] - X[0, :, 2]) > 250.0
+
+
+def _ms_ctx(N, B, ms, obstacles=None, kin_sqp=0):
+    from vcmpc import Context, _abi
+    from vcmpc.config import load_config, make_params
+    cfg = load_config("kinematic_mpc")
+    cfg["horizon"] = N
+    cfg["qp"] = dict(cfg["qp"], solver=1, ms=ms, kin_sqp=kin_sqp)
+    p = make_params(kin_car=load_config("kinematic_car"), kin_mpc=cfg, obstacles=obstacles)
+    return cfg, Context(model=_abi.VC_MODEL_KINEMATIC, N=N, max_batch=B, dtype=_abi.VC_F64, params=p)
+
+
+@pytest.mark.parametrize("N", [20, 50])
+def test_kin_ric_multiple_shooting_vs_oracle(N):
+    """vc_qp.ms = 1: the QP linearised at given warm-start states (the rollout perturbed, so the
+    defects are nonzero) matches the oracle's multiple-shooting QP (oracle/ltv_qp.py
+    kin_qp(..., x_ws=)) to 1e-5; with consistent states (the rollout itself) it equals the
+    single-shooting step."""
+    from vcmpc.workload import kinematic_batch
+    d = kinematic_batch(16, N=N, seed=11 + N)
+    cfg, c1 = _ms_ctx(N, 16, 1)
+    W = Q.kin_weights(cfg)
+    xr = Q.kin_predict(d["x0"], d["ubar"], d["kappa"], d["ds"], 2.5)
+    rng = np.random.default_rng(N)
+    xw = xr.copy()
+    xw[:, 1:, [0, 1, 3, 4]] += rng.normal(scale=[0.05, 0.003, 0.02, 0.005], size=(16, N, 4))
+    with c1:
+        r = c1.solve(d["x0"], d["kappa"], d["ds"], d["ubar"].copy(), xbar=xw.copy())
+        rc = c1.solve(d["x0"], d["kappa"], d["ds"], d["ubar"].copy(), xbar=xr.copy())
+    ref = Q.kin_ltv_solve(d["x0"], d["ubar"], d["kappa"], d["ds"], 2.5, W, x_ws=xw)
+    ref_ss = Q.kin_ltv_solve(d["x0"], d["ubar"], d["kappa"], d["ds"], 2.5, W)
+    err = np.abs(r[2] - ref["u_star"]).max()
+    err_c = np.abs(rc[2] - ref_ss["u_star"]).max()
+    print(f"N={N}: multiple shooting |u* - u*_oracle| {err:.2e} (x* {np.abs(r[1] - ref['x_star']).max():.2e}); "
+          f"consistent states vs the single-shooting oracle {err_c:.2e}")
+    assert (r[3] == 0).all() and (rc[3] == 0).all()
+    assert err < 1e-5 and err_c < 1e-5
+    assert np.abs(r[1] - ref["x_star"]).max() < 1e-6

@@ -13,6 +13,8 @@
 // sufficient decrease (none, or a failed QP: alpha = 0), then the wavefront writes the
 // accepted inputs, lane 0 their rollout x* and u0, and the solve status / iteration count
 // accumulate over the SQP iterations (status: the first non-solved QP's; iterations: summed).
+// With multiple shooting (vc_qp.ms) the state iterate is carried along, x_prev + alpha (x* -
+// x_prev), instead of the rollout; the merit stays the single-shooting one of oracle/kin_sqp.py.
 #include <hip/hip_runtime.h>
 
 #include "vc_kernels.hpp"
@@ -105,13 +107,18 @@ __global__ __launch_bounds__(64) void kin_merit_kernel(KinMeritArgs A) {
   const double phia = pick >= 0 ? bcast(phi, pick) : phi0;
   const double* up = A.u_prev + (size_t)b * N * 2;
   double* ub = A.ubar + (size_t)b * N * 2;
+  if (A.ms) {  // multiple shooting: the state iterate moves with the inputs, x_prev + al (x* - x_prev)
+    double* xo = A.x_out + (size_t)b * (N + 1) * KIN_NX;
+    const double* xp = A.x_prev + (size_t)b * (N + 1) * KIN_NX;
+    for (int e = l; e < (N + 1) * KIN_NX; e += 64) xo[e] = xp[e] + al * (xo[e] - xp[e]);
+  }
   if (l == 0) {  // rollout of the accepted inputs (read before the wavefront overwrites u*)
     double x[KIN_NX];
-    double* xo = A.x_out + (size_t)b * (N + 1) * KIN_NX;
+    double* xo = A.ms ? nullptr : A.x_out + (size_t)b * (N + 1) * KIN_NX;
 #pragma unroll
     for (int i = 0; i < KIN_NX; ++i) {
       x[i] = A.x0[(size_t)b * KIN_NX + i];
-      xo[i] = x[i];
+      if (xo) xo[i] = x[i];
     }
     for (int n = 0; n < N; ++n) {
       const double u[2] = {up[2 * n] + al * (ub[2 * n] - up[2 * n]), up[2 * n + 1] + al * (ub[2 * n + 1] - up[2 * n + 1])};
@@ -124,7 +131,7 @@ __global__ __launch_bounds__(64) void kin_merit_kernel(KinMeritArgs A) {
 #pragma unroll
       for (int i = 0; i < KIN_NX; ++i) {
         x[i] = x[i] + A.ds[(size_t)b * N + n] * f[i];
-        xo[(n + 1) * KIN_NX + i] = x[i];
+        if (xo) xo[(n + 1) * KIN_NX + i] = x[i];
       }
     }
     const int32_t st_prev = A.first ? VC_SOLVED : A.st_acc[b];

@@ -55,6 +55,8 @@ __host__ __device__ constexpr int fcol(int j) { return j < 4 ? j : (j == 4 ? -1 
 template <int N>
 struct KrSmem {
   double xs[N + 1][6];  // prediction (becomes x* at the end)
+  double cdef[N][6];    // multiple shooting: defects F(xs_k, ub_k) - xs_{k+1}
+  double ew[N + 1][5];  // multiple shooting: their linear rollout e over (v, delta, ey, epsi | t)
   double ub[N][2];
   double kap[N], dsv[N];
   double F[N][4][6];    // [A4 | B4]: rows (v, delta, ey, epsi), cols (v, delta, ey, epsi | a, w)
@@ -130,8 +132,24 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
   if (l == 0) s.flag = VC_SOLVED;
   WSYNC();
 
+  const bool ms = A.qp.ms != 0;
+  if (ms) {  // multiple shooting: the warm-start states, x0 in column 0, s = s0 + sum ds (s' = 1)
+    for (int e = l; e < 6 * N; e += WTH) s.xs[1 + e / 6][e % 6] = A.x_in[(size_t)b * 6 * (N + 1) + 6 + e];
+    WSYNC();
+    if (l == 0) {
+      double sa = s.xs[0][2];
+      bool fin = true;
+      for (int kk = 0; kk < N; ++kk) {
+        sa += s.dsv[kk];
+        s.xs[kk + 1][2] = sa;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) fin = fin && isfinite(s.xs[kk + 1][i]);
+      }
+      if (!fin) s.flag = VC_NONFINITE;
+    }
+  }
   // ---------------- predict (lane 0, serial spatial Euler) ----------------
-  if (l == 0) {
+  if (!ms && l == 0) {
     double x[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) x[i] = s.xs[0][i];
@@ -176,6 +194,39 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
     s.tr[l][1] = 0.0;
     s.tr[l][2] = ds * J.qey;
     s.tr[l][3] = ds * J.qep;
+    if (ms) {  // defect of step l
+      const double u2[2] = {a, w};
+      double f[6];
+      kin_spatial_ode<double>(xk, u2, s.kap[l], A.L, f);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) s.cdef[l][i] = xk[i] + ds * f[i] - s.xs[l + 1][i];
+    }
+  }
+  WSYNC();
+  if (ms && l == 0) {  // e_0 = 0, e_{k+1} = A_k e_k + c_k over (v, delta, ey, epsi) and t
+    double e[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    constexpr int ix[4] = {0, 1, 3, 4};
+#pragma unroll
+    for (int a = 0; a < 5; ++a) s.ew[0][a] = 0.0;
+    for (int kk = 0; kk < N; ++kk) {
+      double en[5];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        double acc = s.cdef[kk][ix[r]];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc += s.F[kk][r][c] * e[c];
+        en[r] = acc;
+      }
+      double et = e[4] + s.cdef[kk][5];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) et += s.tr[kk][c] * e[c];
+      en[4] = et;
+#pragma unroll
+      for (int a = 0; a < 5; ++a) {
+        e[a] = en[a];
+        s.ew[kk + 1][a] = en[a];
+      }
+    }
   }
   WSYNC();
 
@@ -247,6 +298,13 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
     d[4] = s.xs[k][0] - W.v_min;
     d[5] = W.delta_max - s.xs[k][1];
     d[6] = s.xs[k][1] - W.delta_min;
+    if (ms) {  // v = e + w: linear terms q + Q e, row bounds d - C e (all stage-local)
+#pragma unroll
+      for (int a = 0; a < 4; ++a) qc[a] += Qc[D0 + a] * s.ew[k][a];
+      d[4] += s.ew[k][0];
+      d[5] -= s.ew[k][1];
+      d[6] += s.ew[k][1];
+    }
 #pragma unroll
     for (int i = 0; i < NRW; ++i) {
       m[i] = i < 4 ? mi : ms;
@@ -735,11 +793,13 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
     }
     const double dt = incl - c;  // sum over j < l
     if (stl) {
-      s.xs[k][0] += s.v[k][0];
-      s.xs[k][1] += s.v[k][1];
-      s.xs[k][3] += s.v[k][2];
-      s.xs[k][4] += s.v[k][3];
-      s.xs[k][5] += dt;
+      const double e0 = ms ? s.ew[k][0] : 0.0, e1 = ms ? s.ew[k][1] : 0.0, e2 = ms ? s.ew[k][2] : 0.0,
+                   e3 = ms ? s.ew[k][3] : 0.0, e4 = ms ? s.ew[k][4] : 0.0;
+      s.xs[k][0] += s.v[k][0] + e0;
+      s.xs[k][1] += s.v[k][1] + e1;
+      s.xs[k][3] += s.v[k][2] + e2;
+      s.xs[k][4] += s.v[k][3] + e3;
+      s.xs[k][5] += dt + e4;
       if (k < N) {
         s.ub[k][0] += s.v[k][5];
         s.ub[k][1] += s.v[k][6];

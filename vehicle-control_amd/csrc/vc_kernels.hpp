@@ -50,6 +50,7 @@ struct KinLtvArgs {
   const double* ubar;   // [B][N][2]  warm start (may alias u_out)
   double* u_out;        // [B][N][2]  u*
   double* x_out;        // [B][N+1][6] x*
+  const double* x_in;   // [B][N+1][6] warm-start states (multiple shooting, qp.ms; may alias x_out)
   double* u0;           // [B][2]
   int32_t* status;      // [B]
   int32_t* iters;       // [B]
@@ -71,7 +72,9 @@ struct KinMeritArgs {
   const double* ds;        // [B][N]
   const double* u_prev;    // [B][N][2]  iterate before this QP step
   double* ubar;            // [B][N][2]  in: the QP's u*; out: u_prev + alpha (u* - u_prev)
-  double* x_out;           // [B][N+1][6] rollout of the accepted iterate
+  double* x_out;           // [B][N+1][6] rollout of the accepted iterate (multiple shooting: in: the
+                           // QP's x*, out: x_prev + alpha (x* - x_prev))
+  const double* x_prev;    // [B][N+1][6] states before this QP step (multiple shooting only)
   double* u0;              // [B][2]
   const int32_t* qp_status;  // [B] this iteration's QP status (aliases status)
   const int32_t* qp_iters;   // [B] this iteration's QP iterations (aliases iters)
@@ -82,6 +85,7 @@ struct KinMeritArgs {
   double* ls_diag;         // [B][4] optional: alpha, phi(u_prev), phi(accepted), directional derivative
   int B, N;
   int first;               // 1 on the first SQP iteration
+  int ms;                  // multiple shooting (vc_qp.ms)
   double L;
   vc_kin_mpc w;
   vc_obstacles obs;

@@ -144,7 +144,7 @@ vc::TrackTable track_table(const vc_ctx* c) {
 // barriers, condition numbers ~1e6) need the stagewise factorisation's accuracy (kin_ric.hip
 // matches the oracle to 1e-8 there, the condensed normal equations to 8e-5; scripts/kin_sqp_debug.py)
 bool kin_condensed(const vc_ctx* c) {
-  return vc::kin_ltv_smem_bytes(c->N) > 0 && c->p.qp.solver == 0 && c->p.qp.kin_sqp <= 0;
+  return vc::kin_ltv_smem_bytes(c->N) > 0 && c->p.qp.solver == 0 && c->p.qp.kin_sqp <= 0 && !c->p.qp.ms;
 }
 bool kin_solve_built(const vc_ctx* c) {
   return c->model == VC_MODEL_KINEMATIC && c->dtype == VC_F64 && (kin_condensed(c) || vc::kin_ric_built(c->N));
@@ -488,7 +488,7 @@ int vc_solve_diag(vc_ctx* c, int B, const void* x0, const void* kappa, const voi
              {kappa, nullptr, (size_t)B * N * 8, nullptr},
              {ds, nullptr, (size_t)B * N * 8, nullptr},
              {ubar, ubar, (size_t)B * N * nu * 8, nullptr},
-             {nullptr, xbar, (size_t)B * (N + 1) * nx * 8, nullptr},
+             {c->p.qp.ms ? xbar : nullptr, xbar, (size_t)B * (N + 1) * nx * 8, nullptr},
              {nullptr, u0, (size_t)B * nu * 8, nullptr},
              {nullptr, status, (size_t)B * 4, nullptr},
              {nullptr, iters, (size_t)B * 4, nullptr},
@@ -516,6 +516,7 @@ int vc_solve_diag(vc_ctx* c, int B, const void* x0, const void* kappa, const voi
     a.iters = iters;
     a.diag = (double*)diag;
   }
+  a.x_in = a.x_out;  // multiple shooting (qp.ms): the warm-start states arrive in xbar
   const int S = c->p.qp.kin_sqp;
   if (S <= 0) {  // the LTV-QP contract: one QP step
     if (kin_condensed(c)) VC_HIP(c, vc::launch_kin_ltv(a, N, c->stream));
@@ -523,7 +524,7 @@ int vc_solve_diag(vc_ctx* c, int B, const void* x0, const void* kappa, const voi
   } else {
     // globalised step (oracle/kin_sqp.py): S x { QP step at ubar; merit line search }
     const size_t o_up = 0, o_st = al256((size_t)B * N * nu * 8), o_it = o_st + al256((size_t)B * 4),
-                 total = o_it + al256((size_t)B * 4);
+                 o_xp = o_it + al256((size_t)B * 4), total = o_xp + al256((size_t)B * (N + 1) * nx * 8);
     if (total > c->ls_bytes) {
       VC_HIP(c, hipStreamSynchronize(c->stream));
       if (c->ls) VC_HIP(c, hipFree(c->ls));
@@ -548,6 +549,8 @@ int vc_solve_diag(vc_ctx* c, int B, const void* x0, const void* kappa, const voi
     m.st_acc = (int32_t*)(base + o_st);
     m.it_acc = (int32_t*)(base + o_it);
     m.ls_diag = nullptr;
+    m.ms = c->p.qp.ms;
+    m.x_prev = (const double*)(base + o_xp);
     m.B = B;
     m.N = N;
     m.L = a.L;
@@ -555,6 +558,9 @@ int vc_solve_diag(vc_ctx* c, int B, const void* x0, const void* kappa, const voi
     m.obs = a.obs;
     for (int i = 0; i < S; ++i) {
       VC_HIP(c, hipMemcpyAsync(base + o_up, a.u_out, (size_t)B * N * nu * 8, hipMemcpyDeviceToDevice, c->stream));
+      if (m.ms)
+        VC_HIP(c, hipMemcpyAsync(base + o_xp, a.x_out, (size_t)B * (N + 1) * nx * 8, hipMemcpyDeviceToDevice,
+                                 c->stream));
       if (kin_condensed(c)) VC_HIP(c, vc::launch_kin_ltv(a, N, c->stream));
       else VC_HIP(c, vc::launch_kin_ric(a, N, c->stream));
       m.first = i == 0;
