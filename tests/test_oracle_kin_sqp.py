@@ -61,3 +61,24 @@ def test_line_search_accepts_only_sufficient_decrease():
     r = KS.kin_sqp_solve(d["x0"], d["ubar"], d["kappa"], d["ds"], 2.5, W, 3)
     phis = np.array([h["phi"] for h in r["hist"]])
     assert (np.diff(np.vstack([phi0, phis]), axis=0) <= 1e-9 * np.abs(phi0)).all()   # monotone merit
+
+
+def test_multiple_shooting_qp_restatement():
+    """oracle/ltv_qp.py kin_qp(x_ws=): with consistent warm-start states (the rollout of ubar)
+    the defects vanish and the QP is the single-shooting one; with perturbed states the solution
+    still satisfies the linearised dynamics x* = x_ws + e + G dz with e_{k+1} = A e_k + c_k."""
+    from vcmpc.workload import kinematic_batch
+    d = kinematic_batch(6, seed=12)
+    W = _W()
+    xr = Q.kin_predict(d["x0"], d["ubar"], d["kappa"], d["ds"], 2.5)
+    a = Q.kin_qp(d["x0"], d["ubar"], d["kappa"], d["ds"], 2.5, W)
+    b = Q.kin_qp(d["x0"], d["ubar"], d["kappa"], d["ds"], 2.5, W, x_ws=xr)
+    assert np.abs(b["e"]).max() < 1e-12
+    for k in ("H", "g", "C", "d"):
+        np.testing.assert_allclose(b[k], a[k], rtol=1e-12, atol=1e-12)
+    xw = xr.copy()
+    xw[:, 1:, 3] += 0.3                                     # shift ey: nonzero defects
+    c = Q.kin_qp(d["x0"], d["ubar"], d["kappa"], d["ds"], 2.5, W, x_ws=xw)
+    assert np.abs(c["e"][:, 1:, 3]).max() > 0.1
+    sol = Q.kin_ltv_solve(d["x0"], d["ubar"], d["kappa"], d["ds"], 2.5, W, x_ws=xw)
+    assert (sol["kkt"]["pfeas"] < 1e-8).all()
