@@ -32,17 +32,24 @@ through the obstacle, so a trajectory that passes through one is pushed out rath
 rewarded by the reference's negative values inside).  The device code is
 csrc/kin_merit.hip; the operation order below is the same.  Parity unpinned by the
 reference (IPOPT cannot run here; no recorded kinematic run exists).
+
+Multiple shooting (vc_qp.ms; ltv_qp.kin_qp(x_ws=)): the iterate is the pair (x, u); the QP step
+is taken at the state iterate x (x_0 = x0), the line search moves both, (x, u) + alpha (dx, du),
+and the merit evaluates every term at the state iterate instead of a rollout, plus an exact L1
+penalty RHO_DEF sum_n |F(x_n, u_n) - x_{n+1}|_1 on the defects (merit(..., x=)).
 """
 from __future__ import annotations
 
 import numpy as np
 
 from . import ltv_qp as Q
+from . import models as M
 
 LS_STEPS = 8        # alpha = 1 .. 2^-7
 ARMIJO = 1e-4
 EPS_FD = 1e-7
 RHO = 1e3           # L1 penalty on the state rows (above every multiplier seen in the contract's QPs)
+RHO_DEF = 1e3       # L1 penalty on the multiple-shooting defects
 IV, ID, IS, IEY, IEP, IT = Q.IV, Q.ID, Q.IS, Q.IEY, Q.IEP, Q.IT
 IA, IW = Q.IA, Q.IW
 
@@ -55,10 +62,28 @@ def barrier_ext(m, m0):
     return np.where(m >= m0, 1.0 / np.maximum(m, m0), ext)
 
 
-def merit(x0, u, kappa, ds, L, W):
-    """phi(u) per problem: x0[B,6], u[B,N,2], kappa/ds[B,N] -> [B]."""
-    x = Q.kin_predict(np.asarray(x0, np.float64), np.asarray(u, np.float64), kappa, ds, L)  # [B, N+1, 6]
+def defects(x0, x, u, kappa, ds, L):
+    """F(x_n, u_n) - x_{n+1} [B, N, 6] of a state iterate x[B, N+1, 6] (x_0 taken as x0)."""
+    x = np.array(x, np.float64, copy=True)
+    x[:, 0] = x0
     u = np.asarray(u, np.float64)
+    kappa, ds = np.asarray(kappa, np.float64), np.asarray(ds, np.float64)
+    xn = np.stack([M.kin_spatial_transition(x[:, n], u[:, n], kappa[:, n], ds[:, n], L)
+                   for n in range(u.shape[1])], axis=1)
+    return xn - x[:, 1:]
+
+
+def merit(x0, u, kappa, ds, L, W, x=None):
+    """phi(u) per problem: x0[B,6], u[B,N,2], kappa/ds[B,N] -> [B].  With a state iterate
+    x[B,N+1,6] (multiple shooting) the terms are evaluated on it, plus RHO_DEF |defects|_1."""
+    u = np.asarray(u, np.float64)
+    pdef = 0.0
+    if x is None:
+        x = Q.kin_predict(np.asarray(x0, np.float64), u, kappa, ds, L)  # [B, N+1, 6]
+    else:
+        pdef = RHO_DEF * np.abs(defects(x0, x, u, kappa, ds, L)).sum(axis=(1, 2))
+        x = np.array(x, np.float64, copy=True)
+        x[:, 0] = x0
     B, N = u.shape[:2]
     ds = np.asarray(ds, np.float64)
     ey = x[:, 1:N, IEY]
@@ -84,21 +109,23 @@ def merit(x0, u, kappa, ds, L, W):
     viol = (np.maximum(W["v_min"] - v, 0.0) + np.maximum(dl - W["delta_max"], 0.0)
             + np.maximum(W["delta_min"] - dl, 0.0))
     phi += RHO * np.sum(viol, axis=1)
-    return phi
+    return phi + pdef
 
 
-def line_search(x0, ubar, dz, kappa, ds, L, W):
-    """(alpha[B], phi0[B], phi_alpha[B], D[B]) of the rule in the module docstring."""
+def line_search(x0, ubar, dz, kappa, ds, L, W, x=None, dx=None):
+    """(alpha[B], phi0[B], phi_alpha[B], D[B]) of the rule in the module docstring (with a state
+    iterate x and its step dx under multiple shooting)."""
     ubar = np.asarray(ubar, np.float64)
-    phi0 = merit(x0, ubar, kappa, ds, L, W)
-    D = (merit(x0, ubar + EPS_FD * dz, kappa, ds, L, W) - phi0) / EPS_FD
+    xa = lambda a: None if x is None else x + a * dx
+    phi0 = merit(x0, ubar, kappa, ds, L, W, xa(0.0))
+    D = (merit(x0, ubar + EPS_FD * dz, kappa, ds, L, W, xa(EPS_FD)) - phi0) / EPS_FD
     B = len(phi0)
     alpha = np.zeros(B)
     phia = phi0.copy()
     done = D >= 0.0
     a = 1.0
     for _ in range(LS_STEPS):
-        pa = merit(x0, ubar + a * dz, kappa, ds, L, W)
+        pa = merit(x0, ubar + a * dz, kappa, ds, L, W, xa(a))
         ok = ~done & (pa <= phi0 + ARMIJO * a * D)
         alpha[ok] = a
         phia[ok] = pa[ok]
@@ -133,16 +160,24 @@ def elastic_qp_step(x0, ubar, kappa, ds, L, W, rho=RHO, eps_t=1e-8, **qp_kw):
     return np.asarray(ubar, np.float64) + dz.reshape(B, N, 2), sol["kkt"], sol["z"][:, n:]
 
 
-def kin_sqp_solve(x0, ubar, kappa, ds, L, W, sqp_iters, **qp_kw):
-    """The globalised step: u_star[B,N,2], x_star[B,N+1,6] (x at u_star), per-iteration
-    (alpha, phi0, phi, D, QP certificates)."""
+def kin_sqp_solve(x0, ubar, kappa, ds, L, W, sqp_iters, x_ws=None, **qp_kw):
+    """The globalised step: u_star[B,N,2], x_star[B,N+1,6] (x at u_star; under multiple
+    shooting, x_ws given, the state iterate), per-iteration (alpha, phi0, phi, D, QP certificates)."""
     u = np.array(ubar, np.float64, copy=True)
+    x = None
+    if x_ws is not None:
+        x = np.array(x_ws, np.float64, copy=True)
+        x[:, 0] = x0
+        x[:, 1:, IS] = x0[:, None, IS] + np.cumsum(ds, axis=1)     # s' = 1 (kin_ric.hip)
     hist = []
     for _ in range(sqp_iters):
-        sol = Q.kin_ltv_solve(x0, u, kappa, ds, L, W, **qp_kw)
+        sol = Q.kin_ltv_solve(x0, u, kappa, ds, L, W, x_ws=x, **qp_kw)
         dz = sol["u_star"] - u
-        alpha, phi0, phia, D = line_search(x0, u, dz, kappa, ds, L, W)
+        dx = None if x is None else sol["x_star"] - x
+        alpha, phi0, phia, D = line_search(x0, u, dz, kappa, ds, L, W, x, dx)
         hist.append(dict(alpha=alpha, phi0=phi0, phi=phia, D=D, kkt=sol["kkt"], polished=sol["polished"]))
         u = u + alpha[:, None, None] * dz
-    x_star = Q.kin_predict(np.asarray(x0, np.float64), u, kappa, ds, L)
+        if x is not None:
+            x = x + alpha[:, None, None] * dx
+    x_star = Q.kin_predict(np.asarray(x0, np.float64), u, kappa, ds, L) if x is None else x
     return dict(u_star=u, x_star=x_star, u0=u[:, 0].copy(), hist=hist)

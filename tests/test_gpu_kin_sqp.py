@@ -98,3 +98,34 @@ def test_kin_sqp_zero_is_the_ltv_contract(golden):
     W = Q.kin_weights(_cfg(0))
     ref = Q.kin_ltv_solve(d["x0"], d["ubar"], d["kappa"], d["ds"], 2.5, W)
     assert np.abs(r0[2] - ref["u_star"]).max() < U_TOL
+
+
+def test_kin_sqp_multiple_shooting_vs_oracle(golden):
+    """vc_qp.ms = 1 with kin_sqp = 3 on the obstacle golden problems from a perturbed state
+    iterate (nonzero defects): the (x, u) line search on the multiple-shooting merit
+    (oracle/kin_sqp.py merit(..., x=)) matches the oracle to 1e-5 on u*, x* is the state iterate."""
+    g = golden
+    obs = _obs(g)
+    S = 3
+    cfg = _cfg(S, 1)
+    cfg["qp"]["ms"] = 1
+    W = Q.kin_weights(cfg)
+    W["obstacles"] = obs
+    x0, ub, kap, ds = (g[k].astype(np.float64) for k in ("kin_x0", "kin_ubar", "kin_kappa", "kin_ds"))
+    xw = Q.kin_predict(x0, ub, kap, ds, 2.5)
+    xw[:, 1:, 3] += 0.03 * np.sin(0.7 * np.arange(xw.shape[1] - 1))
+    ref = KS.kin_sqp_solve(x0, ub, kap, ds, 2.5, W, S, x_ws=xw)
+    with _ctx(cfg, obs, len(x0)) as c:
+        u0, xs, us, st, it = c.solve(x0, kap, ds, ub.copy(), xbar=xw.copy())
+    err = np.abs(us - ref["u_star"]).max(axis=(1, 2))
+    ex = np.abs(xs - ref["x_star"]).max()
+    alphas = np.array([h["alpha"] for h in ref["hist"]])
+    print(f"ms: |u* - u*_oracle| max {err.max():.2e}, |x* - x*_oracle| {ex:.2e}; oracle step sizes "
+          f"{[np.unique(a).tolist() for a in alphas]}; status {np.bincount(st)}")
+    assert (st == 0).all(), st
+    assert err.max() < U_TOL, np.argsort(err)[-5:]
+    assert ex < 1e-6
+    np.testing.assert_array_equal(u0, us[:, 0])
+    phi_start = KS.merit(x0, ub, kap, ds, 2.5, W, x=xw)
+    phi_end = KS.merit(x0, us, kap, ds, 2.5, W, x=xs)
+    assert (phi_end <= phi_start + 1e-9 * np.abs(phi_start)).all()

@@ -82,3 +82,24 @@ def test_multiple_shooting_qp_restatement():
     assert np.abs(c["e"][:, 1:, 3]).max() > 0.1
     sol = Q.kin_ltv_solve(d["x0"], d["ubar"], d["kappa"], d["ds"], 2.5, W, x_ws=xw)
     assert (sol["kkt"]["pfeas"] < 1e-8).all()
+
+
+def test_multiple_shooting_merit_and_line_search():
+    """merit(x=): at the rollout state iterate it equals the single-shooting merit (no defects);
+    the multiple-shooting SQP from a perturbed state iterate never increases it and drives the
+    defects down (measured: 4.7 -> 0.13 in sum over 12 steps)."""
+    from vcmpc.workload import kinematic_batch
+    d = kinematic_batch(8, seed=21)
+    W = _W([(30.0, 0.0, 1.0)])
+    d["x0"][:, 2] = np.linspace(10.0, 25.0, 8)
+    xr = Q.kin_predict(d["x0"], d["ubar"], d["kappa"], d["ds"], 2.5)
+    np.testing.assert_allclose(KS.merit(d["x0"], d["ubar"], d["kappa"], d["ds"], 2.5, W, x=xr),
+                               KS.merit(d["x0"], d["ubar"], d["kappa"], d["ds"], 2.5, W), rtol=1e-13)
+    xw = xr.copy()
+    xw[:, 1:, 3] += 0.05 * np.sin(np.arange(xw.shape[1] - 1))
+    r = KS.kin_sqp_solve(d["x0"], d["ubar"], d["kappa"], d["ds"], 2.5, W, 12, x_ws=xw)
+    phi = np.array([r["hist"][0]["phi0"]] + [h["phi"] for h in r["hist"]])
+    assert (np.diff(phi, axis=0) <= 1e-9 * np.abs(phi[0])).all()
+    c0 = np.abs(KS.defects(d["x0"], xw, d["ubar"], d["kappa"], d["ds"], 2.5)).sum(axis=(1, 2))
+    c1 = np.abs(KS.defects(d["x0"], r["x_star"], r["u_star"], d["kappa"], d["ds"], 2.5)).sum(axis=(1, 2))
+    assert c1.sum() < 0.05 * c0.sum() and (c1 < c0).all()

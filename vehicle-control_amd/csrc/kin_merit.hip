@@ -13,8 +13,10 @@
 // sufficient decrease (none, or a failed QP: alpha = 0), then the wavefront writes the
 // accepted inputs, lane 0 their rollout x* and u0, and the solve status / iteration count
 // accumulate over the SQP iterations (status: the first non-solved QP's; iterations: summed).
-// With multiple shooting (vc_qp.ms) the state iterate is carried along, x_prev + alpha (x* -
-// x_prev), instead of the rollout; the merit stays the single-shooting one of oracle/kin_sqp.py.
+// With multiple shooting (vc_qp.ms) the iterate is the pair (x, u): the candidates are
+// (x_prev, u_prev) + alpha (x* - x_prev, u* - u_prev), the terms are evaluated on the state
+// candidate instead of a rollout (s = s0 + sum ds, s' = 1), plus RHO_DEF |F(x_n, u_n) - x_{n+1}|_1
+// on the defects (oracle/kin_sqp.py merit(..., x=)), and the accepted state iterate is x_out.
 #include <hip/hip_runtime.h>
 
 #include "vc_kernels.hpp"
@@ -28,6 +30,7 @@ constexpr int LS = 8;            // alpha = 1 .. 2^-7  (oracle/kin_sqp.py LS_STE
 constexpr double ARMIJO = 1e-4;  // sufficient-decrease constant
 constexpr double EPS_FD = 1e-7;  // directional-derivative step
 constexpr double RHO = 1e3;      // L1 penalty on the state rows
+constexpr double RHO_DEF = 1e3;  // L1 penalty on the multiple-shooting defects
 
 __device__ __forceinline__ double bcast(double v, int l) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
@@ -51,10 +54,12 @@ __device__ double merit(const KinMeritArgs& A, int b, double alpha) {
   const double* dsv = A.ds + (size_t)b * N;
   const double* up = A.u_prev + (size_t)b * N * 2;
   const double* uq = A.ubar + (size_t)b * N * 2;
+  const double* xq = A.x_out + (size_t)b * (N + 1) * KIN_NX;  // multiple shooting: QP's x*
+  const double* xp = A.x_prev + (size_t)b * (N + 1) * KIN_NX;
   double x[KIN_NX];
 #pragma unroll
   for (int i = 0; i < KIN_NX; ++i) x[i] = x0[i];
-  double blo = 0.0, bhi = 0.0, dev = 0.0, obs = 0.0, ww = 0.0, wa = 0.0, pen = 0.0, a_prev = 0.0;
+  double blo = 0.0, bhi = 0.0, dev = 0.0, obs = 0.0, ww = 0.0, wa = 0.0, pen = 0.0, a_prev = 0.0, pdef = 0.0;
   const double m0 = A.obs.margin_min;
   for (int n = 0; n < N; ++n) {
     const double u[2] = {up[2 * n] + alpha * (uq[2 * n] - up[2 * n]),
@@ -77,10 +82,20 @@ __device__ double merit(const KinMeritArgs& A, int b, double alpha) {
     a_prev = u[0];
     double f[KIN_NX];
     kin_spatial_ode<double>(x, u, kap[n], A.L, f);
+    if (A.ms) {
+      const int o = (n + 1) * KIN_NX;
 #pragma unroll
-    for (int i = 0; i < KIN_NX; ++i) x[i] = x[i] + ds * f[i];
+      for (int i = 0; i < KIN_NX; ++i) {
+        const double xn = i == 2 ? x[2] + ds : xp[o + i] + alpha * (xq[o + i] - xp[o + i]);
+        pdef += fabs(x[i] + ds * f[i] - xn);
+        x[i] = xn;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < KIN_NX; ++i) x[i] = x[i] + ds * f[i];
+    }
   }
-  double phi = blo + bhi + dev + obs + ww + wa;
+  double phi = blo + bhi + dev + obs + ww + wa + RHO_DEF * pdef;
   if (x[0] >= W.v_max) phi += W.w_v * (x[0] - W.v_max) * (x[0] - W.v_max);
   phi += W.w_time * x[5] + W.w_ey * x[3] * x[3] + W.w_epsi * x[4] * x[4];
   return phi + RHO * pen;
@@ -107,10 +122,13 @@ __global__ __launch_bounds__(64) void kin_merit_kernel(KinMeritArgs A) {
   const double phia = pick >= 0 ? bcast(phi, pick) : phi0;
   const double* up = A.u_prev + (size_t)b * N * 2;
   double* ub = A.ubar + (size_t)b * N * 2;
+  __syncthreads();  // every lane's merit reads of x* have completed
   if (A.ms) {  // multiple shooting: the state iterate moves with the inputs, x_prev + al (x* - x_prev)
     double* xo = A.x_out + (size_t)b * (N + 1) * KIN_NX;
     const double* xp = A.x_prev + (size_t)b * (N + 1) * KIN_NX;
-    for (int e = l; e < (N + 1) * KIN_NX; e += 64) xo[e] = xp[e] + al * (xo[e] - xp[e]);
+    for (int e = l; e < (N + 1) * KIN_NX; e += 64)
+      if (e < KIN_NX) xo[e] = A.x0[(size_t)b * KIN_NX + e];  // x_0 = x0
+      else if (e % KIN_NX != 2) xo[e] = xp[e] + al * (xo[e] - xp[e]);  // s stays s0 + sum ds
   }
   if (l == 0) {  // rollout of the accepted inputs (read before the wavefront overwrites u*)
     double x[KIN_NX];

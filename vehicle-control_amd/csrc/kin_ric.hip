@@ -280,7 +280,7 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
       qc[3] += 2.0 * W.w_epsi * s.xs[N][4];
     }
     // rows (:80-93; the optional trust region tightens the input boxes)
-    const double mi = (stl && k < N) ? 1.0 : 0.0, ms = (stl && k >= 1 && k < N) ? 1.0 : 0.0;
+    const double mi = (stl && k < N) ? 1.0 : 0.0, mx = (stl && k >= 1 && k < N) ? 1.0 : 0.0;
     const double ab = k < N ? s.ub[k][0] : 0.0, wb = k < N ? s.ub[k][1] : 0.0;
     double upa = W.a_max - ab, dna = ab - W.a_min, upw = W.w_max - wb, dnw = wb - W.w_min;
     if (A.qp.trust_a > 0) {
@@ -307,7 +307,7 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
     }
 #pragma unroll
     for (int i = 0; i < NRW; ++i) {
-      m[i] = i < 4 ? mi : ms;
+      m[i] = i < 4 ? mi : mx;
       if (m[i] == 0.0) d[i] = 1.0;
     }
   }
@@ -736,13 +736,13 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
       if (stl && m[i] > 0.0) amin = fmin(amin, fmin(step_to_bound(sl[i], dsa[i]), step_to_bound(la[i], dla[i])));
     }
     amin = wmin(amin);
-    double ms = 0.0;
+    double mua = 0.0;
     if (stl) {
 #pragma unroll
-      for (int i = 0; i < NRW; ++i) ms += m[i] * (sl[i] + amin * dsa[i]) * (la[i] + amin * dla[i]);
+      for (int i = 0; i < NRW; ++i) mua += m[i] * (sl[i] + amin * dsa[i]) * (la[i] + amin * dla[i]);
     }
-    ms = wsum(ms) / mcount;
-    const double ratio = mu > 0.0 ? fmin(1.0, ms / mu) : 0.0;
+    mua = wsum(mua) / mcount;
+    const double ratio = mu > 0.0 ? fmin(1.0, mua / mu) : 0.0;
     const double smu = ratio * ratio * ratio * mu;
 
     // (d) corrector: rc = s lam + ds_a dl_a - sigma mu
