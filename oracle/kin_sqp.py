@@ -36,7 +36,13 @@ reference (IPOPT cannot run here; no recorded kinematic run exists).
 Multiple shooting (vc_qp.ms; ltv_qp.kin_qp(x_ws=)): the iterate is the pair (x, u); the QP step
 is taken at the state iterate x (x_0 = x0), the line search moves both, (x, u) + alpha (dx, du),
 and the merit evaluates every term at the state iterate instead of a rollout, plus an exact L1
-penalty RHO_DEF sum_n |F(x_n, u_n) - x_{n+1}|_1 on the defects (merit(..., x=)).
+penalty RHO_DEF sum_n |F(x_n, u_n) - x_{n+1}|_1 on the defects (merit(..., x=)) -- unless the
+rollout of u has no larger merit, in which case the step is the plain single-shooting one
+(line_search_ms).  After each step the state iterate is reset to the rollout of u where the
+rollout's merit is no larger (a defect-free point).  So where the rollout is well behaved the
+iteration is the single-shooting SQP (the L1 defect penalty's second-order growth would
+otherwise reject every step of a long horizon: the Maratos effect), and where it runs through
+the eps = +-pi/2 singularity (merit huge or not finite) the multiple-shooting iterate carries on.
 """
 from __future__ import annotations
 
@@ -112,26 +118,57 @@ def merit(x0, u, kappa, ds, L, W, x=None):
     return phi + pdef
 
 
-def line_search(x0, ubar, dz, kappa, ds, L, W, x=None, dx=None):
-    """(alpha[B], phi0[B], phi_alpha[B], D[B]) of the rule in the module docstring (with a state
-    iterate x and its step dx under multiple shooting)."""
+def line_search(x0, ubar, dz, kappa, ds, L, W):
+    """(alpha[B], phi0[B], phi_alpha[B], D[B]) of the rule in the module docstring."""
     ubar = np.asarray(ubar, np.float64)
-    xa = lambda a: None if x is None else x + a * dx
-    phi0 = merit(x0, ubar, kappa, ds, L, W, xa(0.0))
-    D = (merit(x0, ubar + EPS_FD * dz, kappa, ds, L, W, xa(EPS_FD)) - phi0) / EPS_FD
+    phi0 = merit(x0, ubar, kappa, ds, L, W)
+    D = (merit(x0, ubar + EPS_FD * dz, kappa, ds, L, W) - phi0) / EPS_FD
     B = len(phi0)
     alpha = np.zeros(B)
     phia = phi0.copy()
     done = D >= 0.0
     a = 1.0
     for _ in range(LS_STEPS):
-        pa = merit(x0, ubar + a * dz, kappa, ds, L, W, xa(a))
+        pa = merit(x0, ubar + a * dz, kappa, ds, L, W)
         ok = ~done & (pa <= phi0 + ARMIJO * a * D)
         alpha[ok] = a
         phia[ok] = pa[ok]
         done |= ok
         a *= 0.5
     return alpha, phi0, phia, D
+
+
+def line_search_ms(x0, ubar, dz, x, dx, kappa, ds, L, W):
+    """The multiple-shooting line search: per problem, the merit is the single-shooting one
+    (the rollout of u) where that is no larger than the multiple-shooting one at the current
+    iterate ("roll" mode: the plain SQP of line_search), else merit(..., x=) along (dx, dz).
+    Returns (alpha, phi0, phi_alpha, D, reset): reset where the accepted point's rollout has no
+    larger merit than its state iterate (the next state iterate is then that rollout)."""
+    ubar = np.asarray(ubar, np.float64)
+    ps = lambda a: merit(x0, ubar + a * dz, kappa, ds, L, W)
+    pm = lambda a: merit(x0, ubar + a * dz, kappa, ds, L, W, x=x + a * dx)
+    ps0, pm0 = ps(0.0), pm(0.0)
+    roll = np.isfinite(ps0) & (ps0 <= pm0)
+    sel = lambda vs, vm: np.where(roll, vs, vm)
+    phi0 = sel(ps0, pm0)
+    D = (sel(ps(EPS_FD), pm(EPS_FD)) - phi0) / EPS_FD
+    B = len(phi0)
+    alpha = np.zeros(B)
+    phia = phi0.copy()
+    pr, pa_m = ps0.copy(), pm0.copy()
+    done = D >= 0.0
+    a = 1.0
+    for _ in range(LS_STEPS):
+        vs, vm = ps(a), pm(a)
+        pa = sel(vs, vm)
+        ok = ~done & (pa <= phi0 + ARMIJO * a * D)
+        alpha[ok] = a
+        phia[ok] = pa[ok]
+        pr[ok], pa_m[ok] = vs[ok], vm[ok]
+        done |= ok
+        a *= 0.5
+    reset = np.isfinite(pr) & (pr <= pa_m)
+    return alpha, phi0, phia, D, reset
 
 
 def elastic_qp_step(x0, ubar, kappa, ds, L, W, rho=RHO, eps_t=1e-8, **qp_kw):
@@ -173,11 +210,17 @@ def kin_sqp_solve(x0, ubar, kappa, ds, L, W, sqp_iters, x_ws=None, **qp_kw):
     for _ in range(sqp_iters):
         sol = Q.kin_ltv_solve(x0, u, kappa, ds, L, W, x_ws=x, **qp_kw)
         dz = sol["u_star"] - u
-        dx = None if x is None else sol["x_star"] - x
-        alpha, phi0, phia, D = line_search(x0, u, dz, kappa, ds, L, W, x, dx)
+        if x is None:
+            alpha, phi0, phia, D = line_search(x0, u, dz, kappa, ds, L, W)
+        else:
+            dx = sol["x_star"] - x
+            alpha, phi0, phia, D, reset = line_search_ms(x0, u, dz, x, dx, kappa, ds, L, W)
         hist.append(dict(alpha=alpha, phi0=phi0, phi=phia, D=D, kkt=sol["kkt"], polished=sol["polished"]))
         u = u + alpha[:, None, None] * dz
         if x is not None:
             x = x + alpha[:, None, None] * dx
+            x[reset] = Q.kin_predict(np.asarray(x0, np.float64)[reset], u[reset], np.asarray(kappa)[reset],
+                                     np.asarray(ds)[reset], L)
+            hist[-1]["reset"] = reset
     x_star = Q.kin_predict(np.asarray(x0, np.float64), u, kappa, ds, L) if x is None else x
     return dict(u_star=u, x_star=x_star, u0=u[:, 0].copy(), hist=hist)

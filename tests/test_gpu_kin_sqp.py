@@ -101,9 +101,11 @@ def test_kin_sqp_zero_is_the_ltv_contract(golden):
 
 
 def test_kin_sqp_multiple_shooting_vs_oracle(golden):
-    """vc_qp.ms = 1 with kin_sqp = 3 on the obstacle golden problems from a perturbed state
-    iterate (nonzero defects): the (x, u) line search on the multiple-shooting merit
-    (oracle/kin_sqp.py merit(..., x=)) matches the oracle to 1e-5 on u*, x* is the state iterate."""
+    """vc_qp.ms = 1 with kin_sqp = 3 on the obstacle golden problems, the state iterate a plan
+    that clears the obstacles (the rollout of the mean of ubar and a converged SQP solution;
+    nonzero defects): 15 of 44 problems start in the multiple-shooting merit, the rest in the
+    rollout's (oracle/kin_sqp.py line_search_ms).  u* matches the oracle to 1e-5, x* (the state
+    iterate, or the rollout where that was reset) to 1e-6, and the merit never increases."""
     g = golden
     obs = _obs(g)
     S = 3
@@ -112,8 +114,11 @@ def test_kin_sqp_multiple_shooting_vs_oracle(golden):
     W = Q.kin_weights(cfg)
     W["obstacles"] = obs
     x0, ub, kap, ds = (g[k].astype(np.float64) for k in ("kin_x0", "kin_ubar", "kin_kappa", "kin_ds"))
-    xw = Q.kin_predict(x0, ub, kap, ds, 2.5)
-    xw[:, 1:, 3] += 0.03 * np.sin(0.7 * np.arange(xw.shape[1] - 1))
+    good = KS.kin_sqp_solve(x0, ub, kap, ds, 2.5, W, 6)["u_star"]
+    xw = Q.kin_predict(x0, 0.5 * (ub + good), kap, ds, 2.5)
+    ps0 = KS.merit(x0, ub, kap, ds, 2.5, W)
+    pm0 = KS.merit(x0, ub, kap, ds, 2.5, W, x=xw)
+    assert (pm0 < ps0).sum() >= 10
     ref = KS.kin_sqp_solve(x0, ub, kap, ds, 2.5, W, S, x_ws=xw)
     with _ctx(cfg, obs, len(x0)) as c:
         u0, xs, us, st, it = c.solve(x0, kap, ds, ub.copy(), xbar=xw.copy())
@@ -121,11 +126,11 @@ def test_kin_sqp_multiple_shooting_vs_oracle(golden):
     ex = np.abs(xs - ref["x_star"]).max()
     alphas = np.array([h["alpha"] for h in ref["hist"]])
     print(f"ms: |u* - u*_oracle| max {err.max():.2e}, |x* - x*_oracle| {ex:.2e}; oracle step sizes "
-          f"{[np.unique(a).tolist() for a in alphas]}; status {np.bincount(st)}")
+          f"{[np.unique(a).tolist() for a in alphas]}; resets {[int(h['reset'].sum()) for h in ref['hist']]}; "
+          f"status {np.bincount(st)}")
     assert (st == 0).all(), st
     assert err.max() < U_TOL, np.argsort(err)[-5:]
     assert ex < 1e-6
     np.testing.assert_array_equal(u0, us[:, 0])
-    phi_start = KS.merit(x0, ub, kap, ds, 2.5, W, x=xw)
-    phi_end = KS.merit(x0, us, kap, ds, 2.5, W, x=xs)
-    assert (phi_end <= phi_start + 1e-9 * np.abs(phi_start)).all()
+    phi_end = np.minimum(KS.merit(x0, us, kap, ds, 2.5, W), KS.merit(x0, us, kap, ds, 2.5, W, x=xs))
+    assert (phi_end <= np.minimum(ps0, pm0) * (1 + 1e-9)).all()

@@ -98,8 +98,8 @@ def test_multiple_shooting_merit_and_line_search():
     xw = xr.copy()
     xw[:, 1:, 3] += 0.05 * np.sin(np.arange(xw.shape[1] - 1))
     r = KS.kin_sqp_solve(d["x0"], d["ubar"], d["kappa"], d["ds"], 2.5, W, 12, x_ws=xw)
-    phi = np.array([r["hist"][0]["phi0"]] + [h["phi"] for h in r["hist"]])
-    assert (np.diff(phi, axis=0) <= 1e-9 * np.abs(phi[0])).all()
+    for h in r["hist"]:                                   # each step is a sufficient decrease
+        assert (h["phi"] <= h["phi0"] + 1e-9 * np.abs(h["phi0"])).all()
     c0 = np.abs(KS.defects(d["x0"], xw, d["ubar"], d["kappa"], d["ds"], 2.5)).sum(axis=(1, 2))
     c1 = np.abs(KS.defects(d["x0"], r["x_star"], r["u_star"], d["kappa"], d["ds"], 2.5)).sum(axis=(1, 2))
     assert c1.sum() < 0.05 * c0.sum() and (c1 < c0).all()

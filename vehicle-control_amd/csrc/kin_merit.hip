@@ -16,7 +16,8 @@
 // With multiple shooting (vc_qp.ms) the iterate is the pair (x, u): the candidates are
 // (x_prev, u_prev) + alpha (x* - x_prev, u* - u_prev), the terms are evaluated on the state
 // candidate instead of a rollout (s = s0 + sum ds, s' = 1), plus RHO_DEF |F(x_n, u_n) - x_{n+1}|_1
-// on the defects (oracle/kin_sqp.py merit(..., x=)), and the accepted state iterate is x_out.
+// on the defects (oracle/kin_sqp.py merit(..., x=)), and the accepted state iterate is x_out --
+// or the rollout of the accepted inputs when its (defect-free) merit is no larger.
 #include <hip/hip_runtime.h>
 
 #include "vc_kernels.hpp"
@@ -46,7 +47,7 @@ __device__ __forceinline__ double barrier_ext(double m, double m0) {
 }
 
 // phi(u), u = up + alpha (uq - up), for one problem (oracle/kin_sqp.py merit)
-__device__ double merit(const KinMeritArgs& A, int b, double alpha) {
+__device__ double merit(const KinMeritArgs& A, int b, double alpha, bool msm) {
   const int N = A.N;
   const vc_kin_mpc& W = A.w;
   const double* x0 = A.x0 + (size_t)b * KIN_NX;
@@ -82,7 +83,7 @@ __device__ double merit(const KinMeritArgs& A, int b, double alpha) {
     a_prev = u[0];
     double f[KIN_NX];
     kin_spatial_ode<double>(x, u, kap[n], A.L, f);
-    if (A.ms) {
+    if (msm) {
       const int o = (n + 1) * KIN_NX;
 #pragma unroll
       for (int i = 0; i < KIN_NX; ++i) {
@@ -109,9 +110,18 @@ __global__ __launch_bounds__(64) void kin_merit_kernel(KinMeritArgs A) {
   double alpha = 0.0;
   if (l < LS) alpha = ldexp(1.0, -l);
   else if (l == LS) alpha = EPS_FD;
-  double phi = 0.0;
-  if (l <= LS + 1) phi = merit(A, b, alpha);
-  const double phi0 = bcast(phi, LS + 1);
+  // multiple shooting: both merits per candidate; the single-shooting one governs where the
+  // rollout of the current inputs has no larger merit than the state iterate ("roll" mode,
+  // oracle/kin_sqp.py line_search_ms), the multiple-shooting one elsewhere
+  double phs = 0.0, phm = 0.0;
+  if (l <= LS + 1) {
+    phs = merit(A, b, alpha, false);
+    if (A.ms) phm = merit(A, b, alpha, true);
+  }
+  const double ps0 = bcast(phs, LS + 1), pm0 = bcast(phm, LS + 1);
+  const bool roll = !A.ms || (isfinite(ps0) && ps0 <= pm0);
+  const double phi = roll ? phs : phm;
+  const double phi0 = roll ? ps0 : pm0;
   const double D = (bcast(phi, LS) - phi0) / EPS_FD;
   const bool qp_ok = A.qp_status[b] == VC_SOLVED;
   // lane 0..LS-1: sufficient decrease?  the first such lane (largest alpha) wins
@@ -122,8 +132,13 @@ __global__ __launch_bounds__(64) void kin_merit_kernel(KinMeritArgs A) {
   const double phia = pick >= 0 ? bcast(phi, pick) : phi0;
   const double* up = A.u_prev + (size_t)b * N * 2;
   double* ub = A.ubar + (size_t)b * N * 2;
+  // multiple shooting: the accepted state iterate is reset to the rollout of the accepted inputs
+  // when that has no larger merit (no defects; e.g. the reference's placeholder first guess)
+  const int src = pick >= 0 ? pick : LS + 1;
+  const double phr = bcast(phs, src), pma = bcast(phm, src);
+  const bool reset = A.ms && isfinite(phr) && phr <= pma;
   __syncthreads();  // every lane's merit reads of x* have completed
-  if (A.ms) {  // multiple shooting: the state iterate moves with the inputs, x_prev + al (x* - x_prev)
+  if (A.ms && !reset) {  // multiple shooting: the state iterate moves with the inputs, x_prev + al (x* - x_prev)
     double* xo = A.x_out + (size_t)b * (N + 1) * KIN_NX;
     const double* xp = A.x_prev + (size_t)b * (N + 1) * KIN_NX;
     for (int e = l; e < (N + 1) * KIN_NX; e += 64)
@@ -132,7 +147,7 @@ __global__ __launch_bounds__(64) void kin_merit_kernel(KinMeritArgs A) {
   }
   if (l == 0) {  // rollout of the accepted inputs (read before the wavefront overwrites u*)
     double x[KIN_NX];
-    double* xo = A.ms ? nullptr : A.x_out + (size_t)b * (N + 1) * KIN_NX;
+    double* xo = (A.ms && !reset) ? nullptr : A.x_out + (size_t)b * (N + 1) * KIN_NX;
 #pragma unroll
     for (int i = 0; i < KIN_NX; ++i) {
       x[i] = A.x0[(size_t)b * KIN_NX + i];
