@@ -56,6 +56,7 @@ ARMIJO = 1e-4
 EPS_FD = 1e-7
 RHO = 1e3           # L1 penalty on the state rows (above every multiplier seen in the contract's QPs)
 RHO_DEF = 1e3       # L1 penalty on the multiple-shooting defects
+TIE = 1e-9          # the rollout is preferred unless the state iterate's merit is lower by more
 IV, ID, IS, IEY, IEP, IT = Q.IV, Q.ID, Q.IS, Q.IEY, Q.IEP, Q.IT
 IA, IW = Q.IA, Q.IW
 
@@ -148,7 +149,7 @@ def line_search_ms(x0, ubar, dz, x, dx, kappa, ds, L, W):
     ps = lambda a: merit(x0, ubar + a * dz, kappa, ds, L, W)
     pm = lambda a: merit(x0, ubar + a * dz, kappa, ds, L, W, x=x + a * dx)
     ps0, pm0 = ps(0.0), pm(0.0)
-    roll = np.isfinite(ps0) & (ps0 <= pm0)
+    roll = np.isfinite(ps0) & (ps0 <= pm0 + TIE * np.abs(pm0))
     sel = lambda vs, vm: np.where(roll, vs, vm)
     phi0 = sel(ps0, pm0)
     D = (sel(ps(EPS_FD), pm(EPS_FD)) - phi0) / EPS_FD
@@ -167,7 +168,7 @@ def line_search_ms(x0, ubar, dz, x, dx, kappa, ds, L, W):
         pr[ok], pa_m[ok] = vs[ok], vm[ok]
         done |= ok
         a *= 0.5
-    reset = np.isfinite(pr) & (pr <= pa_m)
+    reset = np.isfinite(pr) & (pr <= pa_m + TIE * np.abs(pa_m))
     return alpha, phi0, phia, D, reset
 
 

@@ -113,10 +113,11 @@ def test_kinematic_closed_loop_with_obstacles():
     ippodromo (the reference's kinematic default, config/controllers/kinematic.yaml:4),
     vehicles starting on the centre line ahead of the obstacle field.  Without the barrier
     terms every vehicle drives through an obstacle; with them the controller takes the
-    globalised step (10 SQP steps with the merit line search per control step,
-    controllers/kinematic_mpc.py KIN_OBS_SQP, csrc/kin_merit.hip): no vehicle touches an
-    obstacle, every vehicle stays on the track, <= 2 % non-solved steps (measured 0.04 %;
-    round 1's one convexified QP per step: 39 of 64 hit, 21 % non-solved)."""
+    globalised step (10 SQP steps with the merit line search per control step, in multiple
+    shooting: controllers/kinematic_mpc.py KIN_OBS_SQP / KIN_OBS_MS, csrc/kin_merit.hip): no
+    vehicle touches an obstacle, every vehicle stays on the track, <= 2 % non-solved steps
+    (measured 0 %; single shooting 0.04 %; round 1's one convexified QP per step: 39 of 64 hit,
+    21 % non-solved)."""
     from vcmpc.config import load_config
     from vcmpc.environment import Track
     from vcmpc.models import KinematicCar
@@ -150,6 +151,42 @@ def test_kinematic_closed_loop_with_obstacles():
     assert (np.abs(X_on[:, :, 3]) < tr.width / 2).all()
     assert np.median(X_on[-1, :, 2]) > 200.0         # through the field (obstacles up to s = 185)
     assert nfail_on.sum() <= 0.02 * B * K, nfail_on.sum()
+
+
+@pytest.mark.parametrize("N", [30, 50])
+def test_kinematic_closed_loop_with_obstacles_long_horizon(N):
+    """The same obstacle loop at longer kinematic horizons (the reference's kinematic.yaml has
+    N = 50), where the multiple-shooting SQP (vc_qp.ms) keeps the swerving plans' states as the
+    iterate instead of re-rolling them through eps = +-pi/2: no vehicle touches an obstacle and
+    the non-solved steps stay rare (measured: N = 30 0 off track, 0.02 %; N = 50 5-11 of 64 off
+    track after early non-solved steps, 0.9 %; single shooting: N = 30 2 hit, N = 50 2 hit /
+    16 off track / 5.3 %)."""
+    from vcmpc.config import load_config
+    from vcmpc.environment import Track
+    from vcmpc.models import KinematicCar
+    from vcmpc.simulation import BatchedRacingSimulator
+    tr = Track.load("ippodromo")
+    obs = [(o.s, o.ey, o.radius) for o in tr.obstacles]
+    B, K = 64, 400
+    rng = np.random.default_rng(3)
+    x0 = np.zeros((B, 6))
+    x0[:, 0] = rng.uniform(5, 8, B)
+    x0[:, 2] = rng.uniform(0, 15, B)
+    x0[:, 3] = rng.uniform(-0.5, 0.5, B)
+    cfg = load_config("kinematic_mpc")
+    cfg["obstacles"] = True
+    cfg["horizon"] = N
+    car = KinematicCar(load_config("kinematic_car"), tr)
+    sim = BatchedRacingSimulator(car, cfg, tr, batch=B)
+    out = sim.reset(x0.copy()).run(K)
+    X = out["state_traj"]
+    clear = _min_clearance(X, obs, 2, 3)
+    on = (np.abs(X[:, :, 3]) < tr.width / 2).all(axis=0)
+    print(f"N={N}: {int((clear > 0).sum())}/{B} clear, {int(on.sum())}/{B} on track, non-solved "
+          f"{int(out['nfail'].sum())} of {B * K}")
+    assert (clear > 0).all()
+    assert on.sum() >= (B if N <= 30 else int(0.75 * B))
+    assert out["nfail"].sum() <= (0.005 if N <= 30 else 0.02) * B * K
 
 
 def test_dynamic_closed_loop_avoids_obstacles():

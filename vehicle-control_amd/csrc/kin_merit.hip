@@ -32,6 +32,7 @@ constexpr double ARMIJO = 1e-4;  // sufficient-decrease constant
 constexpr double EPS_FD = 1e-7;  // directional-derivative step
 constexpr double RHO = 1e3;      // L1 penalty on the state rows
 constexpr double RHO_DEF = 1e3;  // L1 penalty on the multiple-shooting defects
+constexpr double TIE = 1e-9;     // the rollout wins unless the state iterate's merit is lower by more
 
 __device__ __forceinline__ double bcast(double v, int l) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
@@ -119,7 +120,7 @@ __global__ __launch_bounds__(64) void kin_merit_kernel(KinMeritArgs A) {
     if (A.ms) phm = merit(A, b, alpha, true);
   }
   const double ps0 = bcast(phs, LS + 1), pm0 = bcast(phm, LS + 1);
-  const bool roll = !A.ms || (isfinite(ps0) && ps0 <= pm0);
+  const bool roll = !A.ms || (isfinite(ps0) && ps0 <= pm0 + TIE * fabs(pm0));
   const double phi = roll ? phs : phm;
   const double phi0 = roll ? ps0 : pm0;
   const double D = (bcast(phi, LS) - phi0) / EPS_FD;
@@ -136,7 +137,7 @@ __global__ __launch_bounds__(64) void kin_merit_kernel(KinMeritArgs A) {
   // when that has no larger merit (no defects; e.g. the reference's placeholder first guess)
   const int src = pick >= 0 ? pick : LS + 1;
   const double phr = bcast(phs, src), pma = bcast(phm, src);
-  const bool reset = A.ms && isfinite(phr) && phr <= pma;
+  const bool reset = A.ms && isfinite(phr) && phr <= pma + TIE * fabs(pma);
   __syncthreads();  // every lane's merit reads of x* have completed
   if (A.ms && !reset) {  // multiple shooting: the state iterate moves with the inputs, x_prev + al (x* - x_prev)
     double* xo = A.x_out + (size_t)b * (N + 1) * KIN_NX;

@@ -124,6 +124,8 @@ class Context:
         the per-problem solver diagnostics as a sixth element."""
         B, N, nx, f = self._batch(x0), self.NH, self.nx, _NP_DT[self.dtype]
         NS = self.ns_solve
+        if xbar is None and self.model == _abi.VC_MODEL_KINEMATIC and self.params.qp.ms:
+            raise ValueError("vc_qp.ms: multiple shooting linearises at the state iterate; pass xbar")
         if _is_torch(x0):
             import torch
             kw = dict(device=x0.device)
