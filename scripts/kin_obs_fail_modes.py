@@ -107,6 +107,14 @@ def main():
         cat = ("infeasible" if pf > 1e-6 else "feasible") + ("; infeasible without trust" if pf0 > 1e-6
                                                             else "; feasible without trust")
         cat += "; |delta0| > delta_max" if abs(xk[1]) > dmax else ""
+        if args.ms:   # the multiple-shooting QP at the state iterate (what the kernel solved first)
+            xw = np.array(xb, np.float64)
+            xw[0] = xk
+            xw[1:, 2] = xk[2] + np.cumsum(ds)          # s = s0 + sum ds (kin_ric.hip)
+            ms_ref = Q.kin_ltv_solve(xk[None], ub[None], kap[None], ds[None], 2.5, W, x_ws=xw[None])
+            pfm = float(ms_ref["kkt"]["pfeas"][0])
+            cat += "; MS QP " + ("infeasible" if pfm > 1e-6 else "feasible")
+            cat += " (max |defect| %.2g)" % float(np.abs(ms_ref["e"]).max()) if pfm > 1e-6 else ""
         xr = Q.kin_predict(xk[None], ub[None], kap[None], ds[None], 2.5)[0]   # the warm start's rollout
         cat += "; rollout |epsi| > pi/2" if np.abs(xr[:, 4]).max() > np.pi / 2 else ""
         cats[cat] = cats.get(cat, 0) + 1
