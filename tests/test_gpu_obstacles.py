@@ -116,7 +116,7 @@ def test_kinematic_closed_loop_with_obstacles():
     globalised step (10 SQP steps with the merit line search per control step, in multiple
     shooting: controllers/kinematic_mpc.py KIN_OBS_SQP / KIN_OBS_MS, csrc/kin_merit.hip): no
     vehicle touches an obstacle, every vehicle stays on the track, <= 2 % non-solved steps
-    (measured 0 %; single shooting 0.04 %; round 1's one convexified QP per step: 39 of 64 hit,
+    (measured 0.03 %; single shooting 0.04 %; round 1's one convexified QP per step: 39 of 64 hit,
     21 % non-solved)."""
     from vcmpc.config import load_config
     from vcmpc.environment import Track
@@ -158,9 +158,10 @@ def test_kinematic_closed_loop_with_obstacles_long_horizon(N):
     """The same obstacle loop at longer kinematic horizons (the reference's kinematic.yaml has
     N = 50), where the multiple-shooting SQP (vc_qp.ms) keeps the swerving plans' states as the
     iterate instead of re-rolling them through eps = +-pi/2: no vehicle touches an obstacle and
-    the non-solved steps stay rare (measured: N = 30 0 off track, 0.02 %; N = 50 5-11 of 64 off
-    track after early non-solved steps, 0.9 %; single shooting: N = 30 2 hit, N = 50 2 hit /
-    16 off track / 5.3 %)."""
+    the non-solved steps stay rare (measured: N = 30 0 off track, 0.02 %; N = 50 0.11 %, 10 of
+    64 vehicles cross the soft track boundary -- a cost term, kinematic_mpc.py:110-122 -- by up
+    to 1.7 m in one corner and come back; single shooting: N = 30 2 hit, N = 50 2 hit / 16 off
+    track / 5.3 %)."""
     from vcmpc.config import load_config
     from vcmpc.environment import Track
     from vcmpc.models import KinematicCar
@@ -186,7 +187,8 @@ def test_kinematic_closed_loop_with_obstacles_long_horizon(N):
           f"{int(out['nfail'].sum())} of {B * K}")
     assert (clear > 0).all()
     assert on.sum() >= (B if N <= 30 else int(0.75 * B))
-    assert out["nfail"].sum() <= (0.005 if N <= 30 else 0.02) * B * K
+    assert np.abs(X[:, :, 3]).max() < tr.width / 2 + 2.5          # bounded excursions, nobody lost
+    assert out["nfail"].sum() <= 0.005 * B * K
 
 
 def test_dynamic_closed_loop_avoids_obstacles():

@@ -12,7 +12,8 @@
 // thousand flops per lane, negligible next to the QP.  Lane 0 picks the first candidate with
 // sufficient decrease (none, or a failed QP: alpha = 0), then the wavefront writes the
 // accepted inputs, lane 0 their rollout x* and u0, and the solve status / iteration count
-// accumulate over the SQP iterations (status: the first non-solved QP's; iterations: summed).
+// accumulate over the SQP iterations (status: the first QP's -- a later QP's failure only
+// refuses its step; iterations: summed).
 // With multiple shooting (vc_qp.ms) the iterate is the pair (x, u): the candidates are
 // (x_prev, u_prev) + alpha (x* - x_prev, u* - u_prev), the terms are evaluated on the state
 // candidate instead of a rollout (s = s0 + sum ds, s' = 1), plus RHO_DEF |F(x_n, u_n) - x_{n+1}|_1
@@ -168,8 +169,9 @@ __global__ __launch_bounds__(64) void kin_merit_kernel(KinMeritArgs A) {
         if (xo) xo[(n + 1) * KIN_NX + i] = x[i];
       }
     }
-    const int32_t st_prev = A.first ? VC_SOLVED : A.st_acc[b];
-    const int32_t st = st_prev != VC_SOLVED ? st_prev : A.qp_status[b];
+    // the step's status is the first QP's: a later QP that fails only stops the progress (its
+    // step is refused, alpha = 0), the accepted iterate never has a larger merit than the start
+    const int32_t st = A.first ? A.qp_status[b] : A.st_acc[b];
     const int32_t it = (A.first ? 0 : A.it_acc[b]) + A.qp_iters[b];
     A.st_acc[b] = st;
     A.it_acc[b] = it;

@@ -78,7 +78,7 @@ struct KinMeritArgs {
   double* u0;              // [B][2]
   const int32_t* qp_status;  // [B] this iteration's QP status (aliases status)
   const int32_t* qp_iters;   // [B] this iteration's QP iterations (aliases iters)
-  int32_t* status;         // [B] accumulated: the first non-solved QP's status
+  int32_t* status;         // [B] the first QP's status (later failures refuse their step)
   int32_t* iters;          // [B] accumulated interior-point iterations
   int32_t* st_acc;         // [B] scratch accumulators
   int32_t* it_acc;         // [B]

@@ -46,8 +46,8 @@ KIN_SHIFT_FROM_N = 30
 # With obstacles the SQP runs in multiple shooting (vc_qp.ms): the previous plan's states are the
 # state iterate, so a swerving plan is never re-rolled from the new state through eps = +-pi/2
 # (ippodromo, 64 vehicles x 400 steps, 10 SQP steps: N = 50 single shooting 2 hit / 16 off
-# track / 5.3 % non-solved, multiple shooting 0 / 5-11 / 0.9 %; N = 30 2 / 1 / 0.7 % vs 0 / 0 /
-# 0.02 %; N = 20 0 / 0 / 0.04 % vs 0 / 0 / 0 %).
+# track / 5.3 % non-solved, multiple shooting 0 / 10 (soft boundary, <= 1.7 m) / 0.11 %;
+# N = 30 2 / 1 / 0.7 % vs 0 / 0 / 0.02 %; N = 20 0 / 0 / 0.04 % vs 0 / 0 / 0.03 %).
 KIN_OBS_MS = 1
 
 
