@@ -178,7 +178,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
   static_assert(N >= 2 && M >= 2 && H <= WTH, "one lane per stage");
   __shared__ CrSmem<N, M> s;
   const int l = threadIdx.x;
-  const int b = blockIdx.x;
+  const int b = xcd_problem(blockIdx.x, A.B);
   DynCoef<double> c = A.car;
   c.tyre = TYRE;
   const vc_dyn_mpc& W = A.w;

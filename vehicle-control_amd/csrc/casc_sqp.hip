@@ -513,7 +513,7 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
   constexpr int H = L::H, n = L::n;
   __shared__ CascSmem<N, M> s;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int b = blockIdx.x;
+  const int b = xcd_problem(blockIdx.x, A.B);
   DynCoef<double> c = A.car;
   c.tyre = TYRE;
   const vc_dyn_mpc& W = A.w;

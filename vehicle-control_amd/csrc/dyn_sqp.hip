@@ -638,7 +638,7 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
   constexpr int n = 2 * N;
   constexpr int NS = 4 * N;  // stage lanes
   __shared__ DynSmem<N> s;
-  const int b = blockIdx.x;
+  const int b = xcd_problem(blockIdx.x, A.B);
   // Thread coordinates are re-laundered (asm "+v") at the top of every solver loop so the
   // hundreds of LDS addresses derived from them are recomputed per iteration instead of
   // being hoisted out of the loops into live registers (which spilled to scratch).

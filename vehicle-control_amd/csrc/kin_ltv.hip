@@ -108,8 +108,6 @@ __device__ __forceinline__ lds_cdouble* lds_opaque(const double* p) {
 #endif
 enum { T_SWEEP = 0, T_SETUP, T_RESID, T_BUILD, T_CHOL, T_SOLVE, T_UPDATE, T_POLISH, T_OUT, T_NSLOT };
 
-// largest a in (0,1] keeping v + a dv >= 0
-__device__ __forceinline__ double step_bound(double v, double dv) { return dv < 0.0 ? -v / dv : 1.0; }
 
 template <int N>
 struct Dims {
@@ -450,7 +448,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
   // materialise each address in an SGPR and spill them)
   __shared__ Smem<N> s;
   const int lane = threadIdx.x;
-  const int b = blockIdx.x;
+  const int b = xcd_problem(blockIdx.x, A.B);
   if (b >= A.B) return;
   const vc_kin_mpc& W = A.w;
 
@@ -766,6 +764,13 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
         near = res <= 1e-6 * scale && mu <= tol;
         break;
       }
+      // inverse slacks / multipliers of this iteration (0 on absent sides): the two passes
+      // divide by them 16 times, and the fraction to the boundary min over -v/dv (dv < 0)
+      // is 1 / max over -dv (1/v)
+      const double islo_b = bx.hasLo ? rcp_nr(bx.slo) : 0.0, ishi_b = bx.hasHi ? rcp_nr(bx.shi) : 0.0;
+      const double islo_c = cs.hasLo ? rcp_nr(cs.slo) : 0.0, ishi_c = cs.hasHi ? rcp_nr(cs.shi) : 0.0;
+      const double illo_b = bx.hasLo ? rcp_nr(bx.llo) : 0.0, ilhi_b = bx.hasHi ? rcp_nr(bx.lhi) : 0.0;
+      const double illo_c = cs.hasLo ? rcp_nr(cs.llo) : 0.0, ilhi_c = cs.hasHi ? rcp_nr(cs.lhi) : 0.0;
       double sm = 0.0, pp1 = 0.0, pp2 = 0.0, pp3 = 0.0, pp4 = 0.0;
 #pragma unroll 1
       for (int pass = 0; pass < 2; ++pass) {
@@ -773,10 +778,10 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
         // complementarity residuals: affine (pass 0), Mehrotra corrector (pass 1)
         const double rclo_b = bx.slo * bx.llo + pp1 - sm, rchi_b = bx.shi * bx.lhi + pp2 - sm;
         const double rclo_c = cs.slo * cs.llo + pp3 - sm, rchi_c = cs.shi * cs.lhi + pp4 - sm;
-        const double eb = (bx.hasHi ? (-rchi_b / bx.shi - whi_b * rhi_b) : 0.0) +
-                          (bx.hasLo ? (rclo_b / bx.slo + wlo_b * rlo_b) : 0.0);
-        const double ec = (cs.hasHi ? (-rchi_c / cs.shi - whi_c * rhi_c) : 0.0) +
-                          (cs.hasLo ? (rclo_c / cs.slo + wlo_c * rlo_c) : 0.0);
+        const double eb = (bx.hasHi ? (-rchi_b * ishi_b - whi_b * rhi_b) : 0.0) +
+                          (bx.hasLo ? (rclo_b * islo_b + wlo_b * rlo_b) : 0.0);
+        const double ec = (cs.hasHi ? (-rchi_c * ishi_c - whi_c * rhi_c) : 0.0) +
+                          (cs.hasLo ? (rclo_c * islo_c + wlo_c * rlo_c) : 0.0);
         wave_sync();
         s.vc[lane] = (lane < NC) ? ec : 0.0;
         wave_sync();
@@ -789,17 +794,16 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
         wave_sync();
         const double dyc = grow_dot<N>(s, lane);
         const double d1 = bx.hasLo ? dz + rlo_b : 0.0;
-        const double d2 = bx.hasLo ? (-rclo_b / bx.slo - wlo_b * (dz + rlo_b)) : 0.0;
+        const double d2 = bx.hasLo ? (-rclo_b * islo_b - wlo_b * (dz + rlo_b)) : 0.0;
         const double d3 = bx.hasHi ? rhi_b - dz : 0.0;
-        const double d4 = bx.hasHi ? (-rchi_b / bx.shi - whi_b * (rhi_b - dz)) : 0.0;
+        const double d4 = bx.hasHi ? (-rchi_b * ishi_b - whi_b * (rhi_b - dz)) : 0.0;
         const double e1 = cs.hasLo ? dyc + rlo_c : 0.0;
-        const double e2 = cs.hasLo ? (-rclo_c / cs.slo - wlo_c * (dyc + rlo_c)) : 0.0;
+        const double e2 = cs.hasLo ? (-rclo_c * islo_c - wlo_c * (dyc + rlo_c)) : 0.0;
         const double e3 = cs.hasHi ? rhi_c - dyc : 0.0;
-        const double e4 = cs.hasHi ? (-rchi_c / cs.shi - whi_c * (rhi_c - dyc)) : 0.0;
-        const double amax = fmin(1.0, wave_min(fmin(fmin(fmin(step_bound(bx.slo, d1), step_bound(bx.llo, d2)),
-                                                         fmin(step_bound(bx.shi, d3), step_bound(bx.lhi, d4))),
-                                                    fmin(fmin(step_bound(cs.slo, e1), step_bound(cs.llo, e2)),
-                                                         fmin(step_bound(cs.shi, e3), step_bound(cs.lhi, e4))))));
+        const double e4 = cs.hasHi ? (-rchi_c * ishi_c - whi_c * (rhi_c - dyc)) : 0.0;
+        const double tmax = wave_max(fmax(fmax(fmax(-d1 * islo_b, -d2 * illo_b), fmax(-d3 * ishi_b, -d4 * ilhi_b)),
+                                          fmax(fmax(-e1 * islo_c, -e2 * illo_c), fmax(-e3 * ishi_c, -e4 * ilhi_c))));
+        const double amax = 1.0 / fmax(1.0, tmax);  // largest a in (0, 1] keeping every v + a dv >= 0
         if (pass == 0) {
           const double mua = wave_sum((bx.slo + amax * d1) * (bx.llo + amax * d2) +
                                       (bx.shi + amax * d3) * (bx.lhi + amax * d4) +

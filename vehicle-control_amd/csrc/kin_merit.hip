@@ -105,7 +105,7 @@ __device__ double merit(const KinMeritArgs& A, int b, double alpha, bool msm) {
 }
 
 __global__ __launch_bounds__(64) void kin_merit_kernel(KinMeritArgs A) {
-  const int b = blockIdx.x;
+  const int b = xcd_problem(blockIdx.x, A.B);
   const int l = threadIdx.x;
   const int N = A.N;
   // candidate of this lane

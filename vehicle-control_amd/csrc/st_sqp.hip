@@ -190,7 +190,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
   static_assert(N >= 2 && N <= WTH, "one lane per stage");
   __shared__ StSmem<N> s;
   const int l = threadIdx.x;
-  const int b = blockIdx.x;
+  const int b = xcd_problem(blockIdx.x, A.B);
   DynCoef<double> c = A.car;
   c.tyre = TYRE;
   const vc_dyn_mpc& W = A.w;

@@ -13,6 +13,36 @@
 
 namespace vc {
 
+// Problem owned by workgroup g of a one-workgroup-per-problem launch (grid = B).
+// Workgroups are dealt round-robin over the 8 XCDs (g and g + 8 share one L2), so the
+// identity mapping puts neighbouring problems -- whose rows of x0 / kappa / ds / the warm
+// start share 128-B lines -- on different XCDs, and every shared line is fetched into
+// (and written back from) two L2s.  This mapping gives XCD slot g % 8 the contiguous
+// problem range [(g % 8) q, (g % 8 + 1) q), q = B / 8; the B % 8 tail keeps the identity.
+// A bijection on [0, B); placement is a speed hint only (correctness never depends on it).
+__device__ __forceinline__ int xcd_problem(int g, int B) {
+  const int q = B >> 3;
+  return g < 8 * q ? (g & 7) * q + (g >> 3) : g;
+}
+
+// 1/x to full fp64 accuracy: hardware v_rcp_f64 + two Newton steps (five VALU ops against
+// the ~11-op div_scale / div_fmas / div_fixup sequence of an IEEE divide).  x = +-inf or 0
+// (an unbounded row's slack, a zero step component) makes the Newton residual NaN; the
+// hardware reciprocal is then the IEEE 1/x (0 or inf) and is returned as is, so products
+// such as la * rcp_nr(sl) behave exactly like la / sl.  Used by kin_ltv only, whose interior
+// slacks and multipliers are never floored: the Riccati kernels floor theirs at 1e-300,
+// and the same substitution there made every step of st_sqp's Fiala closed loop fail
+// (DESIGN 3.1), so they keep the IEEE divide (whose div_scale pre-scaling covers the
+// full exponent range).
+__device__ __forceinline__ double rcp_nr(double x) {
+  const double r0 = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, r0, 1.0);
+  double r = fma(r0, e, r0);
+  e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  return isfinite(r) ? r : r0;
+}
+
 // Obstacle barrier of one stage as a convexified quadratic in ey:
 //   phi(ey) = sum_j w ds / (d_j - (r_j + 0.1)),  d_j = |(s, ey) - (s_j, ey_j)|
 // (kinematic_mpc.py:130-133, cascaded_mpc.py:173-176).  s is not a decision function
