@@ -352,6 +352,20 @@ __device__ __forceinline__ void build_normal(double (&Mr)[Dims<N>::n], const Sme
   for (int i = 0; i < n; ++i) Mr[i] = (lane < n) ? Mr[i] : 0.0;
 }
 
+// Does MFMA k-step ks (G rows 4 ks .. 4 ks + 3) touch block-row I of the lower block
+// triangle?  Row r of G is zero beyond column 2 crow_stage(r) (stage k's sensitivity sees
+// only the inputs of stages < k), so a k-step whose four rows all end at or before
+// column 16 I adds exact zeros to every tile (I, J <= I) and is skipped.  N = 20: 33 of
+// the 60 tile-steps remain (block-row 0: 10 k-steps, 1: 7, 2: 3).
+template <int N>
+__host__ __device__ constexpr bool kstep_hits(int ks, int I) {
+  for (int q = 0; q < 4; ++q) {
+    const int r = 4 * ks + q;
+    if (r < Dims<N>::NC && 2 * crow_stage<N>(r) > 16 * I) return true;
+  }
+  return false;
+}
+
 // The same normal matrix with the constraint part C'WC on the matrix cores:
 // M_c = (W G)' G as 16x16 tiles of v_mfma_f64_16x16x4_f64 (K = the NC rows of G,
 // 4 per step; only the lower block triangle), then moved from the MFMA
@@ -395,7 +409,8 @@ __device__ __forceinline__ void build_normal_mfma(double (&Mr)[Dims<N>::n], Smem
     for (int I = 0, t = 0; I < NB; ++I) {
       const double a = wk[ks] * g[I];
 #pragma unroll
-      for (int J = 0; J <= I; ++J, ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, g[J], acc[t], 0, 0, 0);
+      for (int J = 0; J <= I; ++J, ++t)
+        if (kstep_hits<N>(ks, I)) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, g[J], acc[t], 0, 0, 0);
     }
   }
   // Mr = H row + diag, then add this lane's row of M_c block-row by block-row
