@@ -240,6 +240,13 @@ int vc_solve_debug(vc_ctx* ctx, int B, const void* x0, const void* kappa, const 
                    void* u0, int32_t* status, int32_t* iters, void* dbg, int flags);
 int vc_debug_stride(void);
 
+/* Test hook (kinematic SQP contexts, vc_qp.kin_sqp > 0): after the QP of SQP iteration
+ * `sqp_iter` (0-based), problem `problem`'s QP output is replaced by NaN with status
+ * VC_NONFINITE -- a QP that failed with non-finite output -- so tests can check that the
+ * merit line search refuses the step and keeps the previous iterate.  sqp_iter < 0 turns
+ * it off (the default).  No reference counterpart. */
+int vc_debug_qp_fault(vc_ctx* ctx, int sqp_iter, int problem);
+
 /* Predict: xbar[B][N+1][nx] from x0[B][nx] and ubar[B][N][nu] (spatial step). */
 int vc_rollout(vc_ctx* ctx, int B, const void* x0, const void* ubar, const void* kappa,
                const void* ds, void* xbar, int flags);
@@ -300,8 +307,10 @@ int vc_drive(vc_ctx* ctx, int B, double* x64, const void* u0, double dt, void* x
  * x64[B][nx] fp64 in/out (plant state), xbar/ubar the warm starts in/out (context
  * dtype, shapes of vc_solve).  A problem whose status is not VC_SOLVED applies the
  * neutral input u = 0, increments nfail[b] (int32, may be NULL; not cleared), and restarts
- * from the neutral warm start (ubar = 0, xbar = the new state) -- in the reference a
- * failed IPOPT solve raises and the simulator's catch-all drops the step (racing.py:416-423).
+ * from the neutral warm start (ubar = 0, xbar = the new state).  This is the build's own
+ * policy: in the reference a failed IPOPT solve raises, step()'s catch-all prints it and
+ * returns None (racing.py:416-423), and the caller's unpacking `action, state = self.step(...)`
+ * (racing.py:232) raises TypeError, which ends the run.
  * Optional logs (may be NULL): log_x[steps+1][B][nx] fp64 (the state before each step
  * and after the last), log_u[steps][B][nu] context dtype (the applied u0).
  * Requires vc_track_set and a built vc_solve combination. */

@@ -217,9 +217,12 @@ def kin_sqp_solve(x0, ubar, kappa, ds, L, W, sqp_iters, x_ws=None, **qp_kw):
             dx = sol["x_star"] - x
             alpha, phi0, phia, D, reset = line_search_ms(x0, u, dz, x, dx, kappa, ds, L, W)
         hist.append(dict(alpha=alpha, phi0=phi0, phi=phia, D=D, kkt=sol["kkt"], polished=sol["polished"]))
-        u = u + alpha[:, None, None] * dz
+        # a refused step (alpha = 0) keeps the iterate as it is: u + 0 * dz would carry a failed
+        # QP's non-finite output into it (kin_merit.hip step_to)
+        acc = (alpha > 0.0)[:, None, None]
+        u = np.where(acc, u + alpha[:, None, None] * dz, u)
         if x is not None:
-            x = x + alpha[:, None, None] * dx
+            x = np.where(acc, x + alpha[:, None, None] * dx, x)
             x[reset] = Q.kin_predict(np.asarray(x0, np.float64)[reset], u[reset], np.asarray(kappa)[reset],
                                      np.asarray(ds)[reset], L)
             hist[-1]["reset"] = reset

@@ -134,3 +134,35 @@ def test_kin_sqp_multiple_shooting_vs_oracle(golden):
     np.testing.assert_array_equal(u0, us[:, 0])
     phi_end = np.minimum(KS.merit(x0, us, kap, ds, 2.5, W), KS.merit(x0, us, kap, ds, 2.5, W, x=xs))
     assert (phi_end <= np.minimum(ps0, pm0) * (1 + 1e-9)).all()
+
+
+@pytest.mark.parametrize("ms", [0, 1], ids=["single_shooting", "multiple_shooting"])
+def test_kin_sqp_later_qp_failure_keeps_iterate(golden, ms):
+    """A later QP of the globalised step that fails with non-finite output (injected through
+    vc_debug_qp_fault after SQP iteration 1 on one problem) refuses its step: the accepted
+    iterate is the one before it (no 0 * NaN), finite, equal to a run that stops one iteration
+    earlier, and the step's status stays the first QP's.  The oracle restates the same rule
+    (oracle/kin_sqp.py kin_sqp_solve: alpha = 0 keeps the iterate)."""
+    g = golden
+    obs = _obs(g)
+    cfg = _cfg(3, 1)
+    cfg["qp"]["ms"] = ms
+    x0, ub, kap, ds = (g[k].astype(np.float64) for k in ("kin_x0", "kin_ubar", "kin_kappa", "kin_ds"))
+    xw = Q.kin_predict(x0, ub, kap, ds, 2.5)
+    bad = 7
+    cfg2 = _cfg(2, 1)
+    cfg2["qp"]["ms"] = ms
+    with _ctx(cfg2, obs, len(x0)) as c:
+        u0r, xsr, usr, str_, _ = c.solve(x0, kap, ds, ub.copy(), xbar=xw.copy())
+    with _ctx(cfg, obs, len(x0)) as c:
+        c._check(c.lib.vc_debug_qp_fault(c._h, 2, bad))
+        u0, xs, us, st, it = c.solve(x0, kap, ds, ub.copy(), xbar=xw.copy())
+    assert np.isfinite(us[bad]).all() and np.isfinite(xs[bad]).all() and np.isfinite(u0[bad]).all()
+    assert st[bad] == str_[bad] == 0
+    np.testing.assert_array_equal(us[bad], usr[bad])   # the third step was refused
+    # x*: the state iterate before the refused step, or (multiple shooting, where its merit is
+    # no lower) the rollout of the accepted inputs
+    roll = Q.kin_predict(x0[bad:bad + 1], usr[bad:bad + 1], kap[bad:bad + 1], ds[bad:bad + 1], 2.5)[0]
+    assert np.array_equal(xs[bad], xsr[bad]) or np.abs(xs[bad] - roll).max() < 1e-9
+    np.testing.assert_array_equal(u0[bad], u0r[bad])
+    assert (st == 0).all(), st

@@ -942,11 +942,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     A.status[b] = st;
     A.iters[b] = it_total;
     if (A.diag) {
-#ifdef VC_TIMING
-      constexpr size_t DS = 4 + 9;
-#else
-      constexpr size_t DS = 4;
-#endif
+      constexpr size_t DS = VC_CASC_DIAG_COLS;  // the ABI's row stride (no section counters here)
       A.diag[(size_t)b * DS + 0] = last_res;
       A.diag[(size_t)b * DS + 1] = last_mu;
       A.diag[(size_t)b * DS + 2] = double((any_fail ? 1 : 0) | (all_conv ? 2 : 0));

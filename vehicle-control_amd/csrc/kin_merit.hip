@@ -48,6 +48,12 @@ __device__ __forceinline__ double barrier_ext(double m, double m0) {
   return 1.0 / m0 - dm / (m0 * m0) + dm * dm / (m0 * m0 * m0);
 }
 
+// p + al (q - p), or p itself for a refused step (al = 0): a failed QP's output may be
+// non-finite, and 0 * NaN would carry it into the accepted iterate
+__device__ __forceinline__ double step_to(double p, double q, double al) {
+  return al == 0.0 ? p : p + al * (q - p);
+}
+
 // phi(u), u = up + alpha (uq - up), for one problem (oracle/kin_sqp.py merit)
 __device__ double merit(const KinMeritArgs& A, int b, double alpha, bool msm) {
   const int N = A.N;
@@ -65,8 +71,7 @@ __device__ double merit(const KinMeritArgs& A, int b, double alpha, bool msm) {
   double blo = 0.0, bhi = 0.0, dev = 0.0, obs = 0.0, ww = 0.0, wa = 0.0, pen = 0.0, a_prev = 0.0, pdef = 0.0;
   const double m0 = A.obs.margin_min;
   for (int n = 0; n < N; ++n) {
-    const double u[2] = {up[2 * n] + alpha * (uq[2 * n] - up[2 * n]),
-                         up[2 * n + 1] + alpha * (uq[2 * n + 1] - up[2 * n + 1])};
+    const double u[2] = {step_to(up[2 * n], uq[2 * n], alpha), step_to(up[2 * n + 1], uq[2 * n + 1], alpha)};
     const double ds = dsv[n];
     if (n >= 1) {  // stage terms on x_n (n = 0 is the fixed initial state)
       const double ey = x[3];
@@ -89,7 +94,7 @@ __device__ double merit(const KinMeritArgs& A, int b, double alpha, bool msm) {
       const int o = (n + 1) * KIN_NX;
 #pragma unroll
       for (int i = 0; i < KIN_NX; ++i) {
-        const double xn = i == 2 ? x[2] + ds : xp[o + i] + alpha * (xq[o + i] - xp[o + i]);
+        const double xn = i == 2 ? x[2] + ds : step_to(xp[o + i], xq[o + i], alpha);
         pdef += fabs(x[i] + ds * f[i] - xn);
         x[i] = xn;
       }
@@ -145,7 +150,7 @@ __global__ __launch_bounds__(64) void kin_merit_kernel(KinMeritArgs A) {
     const double* xp = A.x_prev + (size_t)b * (N + 1) * KIN_NX;
     for (int e = l; e < (N + 1) * KIN_NX; e += 64)
       if (e < KIN_NX) xo[e] = A.x0[(size_t)b * KIN_NX + e];  // x_0 = x0
-      else if (e % KIN_NX != 2) xo[e] = xp[e] + al * (xo[e] - xp[e]);  // s stays s0 + sum ds
+      else if (e % KIN_NX != 2) xo[e] = step_to(xp[e], xo[e], al);  // s stays s0 + sum ds
   }
   if (l == 0) {  // rollout of the accepted inputs (read before the wavefront overwrites u*)
     double x[KIN_NX];
@@ -156,7 +161,7 @@ __global__ __launch_bounds__(64) void kin_merit_kernel(KinMeritArgs A) {
       if (xo) xo[i] = x[i];
     }
     for (int n = 0; n < N; ++n) {
-      const double u[2] = {up[2 * n] + al * (ub[2 * n] - up[2 * n]), up[2 * n + 1] + al * (ub[2 * n + 1] - up[2 * n + 1])};
+      const double u[2] = {step_to(up[2 * n], ub[2 * n], al), step_to(up[2 * n + 1], ub[2 * n + 1], al)};
       if (n == 0) {
         A.u0[(size_t)b * 2] = u[0];
         A.u0[(size_t)b * 2 + 1] = u[1];
@@ -185,10 +190,24 @@ __global__ __launch_bounds__(64) void kin_merit_kernel(KinMeritArgs A) {
     }
   }
   __syncthreads();  // lane 0's reads of u* have completed
-  for (int e = l; e < 2 * N; e += 64) ub[e] = up[e] + al * (ub[e] - up[e]);
+  for (int e = l; e < 2 * N; e += 64) ub[e] = step_to(up[e], ub[e], al);
+}
+
+// a QP that failed with non-finite output (the case kin_ric reports as VC_NONFINITE)
+__global__ __launch_bounds__(64) void kin_qp_fault_kernel(KinLtvArgs a, int N, int b) {
+  const double nan = __builtin_nan("");
+  for (int e = threadIdx.x; e < 2 * N; e += 64) a.u_out[(size_t)b * 2 * N + e] = nan;
+  for (int e = threadIdx.x; e < 6 * (N + 1); e += 64) a.x_out[(size_t)b * 6 * (N + 1) + e] = nan;
+  if (threadIdx.x < 2) a.u0[(size_t)b * 2 + threadIdx.x] = nan;
+  if (threadIdx.x == 0) a.status[b] = VC_NONFINITE;
 }
 
 }  // namespace
+
+hipError_t launch_kin_qp_fault(const KinLtvArgs& a, int N, int b, hipStream_t stream) {
+  hipLaunchKernelGGL(kin_qp_fault_kernel, dim3(1), dim3(64), 0, stream, a, N, b);
+  return hipGetLastError();
+}
 
 hipError_t launch_kin_merit(const KinMeritArgs& a, hipStream_t stream) {
   if (a.B <= 0) return hipSuccess;

@@ -821,11 +821,7 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
   finite = __all(finite ? 1 : 0) != 0;
   if (l < 2) A.u0[(size_t)b * 2 + l] = s.ub[0][l];
   if (l == 0) {
-#ifdef VC_TIMING
-    constexpr size_t DS = 13;  // the ABI's diag stride in the section-timing build (no sections here)
-#else
-    constexpr size_t DS = 4;
-#endif
+    constexpr size_t DS = VC_DIAG_COLS;  // the ABI's row stride (no section counters here)
     int32_t st;
     if (!finite || !finite_pred) st = VC_NONFINITE;
     else if (solved) st = VC_SOLVED;

@@ -8,6 +8,20 @@
 #include "vc_models.hpp"
 #include "vcmpc.h"
 
+// Columns of vc_solve_diag's diag rows, per kernel family: 4 diagnostics, plus the
+// section-cycle counters in the VC_TIMING build (make timing).
+#ifdef VC_TIMING
+#define VC_DIAG_COLS 13      // 4 diagnostics + 9 section-cycle counters (kin_ltv.hip T_*)
+#define VC_DYN_DIAG_COLS 19  // 4 diagnostics + 15 section-cycle counters (dyn_sqp.hip DT_*)
+#define VC_CASC_DIAG_COLS 17 // 4 diagnostics + 13 section-cycle counters (casc_sqp.hip CT_*)
+#define VC_ST_DIAG_COLS 13   // 4 diagnostics + 9 section-cycle counters (st_sqp.hip ST_*)
+#else
+#define VC_DIAG_COLS 4
+#define VC_DYN_DIAG_COLS 4
+#define VC_CASC_DIAG_COLS 4
+#define VC_ST_DIAG_COLS 4
+#endif
+
 // Default floor of the obstacle barrier margin dist - (r + 0.1) [m] (vc_obstacles.margin_min).
 #define VC_OBS_MARGIN_MIN 0.05
 
@@ -222,6 +236,8 @@ hipError_t launch_kin_ltv(const KinLtvArgs& a, int N, hipStream_t stream);
 // (KinLtvArgs.mode / H_out / g_out are not read).
 hipError_t launch_kin_ric(const KinLtvArgs& a, int N, hipStream_t stream);
 hipError_t launch_kin_merit(const KinMeritArgs& a, hipStream_t stream);
+// Test hook (vc_debug_qp_fault): overwrite problem b's QP output with NaN, status VC_NONFINITE.
+hipError_t launch_kin_qp_fault(const KinLtvArgs& a, int N, int b, hipStream_t stream);
 bool kin_ric_built(int N);
 hipError_t launch_dyn_sqp(const DynSqpArgs& a, int N, hipStream_t stream);
 hipError_t launch_casc_sqp(const CascSqpArgs& a, int N, int M, hipStream_t stream);

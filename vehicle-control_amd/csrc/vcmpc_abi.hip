@@ -16,18 +16,6 @@
 #include "vcmpc.h"
 
 
-#ifdef VC_TIMING
-#define VC_DIAG_COLS 13      // 4 diagnostics + 9 section-cycle counters (kin_ltv.hip T_*)
-#define VC_DYN_DIAG_COLS 19  // 4 diagnostics + 15 section-cycle counters (dyn_sqp.hip DT_*)
-#define VC_CASC_DIAG_COLS 17 // 4 diagnostics + 13 section-cycle counters (casc_sqp.hip CT_*)
-#define VC_ST_DIAG_COLS 13   // 4 diagnostics + 9 section-cycle counters (st_sqp.hip ST_*)
-#else
-#define VC_DIAG_COLS 4
-#define VC_DYN_DIAG_COLS 4
-#define VC_CASC_DIAG_COLS 4
-#define VC_ST_DIAG_COLS 4
-#endif
-
 struct vc_ctx {
   int device = 0, model = 0, N = 0, max_batch = 0, dtype = 0;
   vc_params p{};
@@ -42,6 +30,7 @@ struct vc_ctx {
   size_t sim_bytes = 0;
   void* ls = nullptr;     // kinematic SQP scratch (vc_qp.kin_sqp > 0): u_prev, status / iteration sums
   size_t ls_bytes = 0;
+  int fault_iter = -1, fault_problem = -1;  // vc_debug_qp_fault (tests only)
   std::string err;
 };
 
@@ -563,6 +552,8 @@ int vc_solve_diag(vc_ctx* c, int B, const void* x0, const void* kappa, const voi
                                  c->stream));
       if (kin_condensed(c)) VC_HIP(c, vc::launch_kin_ltv(a, N, c->stream));
       else VC_HIP(c, vc::launch_kin_ric(a, N, c->stream));
+      if (i == c->fault_iter && c->fault_problem >= 0 && c->fault_problem < B)
+        VC_HIP(c, vc::launch_kin_qp_fault(a, N, c->fault_problem, c->stream));
       m.first = i == 0;
       VC_HIP(c, vc::launch_kin_merit(m, c->stream));
     }
@@ -582,6 +573,13 @@ int vc_solve_debug(vc_ctx* c, int B, const void* x0, const void* kappa, const vo
 }
 
 int vc_debug_stride(void) { return vc::dyn_sqp_debug_stride(); }
+
+int vc_debug_qp_fault(vc_ctx* c, int sqp_iter, int problem) {
+  if (!c) return VC_E_ARG;
+  c->fault_iter = sqp_iter;
+  c->fault_problem = problem;
+  return 0;
+}
 
 int vc_condense(vc_ctx* c, int B, const void* x0, const void* ubar, const void* kappa, const void* ds, void* H,
                 void* g, int flags) {

@@ -83,8 +83,9 @@ class BatchedSingleTrackMPC(Controller):
         with w projected onto its box (the reference's first guess 1 + U[0, 1) exceeds
         w_max = 0.4; IPOPT recovers by globalisation, the SQP's trust region would only
         take it back 0.2 per iteration).  A problem that does not come back VC_SOLVED is
-        re-solved once from the neutral warm start (Fx = 0, w = 0) -- the reference's
-        simulator instead swallows the solver exception (racing.py:416-423)."""
+        re-solved once from the neutral warm start (Fx = 0, w = 0) -- the build's own
+        policy: in the reference a failed IPOPT solve raises, the simulator's step()
+        returns None (racing.py:416-423) and unpacking it (racing.py:232) ends the run."""
         x0 = np.asarray(states, np.float64).reshape(self.B, self.ns)
         ds, kappa = dyn_horizon_params(x0[:, IS], self.state_prediction[:, IUX, :], self.dt, self.car.track.k)
         cast = lambda a: np.ascontiguousarray(a, dtype=self.np_dtype)

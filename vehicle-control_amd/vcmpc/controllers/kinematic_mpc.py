@@ -115,9 +115,11 @@ class BatchedKinematicMPC(Controller):
         1 + U[0, 1) (kinematic_mpc.py:65-67) is far outside w_max = 0.4 (IPOPT
         recovers from that by globalisation; one QP step cannot).  A problem that
         does not come back VC_SOLVED (e.g. linearised state rows infeasible) keeps
-        its projected warm start as prediction and applies its first action --
-        the reference's simulator instead swallows the solver exception
-        (racing.py:416-423)."""
+        the neutral retry's output as prediction (unshifted) and applies its first
+        action.  Both are the build's own policy (vc_simulate differs: it applies
+        u = 0 and restarts from the neutral warm start); in the reference a failed
+        IPOPT solve raises, the simulator's step() prints it and returns None
+        (racing.py:416-423), and unpacking that (racing.py:232) ends the run."""
         x0 = np.ascontiguousarray(np.asarray(states, np.float64).reshape(self.B, self.ns))
         ds, kappa = horizon_params(x0[:, IS], self.state_prediction[:, IV, :], self.dt, self.car.track.k)
         ubar = np.ascontiguousarray(np.swapaxes(self.action_prediction, 1, 2))
@@ -137,9 +139,10 @@ class BatchedKinematicMPC(Controller):
             u0[idx], xbar[idx], ustar[idx], status[idx], iters[idx] = r
         self.action_prediction = np.swapaxes(ustar, 1, 2).copy()
         self.state_prediction = np.swapaxes(xbar, 1, 2).copy()
-        if self.shift:  # vc_qp.shift, as vc_simulate does: the next warm start one stage on
-            self.action_prediction[:, :, :-1] = self.action_prediction[:, :, 1:].copy()
-            self.state_prediction[:, :, :-1] = self.state_prediction[:, :, 1:].copy()
+        if self.shift:  # vc_qp.shift, as vc_simulate does: a solved vehicle's next warm start one stage on
+            ok = status == 0
+            self.action_prediction[ok, :, :-1] = self.action_prediction[ok, :, 1:].copy()
+            self.state_prediction[ok, :, :-1] = self.state_prediction[ok, :, 1:].copy()
         self.status, self.iters = status, iters
         return u0
 

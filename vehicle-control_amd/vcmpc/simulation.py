@@ -8,8 +8,10 @@ with every step on the GPU (``vc_simulate``): horizon parameters from the
 unshifted warm start and the curvature table, the fused MPC solve, the fp64
 plant step -- no host round trip between steps.
 
-Per-vehicle failure handling (the reference prints and drops the step,
-racing.py:417-422): a solve whose status is not VC_SOLVED applies the neutral
+Per-vehicle failure handling is the build's own policy.  In the reference a failed IPOPT
+solve raises, the simulator's step() prints it and returns None (racing.py:416-423), and the
+caller's unpacking ``action, state = self.step(...)`` (racing.py:232) raises TypeError, which
+ends the run.  Here a solve whose status is not VC_SOLVED applies the neutral
 input u = 0, is counted in ``nfail``, and the next step starts from the neutral
 warm start (ubar = 0).  Almost every such step is the first one, whose linearised QP
 around the reference's random first guess 1 + U[0, 1) is infeasible under the
