@@ -151,57 +151,101 @@ def cpu_baseline(batch, sample):
         t0 = time.perf_counter()
         Q.kin_ltv_solve(d["x0"], d["ubar"], d["kappa"], d["ds"], 2.5, W)
         dt = time.perf_counter() - t0
-    cpu = platform.processor() or platform.machine()
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                cpu = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
+    cpu = cpu_model()
     return {"value": len(d["x0"]) / dt, "unit": "solves/s", "cores": 1, "kind": "port",
             "sample": f"{len(d['x0'])} problems of the C2 workload, one oracle pass (PDIP + active-set polish, "
                       f"numpy fp64, 1 thread) in {dt:.2f} s on {cpu}; a stand-in for the reference's "
                       f"CasADi/IPOPT path, which cannot run here"}
 
 
-def _oracle_chunk(chunk):
-    """Pool worker: one oracle pass over a chunk of C2 problems, one thread."""
+def usable_cpus():
+    """(cores, source): the CPU cores this process may use.  A cgroup CPU quota (cpu.max,
+    cgroup v2; cpu.cfs_quota_us, v1) wins; else the box's per-GPU CPU share that the pool
+    exports as OMP_NUM_THREADS (16 on the GPU boxes, whose affinity mask shows the whole
+    machine); else the affinity mask."""
+    import math
+    aff = len(os.sched_getaffinity(0))
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            txt = open(path).read().split()
+        except OSError:
+            continue
+        try:
+            if path.endswith("cpu.max") and txt[0] != "max":
+                return min(aff, max(1, math.floor(int(txt[0]) / int(txt[1])))), f"cgroup {path} = {' '.join(txt)}"
+            if path.endswith("cfs_quota_us") and int(txt[0]) > 0:
+                per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+                return min(aff, max(1, int(txt[0]) // per)), f"cgroup {path} = {txt[0]} / {per}"
+        except (ValueError, IndexError, OSError):
+            continue
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        return min(aff, int(omp)), (f"no cgroup CPU quota; OMP_NUM_THREADS={omp} (the pool's per-GPU CPU share; "
+                                    f"affinity shows {aff})")
+    return aff, "no cgroup CPU quota; sched_getaffinity"
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
+def _oracle_chunk(job):
+    """Pool worker: one oracle pass over a chunk of C2 ("kin") or C3 ("c3") problems, one thread."""
     from threadpoolctl import threadpool_limits
 
-    from oracle import ltv_qp as Q
     from vcmpc.config import load_config
-    if chunk is None:  # warm-up: imports only
+    if job is None:  # warm-up: imports only
+        from oracle import dyn_sqp, ltv_qp  # noqa: F401
         return 0.0
-    W = Q.kin_weights(load_config("kinematic_mpc"))
+    kind, chunk = job
     with threadpool_limits(limits=1):
-        Q.kin_ltv_solve(chunk["x0"], chunk["ubar"], chunk["kappa"], chunk["ds"], 2.5, W)
+        if kind == "kin":
+            from oracle import ltv_qp as Q
+            W = Q.kin_weights(load_config("kinematic_mpc"))
+            Q.kin_ltv_solve(chunk["x0"], chunk["ubar"], chunk["kappa"], chunk["ds"], 2.5, W)
+        else:
+            from oracle import dyn_sqp as D
+            from oracle import models as M
+            W = D.dyn_weights(load_config("dynamic_mpc"))
+            p = M.dyn_params_from_config(load_config("dynamic_car"))
+            D.dyn_sqp_solve(chunk["x0"], chunk["ubar"], chunk["kappa"], chunk["ds"], p, W, "linear")
     return float(len(chunk["x0"]))
 
 
-def cpu_baseline_all_cores(batch, sample, workers=16):
-    """SURVEY 8(d)'s second CPU figure: the same oracle pass with one single-threaded
-    process per core (`workers` processes; 16 = this pool's CPU share per GPU box).
-    Spawned children (fresh interpreters, no forked HIP state); interpreter start-up and
-    imports are excluded by a warm-up map before the timed one."""
+def cpu_baseline_all_cores(batch, sample, kind="kin", per_worker=None):
+    """SURVEY 8(d)'s second CPU figure: the oracle pass with one single-threaded process per
+    usable core (usable_cpus()), each on its own chunk of the workload.  Spawned children
+    (fresh interpreters, no forked HIP state); interpreter start-up and imports are excluded
+    by a warm-up map before the timed one.  per_worker: problems per process (default: the
+    sample split evenly)."""
     import multiprocessing as mp
 
     import numpy as np
-    d = {k: v[:sample] for k, v in batch.items()}
-    n = len(d["x0"])
-    parts = np.array_split(np.arange(n), workers)
-    chunks = [{k: np.ascontiguousarray(v[p]) for k, v in d.items()} for p in parts if len(p)]
+    workers, source = usable_cpus()
+    n_total = len(batch["x0"])
+    sample = min(sample if per_worker is None else per_worker * workers, n_total)
+    d = {k: np.asarray(v[:sample], np.float64) for k, v in batch.items()}
+    parts = np.array_split(np.arange(sample), workers)
+    chunks = [(kind, {k: np.ascontiguousarray(v[p]) for k, v in d.items()}) for p in parts if len(p)]
     with mp.get_context("spawn").Pool(len(chunks)) as pool:
         pool.map(_oracle_chunk, [None] * len(chunks), chunksize=1)
         t0 = time.perf_counter()
         done = sum(pool.map(_oracle_chunk, chunks, chunksize=1))
         dt = time.perf_counter() - t0
+    what = "C2 kinematic LTV-QP (PDIP + active-set polish)" if kind == "kin" else \
+        "C3 single-track SQP (3 SQP iterations, complex-step linearisation + exact QPs)"
     return {"value": done / dt, "unit": "solves/s", "cores": len(chunks), "kind": "port",
-            "host_cpus_visible": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
-            "sample": f"{int(done)} problems of the C2 workload split over {len(chunks)} single-threaded "
-                      f"oracle processes, {dt:.2f} s wall (the batched numpy oracle stands in for the "
-                      f"reference's CasADi/IPOPT path, which cannot run here; {len(chunks)} = this pool's "
-                      f"CPU share per GPU, the machine shows {os.cpu_count()} CPUs)"}
+            "usable_cores": workers, "usable_cores_source": source, "nproc": os.cpu_count(),
+            "affinity_cpus": len(os.sched_getaffinity(0)), "cpu_model": cpu_model(),
+            "sample": f"{int(done)} problems of the {what} workload split over {len(chunks)} single-threaded "
+                      f"numpy-oracle processes (one per usable core), {dt:.2f} s wall; the oracle stands in "
+                      f"for the reference's CasADi/IPOPT path, which cannot run here"}
 
 
 def cpu_baseline_c3(data, sample):
@@ -776,7 +820,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (seeded C2 sampler, vcmpc/workload.py)",
+            "data": ("synthetic (seeded C2 sampler, vcmpc/workload.py: SURVEY 8(d)'s x0 / kappa / ubar "
+                     "distributions; ds = 0.03 v0 + 0.5, one constant per problem (the SURVEY's per-stage "
+                     "0.03 vbar_n + 0.5 with a constant speed prediction); problems whose warm-start rollout "
+                     "leaves v > 1 m/s or |epsi| < 1.2 rad are re-drawn)"),
             "config": {"workload": f"C2 kinematic-bicycle LTV-MPC, B={B} per GPU, N={N_HORIZON}, fp64",
                        "batch_per_gpu": B, "global_batch": B * world, "horizon": N_HORIZON,
                        "parallelism": f"dp{world} (independent shards)"},
@@ -807,6 +854,10 @@ def main():
                 out["cpu_baseline_all_cores"] = {"error": repr(e)}
             if c3_data is not None and "error" not in c3:
                 c3["cpu_baseline"] = cpu_baseline_c3(c3_data, 8)
+                try:
+                    c3["cpu_baseline_all_cores"] = cpu_baseline_all_cores(c3_data, 0, kind="c3", per_worker=8)
+                except Exception as e:
+                    c3["cpu_baseline_all_cores"] = {"error": repr(e)}
             if ca_data is not None and "error" not in ca:
                 ca["cpu_baseline"] = cpu_baseline_casc(ca_data, 4)
             if c5_aux and "error" not in c5:

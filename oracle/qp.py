@@ -54,8 +54,16 @@ def pdip_batch(H, g, C, d, tol=1e-12, max_iter=200):
     lam = np.ones((B, m))
     iters = np.zeros(B, np.int64)
     done = np.zeros(B, bool)
+    diverged = np.zeros(B, bool)
     scale = 1.0 + np.maximum(np.abs(g).max(axis=1), np.abs(d).max(axis=1))
     for it in range(max_iter):
+        # an infeasible QP drives the iterate off to infinity (multipliers and barrier weights
+        # lam / s beyond any finite KKT point's): such a problem is frozen and reported as
+        # diverged instead of overflowing; feasibility itself is decided by oracle/feasibility.py
+        blow = ~done & ((lam.max(1) > 1e60 * scale) | (np.abs(z).max(1) > 1e60 * scale)
+                        | ((lam / s).max(1) > 1e250))
+        diverged |= blow
+        done |= blow
         rd = np.einsum("bij,bj->bi", H, z) + g + np.einsum("bmi,bm->bi", C, lam)
         rp = np.einsum("bmi,bi->bm", C, z) + s - d
         mu = (s * lam).mean(axis=1)
@@ -79,13 +87,23 @@ def pdip_batch(H, g, C, d, tol=1e-12, max_iter=200):
 
         # predictor
         rc = s * lam
-        dz_a, ds_a, dl_a = solve(rc)
+        with np.errstate(over="ignore", invalid="ignore"):
+            dz_a, ds_a, dl_a = solve(rc)
+        bad = ~done & ~(np.isfinite(dz_a).all(1) & np.isfinite(ds_a).all(1) & np.isfinite(dl_a).all(1))
+        diverged |= bad
+        done |= bad
+        dz_a, ds_a, dl_a = (np.where(done[:, None], 0.0, v) for v in (dz_a, ds_a, dl_a))
         a_aff = np.minimum(_max_step(s, ds_a), _max_step(lam, dl_a))
         mu_aff = ((s + a_aff[:, None] * ds_a) * (lam + a_aff[:, None] * dl_a)).mean(1)
         sigma = (mu_aff / np.maximum(mu, 1e-300)) ** 3
         # corrector
         rc = s * lam + ds_a * dl_a - (sigma * mu)[:, None]
-        dz, ds_, dl = solve(rc)
+        with np.errstate(over="ignore", invalid="ignore"):
+            dz, ds_, dl = solve(rc)
+        bad = ~done & ~(np.isfinite(dz).all(1) & np.isfinite(ds_).all(1) & np.isfinite(dl).all(1))
+        diverged |= bad
+        done |= bad
+        dz, ds_, dl = (np.where(done[:, None], 0.0, v) for v in (dz, ds_, dl))
         alpha = 0.99 * np.minimum(_max_step(s, ds_), _max_step(lam, dl))
         alpha = np.minimum(alpha, 1.0)
         alpha = np.where(done, 0.0, alpha)[:, None]
@@ -94,7 +112,7 @@ def pdip_batch(H, g, C, d, tol=1e-12, max_iter=200):
         lam = lam + alpha * dl
         s = np.maximum(s, 1e-300)
         lam = np.maximum(lam, 1e-300)
-    return z, lam, s, iters, done
+    return z, lam, s, iters, done & ~diverged, diverged
 
 
 def kkt_residuals(H, g, C, d, z, lam):
@@ -161,10 +179,10 @@ def _eqp(H, g, C, d, act):
 
 
 def solve_qp_batch(H, g, C, d, tol=1e-13, max_iter=200, do_polish=True):
-    z, lam, s, iters, done = pdip_batch(H, g, C, d, tol=tol, max_iter=max_iter)
+    z, lam, s, iters, done, diverged = pdip_batch(H, g, C, d, tol=tol, max_iter=max_iter)
     polished = np.zeros(len(g), bool)
     if do_polish:
         for b in range(len(g)):
             z[b], lam[b], polished[b] = polish(H[b], g[b], C[b], d[b], z[b], lam[b], s[b])
     kkt = kkt_residuals(H, g, C, d, z, lam)
-    return dict(z=z, lam=lam, iters=iters, converged=done, polished=polished, kkt=kkt)
+    return dict(z=z, lam=lam, iters=iters, converged=done, diverged=diverged, polished=polished, kkt=kkt)
