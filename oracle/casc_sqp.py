@@ -28,7 +28,8 @@ defined here once and implemented identically by ``csrc/casc_sqp.hip`` (fp64):
                   prediction; the switching cost's lateral residual linearised
                   through Fy_f + Fy_r) + prox ||dz||^2, subject to the linearised
                   rows below, solved exactly (oracle/qp.py)
-    5. update     ubar <- ubar + du*
+    5. update     ubar <- ubar + alpha du*, alpha = the first of 1, 1/2, ... whose prediction
+                  stays in the models' domain (casc_in_domain; oracle/dyn_sqp.py domain_step)
   output u* = ubar, x* = predict(u*), u0 = u*_0.
 
 Constraint rows (one-sided, linearised at the prediction; force rows divided by S):
@@ -83,6 +84,19 @@ def casc_predict(x0, ubar, kappa, ds, p, W, tyre="fiala"):
         j = N + m
         xp[:, m + 1] = M.pm_spatial_transition(xp[:, m], ubar[:, j], kappa[:, j], ds[:, j], p)
     return xs, xp
+
+
+def casc_in_domain(xs, xp, kappa):
+    """[B] both predictions inside their spatial models' domain: the single-track stages as
+    oracle/dyn_sqp.py in_domain, the point-mass stages finite with V > 0 and
+    s' = V cos(epsi) / (1 - kappa ey) > 0 (dynamic_point_mass.py:90-100 divides by s')."""
+    N = xs.shape[1]
+    kp = np.asarray(kappa)[:, N:N + xp.shape[1]]
+    V, ey, ep = xp[..., PV], xp[..., PEY], xp[..., PEP]
+    with np.errstate(invalid="ignore", over="ignore"):
+        sdot = V * np.cos(ep) / (1.0 - kp * ey)
+        ok = np.isfinite(xp).all(axis=(1, 2)) & (V > 0).all(axis=1) & (sdot > 0).all(axis=1)
+    return D.in_domain(xs, kappa) & ok
 
 
 def pack_states(xs, xp):
@@ -285,8 +299,14 @@ def casc_sqp_solve(x0, ubar, kappa, ds, p, W, tyre="fiala", keep_qps=False, **qp
         rec = dict(ubar=u.copy(), dz=sol["z"], kkt=sol["kkt"], polished=sol["polished"], iters=sol["iters"])
         if keep_qps:
             rec.update({k: Q[k] for k in ("H", "g", "C", "d", "Gs", "Gp")})
+        du = sol["z"].reshape(B, H_, 2) * scale
+        alpha = D.domain_step(np.asarray(x0, np.float64), u, du, np.asarray(kappa, np.float64),
+                              np.asarray(ds, np.float64), p, tyre,
+                              lambda x0_, u_, k_, ds_, p_, t_: casc_predict(x0_, u_, k_, ds_, p_, W, t_),
+                              in_domain=casc_in_domain)
+        rec["alpha"] = alpha
         hist.append(rec)
-        u = u + sol["z"].reshape(B, H_, 2) * scale
+        u = np.where((alpha > 0)[:, None, None], u + alpha[:, None, None] * du, u)
     xs, xp = casc_predict(np.asarray(x0, np.float64), u, np.asarray(kappa, np.float64),
                           np.asarray(ds, np.float64), p, W, tyre)
     return dict(u_star=u, x_star=pack_states(xs, xp), u0=u[:, 0].copy(), hist=hist)

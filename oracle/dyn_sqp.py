@@ -18,7 +18,11 @@ here once and implemented identically by ``csrc/dyn_sqp.hip``:
     3. condense   dx_k = G_k dz in the scaled decision variable
                   dz = [dFx_0/S, dw_0, dFx_1/S, dw_1, ...]  (S = fx_scale, 1000 N)
     4. QP         min 1/2 dz'H dz + g'dz  s.t. C dz <= d  (below), solved exactly
-    5. update     ubar <- ubar + du*
+    5. update     ubar <- ubar + alpha du*, alpha = the first of 1, 1/2, ..., 2^-(DOM_HALVINGS-1)
+                  whose prediction stays in the spatial model's domain (in_domain: finite,
+                  Ux > 0 and s' > 0 at every stage), 0 if none -- IPOPT cuts its step back the
+                  same way when the NLP functions cannot be evaluated at a trial point; a full
+                  step (alpha = 1) wherever the prediction stays in the domain
   output u* = ubar, x* = predict(u*), u0 = u*_0.
 
 QP cost = the reference NLP cost in Gauss-Newton form about (xbar, ubar), with every
@@ -51,6 +55,42 @@ from . import obstacles as OB
 IUX, IUY, IR, ID, IS, IEY, IEP, IT = range(8)
 IFX, IW = 0, 1
 CSTEP = 1e-30  # complex-step size
+
+
+DOM_HALVINGS = 8    # step cut-backs tried when the full SQP step leaves the model's domain
+
+
+def in_domain(xbar, kappa):
+    """[B] prediction inside the spatial model's domain: finite, Ux > 0 and
+    s' = (Ux cos epsi - Uy sin epsi) / (1 - kappa ey) > 0 at every stage (the spatial
+    transformation dynamic_car.py:169-191 divides by s'; the slip angles by Ux)."""
+    ux, uy, ey, ep = xbar[..., IUX], xbar[..., IUY], xbar[..., IEY], xbar[..., IEP]
+    k = np.asarray(kappa)[:, :xbar.shape[1]]
+    with np.errstate(invalid="ignore", over="ignore"):
+        sdot = (ux * np.cos(ep) - uy * np.sin(ep)) / (1.0 - k * ey)
+        ok = np.isfinite(xbar).all(axis=(1, 2)) & (ux > 0).all(axis=1) & (sdot > 0).all(axis=1)
+    return ok
+
+
+def domain_step(x0, u, du, kappa, ds, p, tyre, predict, in_domain=None):
+    """alpha[B] of step 5: the first of 1, 1/2, ... with predict(u + alpha du) in the domain,
+    0 where none is (or where du is not finite).  predict returns what in_domain takes
+    (with kappa) -- the single-track prediction by default."""
+    in_domain = in_domain or globals()["in_domain"]
+    B = u.shape[0]
+    alpha = np.zeros(B)
+    todo = np.isfinite(du).all(axis=tuple(range(1, du.ndim)))
+    a = 1.0
+    for _ in range(DOM_HALVINGS):
+        if not todo.any():
+            break
+        idx = np.nonzero(todo)[0]
+        pred = predict(x0[idx], u[idx] + a * du[idx], kappa[idx], ds[idx], p, tyre)
+        ok = in_domain(*(pred if isinstance(pred, tuple) else (pred,)), kappa[idx])
+        alpha[idx[ok]] = a
+        todo[idx[ok]] = False
+        a *= 0.5
+    return alpha
 
 
 def dyn_weights(cfg: dict) -> dict:
@@ -250,8 +290,12 @@ def dyn_sqp_solve(x0, ubar, kappa, ds, p, W, tyre="linear", keep_qps=False, **qp
                    iters=sol["iters"])
         if keep_qps:
             rec.update({k: Q[k] for k in ("xbar", "A", "Bm", "G", "H", "g", "C", "d")})
+        du = dz.reshape(B, N, 2) * np.array([S, 1.0])
+        alpha = domain_step(np.asarray(x0, np.float64), u, du, np.asarray(kappa, np.float64),
+                            np.asarray(ds, np.float64), p, tyre, dyn_predict)
+        rec["alpha"] = alpha
         hist.append(rec)
-        u = u + dz.reshape(B, N, 2) * np.array([S, 1.0])
+        u = np.where((alpha > 0)[:, None, None], u + alpha[:, None, None] * du, u)
     x_star = dyn_predict(np.asarray(x0, np.float64), u, np.asarray(kappa, np.float64),
                          np.asarray(ds, np.float64), p, tyre)
     return dict(u_star=u, x_star=x_star, u0=u[:, 0].copy(), hist=hist)

@@ -107,8 +107,8 @@ def test_casc_ric_matches_condensed_kernel():
 @pytest.mark.parametrize("M", [15, 40])
 def test_casc_ric_batch_properties(M, dyn_params):
     """B = 4096 (the bench's cascaded batch): every problem solved unless one of its SQP
-    iterations meets a linearised QP that is infeasible (the oracle's exact solver certifies
-    it: primal residual > 1e-6 -- a property of the contract, not of the kernel); w inside
+    iterations meets a linearised QP with no feasible point (phase-1 LP with a checked Farkas
+    certificate -- a property of the contract at that warm start, not of the kernel); w inside
     its box, finite outputs, bit-identical host / device pointer runs."""
     import torch
     from vcmpc.workload import cascaded_batch
@@ -124,12 +124,16 @@ def test_casc_ric_batch_properties(M, dyn_params):
           f"non-solved {[(int(b), dg[b].tolist()) for b in bad[:4]]}")
     assert len(bad) <= 8
     if len(bad):
+        # a non-solved problem must meet a QP with no feasible point: phase-1 LP + checked Farkas
+        # certificate (oracle/feasibility.py) on the oracle's SQP iterates up to the first such QP
+        from oracle import feasibility as F
         W = CS.casc_weights(_cfg(M))
         sub = {k: v[bad] for k, v in d.items()}
-        ref = CS.casc_sqp_solve(sub["x0"], sub["ubar"], sub["kappa"], sub["ds"], dyn_params, W, tyre="fiala")
-        pfeas = np.max([h["kkt"]["pfeas"] for h in ref["hist"]], axis=0)
-        print("oracle primal residual of the non-solved problems' QPs:", pfeas)
-        assert (pfeas > 1e-6).all()
+        ref = CS.casc_sqp_solve(sub["x0"], sub["ubar"], sub["kappa"], sub["ds"], dyn_params, W, tyre="fiala",
+                                keep_qps=True)
+        first, farkas = F.first_infeasible_iteration(ref["hist"])
+        print("first SQP iteration with an infeasible QP (-1: none):", first.tolist(), "Farkas ok:", farkas.tolist())
+        assert (first >= 0).all() and farkas.all()
     ok = st == 0
     assert np.isfinite(us[ok]).all() and np.isfinite(xs[ok]).all()
     assert (np.abs(us[:, :N, 1]) <= 0.4 + 1e-12).all()

@@ -65,6 +65,7 @@ struct CrSmem {
   static constexpr int H = N + M;
   double xs[H][8];    // prediction: single-track states k < N, point-mass (V, s, ey, epsi, t) k >= N
   double ub[H][2];    // current ubar
+  double uo[H][2];    // the iterate before the SQP step under test (domain cut-back)
   double kap[H], dsv[H];
   double J[H][6][8];  // [A6 | B6 diag(S, 1 or S)] of the transition out of stage k
   union {
@@ -206,13 +207,19 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
   double last_res = 0.0, last_mu = 0.0;
   const double tol_r = 1e-10, tol_mu = 1e-13;
 
-  for (int sq = 0;; ++sq) {
+  // SQP update state: a step under test (tries > 0) is ub = uo + 2^-(tries-1) du (du in
+  // u.q.v[k][7..8], untouched by the rollout), the last try the unchanged iterate
+  // (oracle/casc_sqp.py, oracle/dyn_sqp.py domain_step)
+  int tries = 0, sq = 0;
+  bool first = true;
+  for (;;) {
     // ---------------- predict (lane 0: RK4, switch, point-mass Euler) ----------------
+    // the only rollout site; flag[2]: finite and inside both models' domain (casc_in_domain)
     if (l == 0) {
       double x[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) x[i] = s.xs[0][i];
-      bool fin = true;
+      bool fin = true, dom = dyn_in_domain(x, s.kap[0]);
       for (int kk = 0; kk < N - 1; ++kk) {
         const double u2[2] = {s.ub[kk][0], s.ub[kk][1]};
         const double kp = s.kap[kk];
@@ -224,11 +231,13 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
           s.xs[kk + 1][i] = xn[i];
           fin = fin && isfinite(xn[i]);
         }
+        dom = dom && dyn_in_domain(x, s.kap[kk + 1]);
       }
       double p[5];
       st_to_pm<double>(x, p);  // cascaded_mpc.py:256-277
 #pragma unroll
       for (int i = 0; i < 5; ++i) s.xs[N][i] = p[i];
+      dom = dom && pm_in_domain(p, s.kap[N]);
       for (int j = N; j < H - 1; ++j) {  // dynamic_point_mass.py:76-100, Euler
         const double u2[2] = {s.ub[j][0], s.ub[j][1]};
         double f[5];
@@ -240,10 +249,30 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
           s.xs[j + 1][i] = p[i];
           fin = fin && isfinite(p[i]);
         }
+        dom = dom && pm_in_domain(p, s.kap[j + 1]);
       }
-      if (!fin) s.flag[0] = VC_NONFINITE;
+      s.flag[2] = (fin && dom) ? 1 : 0;
+      if (first && !fin) s.flag[0] = VC_NONFINITE;
     }
     WSYNC();
+    first = false;
+    if (tries > 0) {
+      // ---------------- SQP update: cut the step back while its rollout leaves the domain ----------------
+      if (s.flag[2] == 0 && tries <= DOM_HALVINGS) {
+        const double a = tries < DOM_HALVINGS ? ldexp(1.0, -tries) : 0.0;
+        if (stl) {
+          const double u0v = s.uo[k][0], u1v = s.uo[k][1];
+          s.ub[k][0] = a > 0.0 ? u0v + a * (s.u.q.v[k][7] * S) : u0v;
+          if (pm) s.ub[k][1] = a > 0.0 ? u1v + a * (s.u.q.v[k][8] * S) : u1v;
+          else s.ub[k][1] = a > 0.0 ? fmin(fmax(u1v + a * s.u.q.v[k][8], W.w_min), W.w_max) : u1v;
+        }
+        ++tries;
+        WSYNC();
+        continue;
+      }
+      tries = 0;
+      ++sq;
+    }
     if (sq == W.sqp_iters || s.flag[0] == VC_NONFINITE) break;
 
     // ---------------- linearize + stage functions ----------------
@@ -912,11 +941,16 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     any_fail = any_fail || fail;
 
     // ---------------- SQP update: ubar += dz (Fx, and the point mass's Fy, scaled by S) ----------------
+    // tested by the next rollout (domain cut-back above)
     if (stl) {
-      s.ub[k][0] += s.u.q.v[k][7] * S;
-      if (pm) s.ub[k][1] += s.u.q.v[k][8] * S;
-      else s.ub[k][1] = fmin(fmax(s.ub[k][1] + s.u.q.v[k][8], W.w_min), W.w_max);
+      const double u0v = s.ub[k][0], u1v = s.ub[k][1];
+      s.uo[k][0] = u0v;
+      s.uo[k][1] = u1v;
+      s.ub[k][0] = u0v + s.u.q.v[k][7] * S;
+      if (pm) s.ub[k][1] = u1v + s.u.q.v[k][8] * S;
+      else s.ub[k][1] = fmin(fmax(u1v + s.u.q.v[k][8], W.w_min), W.w_max);
     }
+    tries = 1;
     WSYNC();
   }
 

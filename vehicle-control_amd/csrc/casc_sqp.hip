@@ -70,6 +70,7 @@ struct CascSmem {
   double xs[N][8];
   double xp[M][5];
   double ub[L::H][2];
+  double uo[L::H][2];  // the iterate before the SQP step under test (domain cut-back)
   double kap[L::H], dsv[L::H];
   double z[L::n], dz[L::n], rhs[L::n], gp[L::n], invd[L::n];
   double Y[L::H][8], R[L::H][8];
@@ -77,6 +78,7 @@ struct CascSmem {
   double sc[8];                 // lateral residual value + gradient (Ux, Uy, r, delta, Fx)
   double red[8];
   int flag[4];
+  int dom;             // the last rollout is inside both models' domain (casc_in_domain)
 };
 
 __device__ __forceinline__ int sym7(int a, int b) {  // a <= b
@@ -540,12 +542,13 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
   }
   __syncthreads();
 
+  bool first = true;  // the warm start's rollout: non-finite -> VC_NONFINITE
   auto predict = [&]() {
     if (t == 0) {
       double x[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) x[i] = s.xs[0][i];
-      bool fin = true;
+      bool fin = true, dom = dyn_in_domain(x, s.kap[0]);
       for (int k = 0; k < N - 1; ++k) {
         const double u2[2] = {s.ub[k][0], s.ub[k][1]};
         const double kp = s.kap[k];
@@ -557,11 +560,13 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
           s.xs[k + 1][i] = xn[i];
           fin = fin && isfinite(xn[i]);
         }
+        dom = dom && dyn_in_domain(x, s.kap[k + 1]);
       }
       double p[5];
       st_to_pm<double>(x, p);
 #pragma unroll
       for (int i = 0; i < 5; ++i) s.xp[0][i] = p[i];
+      dom = dom && pm_in_domain(p, s.kap[N]);
       for (int m = 0; m < M - 1; ++m) {
         const int j = N + m;
         const double u2[2] = {s.ub[j][0], s.ub[j][1]};
@@ -574,8 +579,10 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
           s.xp[m + 1][i] = p[i];
           fin = fin && isfinite(p[i]);
         }
+        dom = dom && pm_in_domain(p, s.kap[j + 1]);
       }
-      if (!fin) s.flag[0] = VC_NONFINITE;
+      s.dom = (fin && dom) ? 1 : 0;
+      if (first && !fin) s.flag[0] = VC_NONFINITE;
     }
   };
 
@@ -663,12 +670,30 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
 
   // one predict call site (the final pass is the output rollout x* = rollout(u*)): a second
   // call site made the compiler outline the rollout, and the call spilled ~400 VGPRs
-  int sqp_done = 0;
-  for (int it = 0;; ++it) {
+  // SQP update state: a step under test (tries > 0) is ub = uo + 2^-(tries-1) du (du = the QP
+  // solution z, untouched by the rollout), the last try the unchanged iterate (oracle/casc_sqp.py)
+  int sqp_done = 0, tries = 0, it = 0;
+  for (;;) {
     CT_STAMP(t_p0)
     predict();
     __syncthreads();
+    first = false;
     CT_ACC(CT_PRED, t_p0)
+    if (tries > 0) {  // cut the step back while its rollout leaves the domain
+      if (s.dom == 0 && tries <= DOM_HALVINGS) {
+        const double a = tries < DOM_HALVINGS ? ldexp(1.0, -tries) : 0.0;
+        if (t < n) {
+          const int kk = t >> 1, cc = t & 1;
+          const double scl = (cc == 0 || kk >= N) ? S : 1.0;
+          s.ub[kk][cc] = a > 0.0 ? s.uo[kk][cc] + a * (s.z[t] * scl) : s.uo[kk][cc];
+        }
+        ++tries;
+        __syncthreads();
+        continue;
+      }
+      tries = 0;
+      ++it;
+    }
     CT_STAMP(t_l0)
     if (it == W.sqp_iters || s.flag[0] == VC_NONFINITE) break;
 
@@ -1217,8 +1242,10 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
     if (t < n) {
       const int kk = t >> 1, cc = t & 1;
       const double scl = (cc == 0 || kk >= N) ? S : 1.0;
+      s.uo[kk][cc] = s.ub[kk][cc];
       s.ub[kk][cc] += s.z[t] * scl;
     }
+    tries = 1;
     __syncthreads();
     ++sqp_done;
   }

@@ -81,6 +81,7 @@ struct DynSmem {
   float W[N][32];            // per-stage weight block: 5x5 over (Ux,Uy,r,dlt,Fx) at row stride 6, [30] q_ey, [31] q_ep
   float xb[N][8];
   float ub[N][2];
+  float uo[N][2];  // the iterate before the SQP step under test (domain cut-back)
   float kap[N], dsv[N];
   float y[N][8];             // forward pass: (Ux,Uy,r,dlt,ey) of V_k z, [5] terminal epsi
   float va[2][N][8];         // adjoint inputs: (Ux,Uy,r,dlt,ey, Fx-unit, w-direct, epsi(N-1))
@@ -133,6 +134,7 @@ __device__ __forceinline__ void predict(DynSmem<N>& s, const DynCoef<float>& p, 
   float x[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) x[i] = s.xb[0][i];
+  bool dom = dyn_in_domain(x, s.kap[0]);
 #pragma unroll 1
   for (int k = 0; k < N - 1; ++k) {
     const float u[2] = {s.ub[k][0], s.ub[k][1]};
@@ -141,11 +143,14 @@ __device__ __forceinline__ void predict(DynSmem<N>& s, const DynCoef<float>& p, 
     rk4_apply<float, 8>(x, s.dsv[k], [&](const float* xs, float* f) { dyn_spatial_ode_alg(xs, u, kap, p, f); }, xn);
 #pragma unroll
     for (int i = 0; i < 8; ++i) x[i] = xn[i];
+    dom = dom && dyn_in_domain(x, s.kap[k + 1]);
     if (lane == 0) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) s.xb[k + 1][i] = x[i];
     }
   }
+  // flag[2]: the rollout is inside the spatial model's domain (oracle/dyn_sqp.py in_domain)
+  if (lane == 0) s.flag[2] = dom ? 1 : 0;
 }
 
 // ---- phase 2: Jacobians of the RK4 spatial step by dual numbers (task = stage x seed pair)
@@ -673,8 +678,12 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
   bool all_conv = true, any_fail = false;
   float last_res = 0.f, last_mu = 0.f;
 
+  // SQP update state: a step under test (tries > 0) is ub = uo + 2^-(tries-1) du (du = the QP
+  // iterate vz, untouched by the rollout), the last try the unchanged iterate; the loop's one
+  // rollout site also makes the output rollout x* = rollout(u*)
+  int tries = 0, sq = 0;
 #pragma unroll 1
-  for (int sq = 0; sq < W.sqp_iters; ++sq) {
+  for (;;) {
     asm volatile("" : "+v"(t), "+v"(lane), "+v"(k), "+v"(q));
     asm volatile("" : "+s"(wv));
     // ---------------- predict ----------------
@@ -682,6 +691,23 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
     if (wv == 0) predict(s, p, lane);
     __syncthreads();
     DT_ACC(DT_PRED, t_p0)
+    if (tries > 0) {
+      // ---------------- SQP update: cut the step back while its rollout leaves the domain ----------------
+      // (oracle/dyn_sqp.py domain_step; IPOPT cuts its step back alike on evaluation errors)
+      if (s.flag[2] == 0 && tries <= DOM_HALVINGS) {
+        const float a = tries < DOM_HALVINGS ? ldexpf(1.f, -tries) : 0.f;
+        if (t < n) {
+          const float uo = s.uo[t >> 1][t & 1];
+          s.ub[t >> 1][t & 1] = a > 0.f ? uo + a * (s.vz[t] * ((t & 1) ? 1.f : S)) : uo;
+        }
+        ++tries;
+        __syncthreads();
+        continue;
+      }
+      tries = 0;
+      ++sq;
+    }
+    if (sq == W.sqp_iters) break;
     DT_STAMP(t_l0)
 
     // ---------------- linearize (waves 1-3) | stage terms (stage lanes of wave 0-2) ----------
@@ -1187,15 +1213,18 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
     any_fail = any_fail || fail;
     n_polished += polished ? 1 : 0;
 
-    // ---------------- SQP update: ubar += du ----------------
-    if (t < n) s.ub[t >> 1][t & 1] += s.vz[t] * ((t & 1) ? 1.f : S);
+    // ---------------- SQP update: ubar += du, tested by the next rollout ----------------
+    if (t < n) {
+      const float uo = s.ub[t >> 1][t & 1];
+      s.uo[t >> 1][t & 1] = uo;
+      s.ub[t >> 1][t & 1] = uo + s.vz[t] * ((t & 1) ? 1.f : S);
+    }
+    tries = 1;
     __syncthreads();
   }
 
-  // ---------------- outputs: u*, x* = rollout(u*), u0, status ----------------
+  // ---------------- outputs: u*, x* = rollout(u*) (the loop's last predict), u0, status ----------------
   DT_STAMP(t_o0)
-  if (wv == 0) predict(s, p, lane);
-  __syncthreads();
   DT_ACC(DT_OUT, t_o0)
   bool finite = true;
   if (t < n) {

@@ -60,6 +60,7 @@ template <int N>
 struct StSmem {
   double xs[N][8];    // prediction (N columns, dynamics for k < N-1)
   double ub[N][2];    // current ubar
+  double uo[N][2];    // the iterate before the SQP step under test (domain cut-back)
   double kap[N], dsv[N];
   double J[N][6][8];  // [A6 | B6 diag(S, 1)] of step k (rows/cols Ux, Uy, r, delta, ey, epsi | dFx, dw)
   union {
@@ -236,14 +237,21 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
   double last_res = 0.0, last_mu = 0.0;
   const double tol_r = 1e-10, tol_mu = 1e-13;
 
-  for (int sq = 0;; ++sq) {
-    // ---------------- predict (lane 0, serial RK4) ----------------
+  // SQP update state: a step under test (tries > 0) is ub = u + 2^-(tries-1) du, the last try
+  // the unchanged iterate (oracle/dyn_sqp.py domain_step)
+  // (the iterate in uo, the scaled step in u.q.v[k][7..8], untouched by the rollout)
+  int tries = 0, sq = 0;
+  bool first = true;
+  for (;;) {
+    // ---------------- predict (lane 0, serial RK4): xs = rollout(ubar) ----------------
+    // the only rollout site (a second one makes the compiler outline it and spill);
+    // flag[1]: finite, flag[2]: inside the spatial model's domain (Ux > 0, s' > 0)
     ST_STAMP(t_p0)
     if (l == 0) {
       double x[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) x[i] = s.xs[0][i];
-      bool fin = true;
+      bool fin = true, dom = dyn_in_domain(x, s.kap[0]);
       for (int kk = 0; kk < N - 1; ++kk) {
         const double u2[2] = {s.ub[kk][0], s.ub[kk][1]};
         const double kp = s.kap[kk];
@@ -255,11 +263,33 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
           s.xs[kk + 1][i] = xn[i];
           fin = fin && isfinite(xn[i]);
         }
+        dom = dom && dyn_in_domain(x, s.kap[kk + 1]);
       }
-      if (!fin) s.flag[0] = VC_NONFINITE;
+      s.flag[1] = fin ? 1 : 0;
+      s.flag[2] = (fin && dom) ? 1 : 0;
+      if (first && !fin) s.flag[0] = VC_NONFINITE;
     }
     WSYNC();
     ST_ACC(ST_PRED, t_p0)
+    first = false;
+    if (tries > 0) {
+      // ---------------- SQP update: the step's rollout left the domain? ----------------
+      // alpha = the first of 1, 1/2, ... whose rollout stays in the model's domain, 0 if none
+      // (IPOPT cuts its step back alike on evaluation errors)
+      if (s.flag[2] == 0 && tries <= DOM_HALVINGS) {
+        const double a = tries < DOM_HALVINGS ? ldexp(1.0, -tries) : 0.0;
+        if (stl) {
+          const double uF = s.uo[k][0], uW = s.uo[k][1];
+          s.ub[k][0] = a > 0.0 ? uF + a * (s.u.q.v[k][7] * S) : uF;
+          s.ub[k][1] = a > 0.0 ? fmin(fmax(uW + a * s.u.q.v[k][8], W.w_min), W.w_max) : uW;
+        }
+        ++tries;
+        WSYNC();
+        continue;
+      }
+      tries = 0;
+      ++sq;
+    }
     if (sq == W.sqp_iters || s.flag[0] == VC_NONFINITE) break;
 
     // ---------------- linearize + stage functions ----------------
@@ -821,13 +851,17 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     all_conv = all_conv && conv;
     any_fail = any_fail || fail;
 
-    // ---------------- SQP update: ubar += dz ----------------
+    // ---------------- SQP update: ubar += dz, tested by the next rollout ----------------
     // w is projected onto its box: exact at a converged QP (|violation| <= tol_r), and it
     // keeps a non-converged iterate (infeasible-start interior point) from leaving it
     if (stl) {
-      s.ub[k][0] += s.u.q.v[k][7] * S;
-      s.ub[k][1] = fmin(fmax(s.ub[k][1] + s.u.q.v[k][8], W.w_min), W.w_max);
+      const double uF = s.ub[k][0], uW = s.ub[k][1];
+      s.uo[k][0] = uF;
+      s.uo[k][1] = uW;
+      s.ub[k][0] = uF + s.u.q.v[k][7] * S;
+      s.ub[k][1] = fmin(fmax(uW + s.u.q.v[k][8], W.w_min), W.w_max);
     }
+    tries = 1;
     WSYNC();
   }
 

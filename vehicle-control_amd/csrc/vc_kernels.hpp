@@ -57,6 +57,25 @@ __device__ __forceinline__ double rcp_nr(double x) {
   return isfinite(r) ? r : r0;
 }
 
+// Domain of the spatial single-track model at one state (oracle/dyn_sqp.py in_domain): Ux > 0
+// and s' = (Ux cos epsi - Uy sin epsi) / (1 - kappa ey) > 0 (dynamic_car.py:169-191 divides by
+// s', the slip angles by Ux).  False for non-finite states.  The SQP kernels cut a step back
+// (DOM_HALVINGS halvings, then no step) when its rollout leaves the domain.
+constexpr int DOM_HALVINGS = 8;
+template <typename T>
+__device__ __forceinline__ bool dyn_in_domain(const T* x, T kappa) {
+  const T sdot = (x[0] * cos(x[6]) - x[1] * sin(x[6])) / (T(1) - kappa * x[5]);
+  return x[0] > T(0) && sdot > T(0);
+}
+
+// ... and of the point-mass tail (oracle/casc_sqp.py casc_in_domain): V > 0 and
+// s' = V cos(epsi) / (1 - kappa ey) > 0 (dynamic_point_mass.py:90-100), p = (V, s, ey, epsi, t)
+template <typename T>
+__device__ __forceinline__ bool pm_in_domain(const T* p, T kappa) {
+  const T sdot = p[0] * cos(p[3]) / (T(1) - kappa * p[2]);
+  return p[0] > T(0) && sdot > T(0);
+}
+
 // Obstacle barrier of one stage as a convexified quadratic in ey:
 //   phi(ey) = sum_j w ds / (d_j - (r_j + 0.1)),  d_j = |(s, ey) - (s_j, ey_j)|
 // (kinematic_mpc.py:130-133, cascaded_mpc.py:173-176).  s is not a decision function
