@@ -18,11 +18,12 @@ here once and implemented identically by ``csrc/dyn_sqp.hip``:
     3. condense   dx_k = G_k dz in the scaled decision variable
                   dz = [dFx_0/S, dw_0, dFx_1/S, dw_1, ...]  (S = fx_scale, 1000 N)
     4. QP         min 1/2 dz'H dz + g'dz  s.t. C dz <= d  (below), solved exactly
-    5. update     ubar <- ubar + alpha du*, alpha = the first of 1, 1/2, ..., 2^-(DOM_HALVINGS-1)
-                  whose prediction stays in the spatial model's domain (in_domain: finite,
-                  Ux > 0 and s' > 0 at every stage), 0 if none -- IPOPT cuts its step back the
-                  same way when the NLP functions cannot be evaluated at a trial point; a full
-                  step (alpha = 1) wherever the prediction stays in the domain
+    5. update     ubar <- ubar + alpha du*.  From an iterate whose prediction is inside the
+                  spatial model's domain (in_domain: finite, Ux > 0 and s' > 0 at every stage),
+                  alpha = the first of 1, 1/2, ..., 2^-(DOM_HALVINGS-1) whose prediction stays
+                  inside, 0 if none -- IPOPT cuts its step back the same way when the NLP
+                  functions cannot be evaluated at a trial point; alpha = 1 from an iterate
+                  outside the domain, and wherever the full step stays inside
   output u* = ubar, x* = predict(u*), u0 = u*_0.
 
 QP cost = the reference NLP cost in Gauss-Newton form about (xbar, ubar), with every
@@ -80,6 +81,12 @@ def domain_step(x0, u, du, kappa, ds, p, tyre, predict, in_domain=None):
     B = u.shape[0]
     alpha = np.zeros(B)
     todo = np.isfinite(du).all(axis=tuple(range(1, du.ndim)))
+    # an iterate whose own prediction is outside the domain takes the full step (the test
+    # cannot tell a better point from a worse one there)
+    pred0 = predict(x0, u, kappa, ds, p, tyre)
+    out0 = ~in_domain(*(pred0 if isinstance(pred0, tuple) else (pred0,)), kappa)
+    alpha[todo & out0] = 1.0
+    todo &= ~out0
     a = 1.0
     for _ in range(DOM_HALVINGS):
         if not todo.any():

@@ -211,7 +211,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
   // u.q.v[k][7..8], untouched by the rollout), the last try the unchanged iterate
   // (oracle/casc_sqp.py, oracle/dyn_sqp.py domain_step)
   int tries = 0, sq = 0;
-  bool first = true;
+  bool first = true, test = false;  // test: the iterate's own rollout is inside the domain
   for (;;) {
     // ---------------- predict (lane 0: RK4, switch, point-mass Euler) ----------------
     // the only rollout site; flag[2]: finite and inside both models' domain (casc_in_domain)
@@ -258,7 +258,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     first = false;
     if (tries > 0) {
       // ---------------- SQP update: cut the step back while its rollout leaves the domain ----------------
-      if (s.flag[2] == 0 && tries <= DOM_HALVINGS) {
+      if (test && s.flag[2] == 0 && tries <= DOM_HALVINGS) {
         const double a = tries < DOM_HALVINGS ? ldexp(1.0, -tries) : 0.0;
         if (stl) {
           const double u0v = s.uo[k][0], u1v = s.uo[k][1];
@@ -950,6 +950,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       if (pm) s.ub[k][1] = u1v + s.u.q.v[k][8] * S;
       else s.ub[k][1] = fmin(fmax(u1v + s.u.q.v[k][8], W.w_min), W.w_max);
     }
+    test = s.flag[2] != 0;  // from an iterate outside the domain: the full step, untested
     tries = 1;
     WSYNC();
   }

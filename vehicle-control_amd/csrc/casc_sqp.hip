@@ -673,6 +673,7 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
   // SQP update state: a step under test (tries > 0) is ub = uo + 2^-(tries-1) du (du = the QP
   // solution z, untouched by the rollout), the last try the unchanged iterate (oracle/casc_sqp.py)
   int sqp_done = 0, tries = 0, it = 0;
+  bool test = false;  // the iterate's own rollout is inside the domain (else the full step, untested)
   for (;;) {
     CT_STAMP(t_p0)
     predict();
@@ -680,7 +681,7 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
     first = false;
     CT_ACC(CT_PRED, t_p0)
     if (tries > 0) {  // cut the step back while its rollout leaves the domain
-      if (s.dom == 0 && tries <= DOM_HALVINGS) {
+      if (test && s.dom == 0 && tries <= DOM_HALVINGS) {
         const double a = tries < DOM_HALVINGS ? ldexp(1.0, -tries) : 0.0;
         if (t < n) {
           const int kk = t >> 1, cc = t & 1;
@@ -1245,6 +1246,7 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
       s.uo[kk][cc] = s.ub[kk][cc];
       s.ub[kk][cc] += s.z[t] * scl;
     }
+    test = s.dom != 0;
     tries = 1;
     __syncthreads();
     ++sqp_done;

@@ -682,6 +682,7 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
   // iterate vz, untouched by the rollout), the last try the unchanged iterate; the loop's one
   // rollout site also makes the output rollout x* = rollout(u*)
   int tries = 0, sq = 0;
+  bool test = false;  // the iterate's own rollout is inside the domain (else the full step, untested)
 #pragma unroll 1
   for (;;) {
     asm volatile("" : "+v"(t), "+v"(lane), "+v"(k), "+v"(q));
@@ -694,7 +695,7 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
     if (tries > 0) {
       // ---------------- SQP update: cut the step back while its rollout leaves the domain ----------------
       // (oracle/dyn_sqp.py domain_step; IPOPT cuts its step back alike on evaluation errors)
-      if (s.flag[2] == 0 && tries <= DOM_HALVINGS) {
+      if (test && s.flag[2] == 0 && tries <= DOM_HALVINGS) {
         const float a = tries < DOM_HALVINGS ? ldexpf(1.f, -tries) : 0.f;
         if (t < n) {
           const float uo = s.uo[t >> 1][t & 1];
@@ -1219,6 +1220,7 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
       s.uo[t >> 1][t & 1] = uo;
       s.ub[t >> 1][t & 1] = uo + s.vz[t] * ((t & 1) ? 1.f : S);
     }
+    test = s.flag[2] != 0;
     tries = 1;
     __syncthreads();
   }

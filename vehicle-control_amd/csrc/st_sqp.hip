@@ -241,7 +241,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
   // the unchanged iterate (oracle/dyn_sqp.py domain_step)
   // (the iterate in uo, the scaled step in u.q.v[k][7..8], untouched by the rollout)
   int tries = 0, sq = 0;
-  bool first = true;
+  bool first = true, test = false;  // test: the iterate's own rollout is inside the domain
   for (;;) {
     // ---------------- predict (lane 0, serial RK4): xs = rollout(ubar) ----------------
     // the only rollout site (a second one makes the compiler outline it and spill);
@@ -276,7 +276,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       // ---------------- SQP update: the step's rollout left the domain? ----------------
       // alpha = the first of 1, 1/2, ... whose rollout stays in the model's domain, 0 if none
       // (IPOPT cuts its step back alike on evaluation errors)
-      if (s.flag[2] == 0 && tries <= DOM_HALVINGS) {
+      if (test && s.flag[2] == 0 && tries <= DOM_HALVINGS) {
         const double a = tries < DOM_HALVINGS ? ldexp(1.0, -tries) : 0.0;
         if (stl) {
           const double uF = s.uo[k][0], uW = s.uo[k][1];
@@ -861,6 +861,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       s.ub[k][0] = uF + s.u.q.v[k][7] * S;
       s.ub[k][1] = fmin(fmax(uW + s.u.q.v[k][8], W.w_min), W.w_max);
     }
+    test = s.flag[2] != 0;  // from an iterate outside the domain: the full step, untested
     tries = 1;
     WSYNC();
   }
