@@ -35,7 +35,7 @@ def config_for(run, rec):
     return cfg
 
 
-def replay(run, g, rec, sqp, skip=5):
+def replay(run, g, rec, sqp, skip=5, qp=None):
     from vcmpc.config import load_config
     from vcmpc.controllers.cascaded_mpc import BatchedCascadedMPC, BatchedSingleTrackMPC
     from vcmpc.environment import Track
@@ -43,7 +43,7 @@ def replay(run, g, rec, sqp, skip=5):
     track = Track.load("ippodromo")
     car = DynamicCar(load_config("dynamic_car"), track, tyre="fiala")
     cfg = config_for(run, rec)
-    cfg["qp"] = dict(cfg["qp"], sqp_iters=sqp)
+    cfg["qp"] = dict(cfg["qp"], sqp_iters=sqp, **(qp or {}))
     X, U, P = g[f"{run}/state_traj"], g[f"{run}/action_traj"], g[f"{run}/preds"]
     ctl = (BatchedCascadedMPC if cfg.get("horizon_pm", 0) else BatchedSingleTrackMPC)(car, cfg, batch=1)
     N = int(cfg["horizon"])
@@ -66,7 +66,7 @@ def replay(run, g, rec, sqp, skip=5):
     du, dplan = np.abs(np.array(du)), np.array(dplan)
     us = np.array(us)
     rel = du / np.maximum(np.abs(U[skip + 1:skip + 1 + len(du)]), [100.0, 0.01])
-    return dict(run=run, sqp=sqp, steps=T - skip, nonsolved=nfail,
+    return dict(run=run, sqp=sqp, qp=cfg["qp"], steps=T - skip, nonsolved=nfail,
                 dFx_median=float(np.median(du[:, 0])), dFx_p90=float(np.percentile(du[:, 0], 90)),
                 dFx_max=float(du[:, 0].max()), dw_median=float(np.median(du[:, 1])),
                 dw_p90=float(np.percentile(du[:, 1], 90)), dw_max=float(du[:, 1].max()),
@@ -81,15 +81,17 @@ def main():
     ap.add_argument("--sqp", type=int, nargs="+", default=[3, 5, 10, 20])
     ap.add_argument("--runs", nargs="+", default=["cascaded7_ippodromo", "singletrack_ippodromo"])
     ap.add_argument("--out", default=None)
+    ap.add_argument("--prox", type=float, nargs="+", default=[None], help="override qp.prox (sweep)")
     args = ap.parse_args()
     g = dict(np.load(os.path.join(ROOT, "tests", "golden", "replay_kat.npz"), allow_pickle=False))
     recs = json.loads(str(g["configs"]))
     res = []
     for run in args.runs:
-        for sqp in args.sqp:
-            r = replay(run, g, recs[run], sqp)
-            res.append(r)
-            print(json.dumps(r), flush=True)
+        for prox in args.prox:
+            for sqp in args.sqp:
+                r = replay(run, g, recs[run], sqp, qp=None if prox is None else {"prox": prox})
+                res.append(r)
+                print(json.dumps({k: v for k, v in r.items() if k != "example_plan"}), flush=True)
     if args.out:
         with open(args.out, "w") as f:
             json.dump(res, f, indent=1)
