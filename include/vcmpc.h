@@ -247,6 +247,12 @@ int vc_debug_stride(void);
  * it off (the default).  No reference counterpart. */
 int vc_debug_qp_fault(vc_ctx* ctx, int sqp_iter, int problem);
 
+/* Test diagnostics: the reciprocal forms of the solve kernels evaluated on the device for n
+ * (<= max_batch) inputs x[n] fp64, out[n][4] fp64: IEEE 1/x, rcp_nr(x) (kin_ltv), the
+ * Riccati kernels' v_rcp_f64 + two Newton steps, the raw v_rcp_f64 (csrc/numerics.hip).
+ * No reference counterpart. */
+int vc_debug_rcp(vc_ctx* ctx, int n, const void* x, void* out, int flags);
+
 /* Predict: xbar[B][N+1][nx] from x0[B][nx] and ubar[B][N][nu] (spatial step). */
 int vc_rollout(vc_ctx* ctx, int B, const void* x0, const void* ubar, const void* kappa,
                const void* ds, void* xbar, int flags);

@@ -49,6 +49,7 @@ def replay(run, g, rec, sqp, skip=5, qp=None):
     N = int(cfg["horizon"])
     T = min(len(X), len(U))
     du, dplan, nfail, us, dbg = [], [], 0, [], None
+    rec_nan = own_nan = 0
     for n in range(T):
         u = ctl.command(X[n][None])[0]
         us.append(u)
@@ -60,7 +61,13 @@ def replay(run, g, rec, sqp, skip=5, qp=None):
         if n < len(P):
             sp = ctl.state_prediction[0]
             xy = np.array([track.rel2glob(sp[4, i], sp[5, i], sp[6, i])[:2] for i in range(min(N, 20))])
-            dplan.append(np.hypot(*(xy - P[n, :len(xy)]).T).max())
+            # the recorded plans hold NaN past the reference track's spline range (its k / x / y
+            # do not wrap; e.g. cascaded7 step 406, stages >= 17): compare on the recorded stages
+            # that exist, and count our own non-finite plans separately
+            rec_ok = np.isfinite(P[n, :len(xy)]).all(axis=1)
+            rec_nan += int(not rec_ok.all())
+            own_nan += int(not np.isfinite(xy).all())
+            dplan.append(np.hypot(*(xy[rec_ok] - P[n, :len(xy)][rec_ok]).T).max())
             if dbg is None and n == 50:
                 dbg = dict(ours=xy[:3].tolist(), recorded=P[n, :3].tolist())
     du, dplan = np.abs(np.array(du)), np.array(dplan)
@@ -71,7 +78,7 @@ def replay(run, g, rec, sqp, skip=5, qp=None):
                 dFx_max=float(du[:, 0].max()), dw_median=float(np.median(du[:, 1])),
                 dw_p90=float(np.percentile(du[:, 1], 90)), dw_max=float(du[:, 1].max()),
                 plan_dev_median_m=float(np.nanmedian(dplan)), plan_dev_p90_m=float(np.nanpercentile(dplan, 90)),
-                plan_nan_steps=int(np.isnan(dplan).sum()),
+                plan_nan_steps=int(np.isnan(dplan).sum()) + own_nan, recorded_plan_nan_steps=rec_nan,
                 Fx_scale=float(np.abs(U[:, 0]).max()), w_scale=float(np.abs(U[:, 1]).max()),
                 frac_within_1pct=float(np.mean((rel < 0.01).all(axis=1))), example_plan=dbg)
 

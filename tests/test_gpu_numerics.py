@@ -1,0 +1,72 @@
+"""GPU: the reciprocal forms the solve kernels use, evaluated on the device (vc_debug_rcp,
+csrc/numerics.hip) against IEEE 1/x bit for bit, on the value classes the interior points
+produce: slacks and multipliers floored at 1e-300 (st_sqp / kin_ric / casc_ric), subnormals,
++-0, +-inf, values near the overflow / underflow edges, and a log-uniform sweep.
+
+DESIGN 3.1 records a round-2 breakage: replacing the Riccati kernels' IEEE divides of
+slacks / multipliers by v_rcp_f64 + Newton made the single-track closed loop fail.  This test
+names the input classes where each form differs from IEEE; the kernels only use each form
+where those classes cannot occur (asserted below for the ranges they do see)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _probe(x):
+    from vcmpc import Context, _abi
+    x = np.ascontiguousarray(x, np.float64)
+    out = np.zeros((len(x), 4))
+    with Context(N=20, max_batch=len(x)) as c:
+        c._check(c.lib.vc_debug_rcp(c._h, len(x), x.ctypes.data, out.ctypes.data, _abi.VC_HOST_PTRS))
+    return out
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, np.float64).view(np.int64)
+
+
+@pytest.fixture(scope="module")
+def probe():
+    rng = np.random.default_rng(7)
+    tiny = np.finfo(np.float64).tiny
+    special = np.array([1e-300, 1e-305, 1e-307, 2 * tiny, tiny, tiny / 2, 1e-310, 5e-324, 0.0, -0.0,
+                        np.inf, -np.inf, 1e300, 1e307, 4.4e307, 4.5e307, 8.9e307, 1.7e308,
+                        1.0, 3.0, -7.5, 2.0 ** -1022, 2.0 ** 1023, 1.5 * 2.0 ** 1023])
+    sweep = np.exp(rng.uniform(np.log(1e-300), np.log(1e300), 20000))
+    x = np.concatenate([special, sweep, -sweep[:1000]])
+    return x, _probe(x), len(special)
+
+
+def test_ieee_divide_is_ieee(probe):
+    x, out, _ = probe
+    with np.errstate(divide="ignore"):
+        ref = 1.0 / x
+    np.testing.assert_array_equal(_bits(out[:, 0]), _bits(ref))
+
+
+def test_reciprocal_classes(probe):
+    """Where rcp_nr and the Riccati form equal IEEE 1/x, and where they do not."""
+    x, out, nspec = probe
+    with np.errstate(divide="ignore"):
+        ref = 1.0 / x
+    tiny = np.finfo(np.float64).tiny
+    normal_safe = np.isfinite(x) & (np.abs(x) >= tiny) & (np.abs(x) <= 2.0 ** 1022)   # 1/x normal
+    for col, name in ((1, "rcp_nr"), (2, "rcp + 2 Newton")):
+        got = out[:, col]
+        same = _bits(got) == _bits(ref)
+        rel = np.abs(got - ref) / np.abs(ref)
+        bad = ~same & normal_safe
+        print(f"{name}: bit-identical on {same[normal_safe].mean():.5f} of the normal-range inputs, "
+              f"max rel err there {np.nanmax(np.where(normal_safe, rel, 0)):.2e}; outside the normal range: "
+              + ", ".join(f"{v:.3g} -> {g:.3g} (IEEE {r:.3g})" for v, g, r in
+                          zip(x[:nspec][~normal_safe[:nspec]], got[:nspec][~normal_safe[:nspec]],
+                              ref[:nspec][~normal_safe[:nspec]])))
+        # inside the normal range both forms are within 1 ulp of IEEE
+        assert np.nanmax(np.where(normal_safe, rel, 0)) <= 2.3e-16, x[bad][:5]
+    # the classes the kernels see: kin_ltv's slacks / multipliers are positive normals; the
+    # Riccati kernels' 2x2 determinants are finite positives of the normal range
+    sl = np.exp(np.random.default_rng(1).uniform(np.log(1e-290), np.log(1e290), 4000))
+    o = _probe(sl)
+    assert (np.abs(o[:, 1] - 1.0 / sl) <= 2.3e-16 * (1.0 / sl)).all()
+    assert (np.abs(o[:, 2] - 1.0 / sl) <= 2.3e-16 * (1.0 / sl)).all()

@@ -255,6 +255,8 @@ hipError_t launch_kin_ltv(const KinLtvArgs& a, int N, hipStream_t stream);
 // (KinLtvArgs.mode / H_out / g_out are not read).
 hipError_t launch_kin_ric(const KinLtvArgs& a, int N, hipStream_t stream);
 hipError_t launch_kin_merit(const KinMeritArgs& a, hipStream_t stream);
+// Test hook (vc_debug_rcp): the reciprocal forms of the solve kernels on n inputs, out[n][4].
+hipError_t launch_rcp_probe(int n, const double* x, double* out, hipStream_t st);
 // Test hook (vc_debug_qp_fault): overwrite problem b's QP output with NaN, status VC_NONFINITE.
 hipError_t launch_kin_qp_fault(const KinLtvArgs& a, int N, int b, hipStream_t stream);
 bool kin_ric_built(int N);

@@ -574,6 +574,22 @@ int vc_solve_debug(vc_ctx* c, int B, const void* x0, const void* kappa, const vo
 
 int vc_debug_stride(void) { return vc::dyn_sqp_debug_stride(); }
 
+int vc_debug_rcp(vc_ctx* c, int n, const void* x, void* out, int flags) {
+  if (!c) return VC_E_ARG;
+  if (n < 0 || n > c->max_batch) return fail(c, VC_E_ARG, "n %d outside [0, max_batch=%d]", n, c->max_batch);
+  if (int r = check_common(c, 0, flags)) return r;
+  if (!x || !out) return fail(c, VC_E_ARG, "null pointer");
+  if (n == 0) return 0;
+  if (flags == VC_DEVICE_PTRS) {
+    VC_HIP(c, vc::launch_rcp_probe(n, (const double*)x, (double*)out, c->stream));
+    return 0;
+  }
+  std::vector<Slot> slots = {{x, nullptr, (size_t)n * 8, nullptr}, {nullptr, out, (size_t)n * 32, nullptr}};
+  if (int r = stage(c, slots)) return r;
+  VC_HIP(c, vc::launch_rcp_probe(n, (const double*)slots[0].dev, (double*)slots[1].dev, c->stream));
+  return unstage(c, slots);
+}
+
 int vc_debug_qp_fault(vc_ctx* c, int sqp_iter, int problem) {
   if (!c) return VC_E_ARG;
   c->fault_iter = sqp_iter;

@@ -99,6 +99,7 @@ PROTOTYPES = {
     "vc_solve_debug": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int]),
     "vc_debug_stride": (C.c_int, []),
     "vc_debug_qp_fault": (C.c_int, [_vp, C.c_int, C.c_int]),
+    "vc_debug_rcp": (C.c_int, [_vp, C.c_int, _vp, _vp, C.c_int]),
     "vc_rollout": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, C.c_int]),
     "vc_linearize": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int]),
     "vc_condense": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int]),
