@@ -386,9 +386,9 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
     WSYNC();
     const double h00 = s.Hm[5][5], h01 = s.Hm[5][6], h11 = s.Hm[6][6];
     const double det = h00 * h11 - h01 * h01;
-    double id = __builtin_amdgcn_rcp(det);
-    id = id * (2.0 - det * id);
-    id = id * (2.0 - det * id);
+    // IEEE-exact reciprocal (tests/test_gpu_numerics.py): the plain v_rcp_f64 + Newton form turns
+    // det = +inf (h00 h11 overflowing at barrier weights ~1e154) into NaN where 1/det = 0
+    const double id = rcp_nr(det);
     const double i00 = h11 * id, i01 = -h01 * id, i11 = h00 * id;
     {
       const int kc = l >= 15 && l < 25 ? (l - 15) / NXT : 0, ki = l >= 15 && l < 25 ? (l - 15) % NXT : 0;

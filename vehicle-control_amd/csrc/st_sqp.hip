@@ -522,9 +522,9 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       const double h00 = s.Hm[7][7], h01 = s.Hm[7][8], h11 = s.Hm[8][8];
       const double det = h00 * h11 - h01 * h01;
       // 1 / det: v_rcp_f64 + two Newton steps (full fp64 accuracy, no IEEE divide sequence)
-      double id = __builtin_amdgcn_rcp(det);
-      id = id * (2.0 - det * id);
-      id = id * (2.0 - det * id);
+      // IEEE-exact reciprocal (tests/test_gpu_numerics.py): the plain v_rcp_f64 + Newton form turns
+      // det = +inf (h00 h11 overflowing at barrier weights ~1e154) into NaN where 1/det = 0
+      const double id = rcp_nr(det);
       const double i00 = h11 * id, i01 = -h01 * id, i11 = h00 * id;
       {
         // lanes 0..27: P entry (pi, pj); lanes 28..41: K entry; lane 42: Huu^-1
