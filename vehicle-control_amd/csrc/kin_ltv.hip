@@ -71,8 +71,15 @@ __device__ __forceinline__ double wave_max(double v) {
 __device__ __forceinline__ double wave_min(double v) {
   return wave_reduce(v, __builtin_inf(), [](double a, double b) { return fmin(a, b); });
 }
-// one-wave workgroup: LDS ordering point (s_waitcnt + a trivial s_barrier)
-__device__ __forceinline__ void wave_sync() { __syncthreads(); }
+// one-wave workgroup: LDS ordering point.  The LDS operations of one wave execute in issue
+// order, so a store followed by another lane's load of the same address needs no wait: only
+// the compiler must not move memory operations across this point (a __syncthreads here made
+// every column step of the factorisation wait for its own store, s_waitcnt lgkmcnt(0)).
+__device__ __forceinline__ void wave_sync() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
 __device__ __forceinline__ void fence() { __builtin_amdgcn_sched_barrier(0); }
 // compiler-only memory barrier: stops LICM from hoisting the (loop-invariant) LDS
 // reads of G / the factor out of the solver loops into thousands of live registers
