@@ -35,7 +35,7 @@ def config_for(run, rec):
     return cfg
 
 
-def replay(run, g, rec, sqp, skip=5, qp=None):
+def replay(run, g, rec, sqp, skip=5, qp=None, dump=None):
     from vcmpc.config import load_config
     from vcmpc.controllers.cascaded_mpc import BatchedCascadedMPC, BatchedSingleTrackMPC
     from vcmpc.environment import Track
@@ -72,6 +72,8 @@ def replay(run, g, rec, sqp, skip=5, qp=None):
                 dbg = dict(ours=xy[:3].tolist(), recorded=P[n, :3].tolist())
     du, dplan = np.abs(np.array(du)), np.array(dplan)
     us = np.array(us)
+    if dump:   # per-step arrays for a closer look (our u0, the recorded command, the state)
+        np.savez(dump, u=us, U=U, X=X, du=du, dplan=dplan, skip=skip)
     rel = du / np.maximum(np.abs(U[skip + 1:skip + 1 + len(du)]), [100.0, 0.01])
     return dict(run=run, sqp=sqp, qp=cfg["qp"], steps=T - skip, nonsolved=nfail,
                 dFx_median=float(np.median(du[:, 0])), dFx_p90=float(np.percentile(du[:, 0], 90)),
@@ -89,6 +91,7 @@ def main():
     ap.add_argument("--runs", nargs="+", default=["cascaded7_ippodromo", "singletrack_ippodromo"])
     ap.add_argument("--out", default=None)
     ap.add_argument("--prox", type=float, nargs="+", default=[None], help="override qp.prox (sweep)")
+    ap.add_argument("--dump", default=None, help="npz prefix for per-step arrays")
     args = ap.parse_args()
     g = dict(np.load(os.path.join(ROOT, "tests", "golden", "replay_kat.npz"), allow_pickle=False))
     recs = json.loads(str(g["configs"]))
@@ -96,7 +99,8 @@ def main():
     for run in args.runs:
         for prox in args.prox:
             for sqp in args.sqp:
-                r = replay(run, g, recs[run], sqp, qp=None if prox is None else {"prox": prox})
+                r = replay(run, g, recs[run], sqp, qp=None if prox is None else {"prox": prox},
+                           dump=None if args.dump is None else f"{args.dump}_{run}_p{prox}_s{sqp}.npz")
                 res.append(r)
                 print(json.dumps({k: v for k, v in r.items() if k != "example_plan"}), flush=True)
     if args.out:

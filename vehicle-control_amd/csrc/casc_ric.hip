@@ -88,6 +88,12 @@ struct CrSmem {
   double P[7][7];
   double T[7][8];
   double Hm[9][9];
+  // model coefficients and weights: each phase loads its own register copy from here (held in
+  // registers across the SQP loop they were spilled to scratch)
+  DynCoef<double> car;
+  vc_dyn_mpc w;
+  vc_casc_mpc cw;
+  vc_qp qp;
   int flag[4];
 };
 
@@ -180,11 +186,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
   __shared__ CrSmem<N, M> s;
   const int l = threadIdx.x;
   const int b = xcd_problem(blockIdx.x, A.B);
-  DynCoef<double> c = A.car;
-  c.tyre = TYRE;
-  const vc_dyn_mpc& W = A.w;
-  const vc_casc_mpc& CW = A.cw;
-  const double S = W.fx_scale;
+  const double S = A.w.fx_scale;
   const bool stl = l < H;
   const int k = stl ? l : 0;  // this lane's stage
   const bool pm = k >= N;     // point-mass stage
@@ -199,7 +201,13 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
   if (l >= N && l < H) {  // point-mass slots 5..7 are reported as 0 (free in the reference's NLP)
     s.xs[l][5] = s.xs[l][6] = s.xs[l][7] = 0.0;
   }
-  if (l == 0) s.flag[0] = VC_SOLVED;
+  if (l == 0) {
+    s.flag[0] = VC_SOLVED;
+    s.car = A.car;
+    s.w = A.w;
+    s.cw = A.cw;
+    s.qp = A.qp;
+  }
   WSYNC();
 
   int it_total = 0, it_max = 0;
@@ -216,6 +224,8 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     // ---------------- predict (lane 0: RK4, switch, point-mass Euler) ----------------
     // the only rollout site; flag[2]: finite and inside both models' domain (casc_in_domain)
     if (l == 0) {
+      DynCoef<double> c = s.car;
+      c.tyre = TYRE;
       double x[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) x[i] = s.xs[0][i];
@@ -264,7 +274,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
           const double u0v = s.uo[k][0], u1v = s.uo[k][1];
           s.ub[k][0] = a > 0.0 ? u0v + a * (s.u.q.v[k][7] * S) : u0v;
           if (pm) s.ub[k][1] = a > 0.0 ? u1v + a * (s.u.q.v[k][8] * S) : u1v;
-          else s.ub[k][1] = a > 0.0 ? fmin(fmax(u1v + a * s.u.q.v[k][8], W.w_min), W.w_max) : u1v;
+          else s.ub[k][1] = a > 0.0 ? fmin(fmax(u1v + a * s.u.q.v[k][8], s.w.w_min), s.w.w_max) : u1v;
         }
         ++tries;
         WSYNC();
@@ -273,10 +283,12 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       tries = 0;
       ++sq;
     }
-    if (sq == W.sqp_iters || s.flag[0] == VC_NONFINITE) break;
+    if (sq == s.w.sqp_iters || s.flag[0] == VC_NONFINITE) break;
 
     // ---------------- linearize + stage functions ----------------
     {
+      DynCoef<double> c = s.car;
+      c.tyre = TYRE;
       constexpr int NLIN = 8 * (N - 1), NSTF = 5 * N, NPM = 3 * (M - 1);
       using D2 = Dual<2, double>;
       using D1 = Dual<1, double>;
@@ -386,6 +398,8 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     // (V, ey, epsi); t passes through unchanged
     if (l < 5) {
       using D1 = Dual<1, double>;
+      DynCoef<double> c = s.car;
+      c.tyre = TYRE;
       D1 X5[5];
 #pragma unroll
       for (int i = 0; i < 4; ++i) X5[i] = D1(s.xs[N - 1][i]);
@@ -426,6 +440,10 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
 #pragma unroll
     for (int e = 0; e < 9; ++e) qc[e] = 0.0;
     {
+      const vc_dyn_mpc W = s.w;
+      const vc_casc_mpc CW = s.cw;
+      const vc_qp QP = s.qp;
+      const double Peng = s.car.Peng;
       const double ds = s.dsv[k];
       // ey / s slots of this stage's state
       const double ey = pm ? s.xs[k][2] : s.xs[k][5], sa = pm ? s.xs[k][1] : s.xs[k][4];
@@ -445,8 +463,8 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
         qc[4] += qey + po;
       }
       // prox on the scaled step, w^2 on the single track (:153)
-      Qc[Q77] += 2.0 * A.qp.prox;
-      Qc[Q88] += 2.0 * A.qp.prox;
+      Qc[Q77] += 2.0 * QP.prox;
+      Qc[Q88] += 2.0 * QP.prox;
       if (!pm) {
         Qc[Q88] += 2.0 * W.w_w;
         qc[8] += 2.0 * W.w_w * s.ub[k][1];
@@ -536,9 +554,9 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
         }
         const double wv = s.ub[k][1];
         double up = W.w_max - wv, dn = wv - W.w_min;
-        if (A.qp.trust_w > 0) {
-          up = fmin(up, A.qp.trust_w);
-          dn = fmin(dn, A.qp.trust_w);
+        if (QP.trust_w > 0) {
+          up = fmin(up, QP.trust_w);
+          dn = fmin(dn, QP.trust_w);
         }
         R.d[8] = up;
         R.d[9] = dn;
@@ -550,9 +568,9 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
         R.d[1] = R.d[2] = 1.0;
         R.set(1, false); R.set(2, false);
         // Fx - Peng / V <= 0 (divided by S), linearised in (V, Fx)
-        R.c[0][0] = c.Peng / (V * V) / S;
+        R.c[0][0] = Peng / (V * V) / S;
         R.c[0][4] = 1.0;
-        R.d[3] = -(s.ub[k][0] - c.Peng / V) / S;
+        R.d[3] = -(s.ub[k][0] - Peng / V) / S;
         R.set(3, on > 0.0);
 #pragma unroll
         for (int r = 4; r < 8; ++r) {
@@ -807,7 +825,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     int it = 0;
     bool conv = false, fail = false;
 #pragma unroll 1
-    for (; it < A.qp.max_iter; ++it) {
+    for (; it < s.qp.max_iter; ++it) {
       double vk[9], rp[NR], wg[NR], grk[9], val[NR];
       double rpm = 0.0, mus = 0.0;
 #pragma unroll
@@ -948,7 +966,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       s.uo[k][1] = u1v;
       s.ub[k][0] = u0v + s.u.q.v[k][7] * S;
       if (pm) s.ub[k][1] = u1v + s.u.q.v[k][8] * S;
-      else s.ub[k][1] = fmin(fmax(u1v + s.u.q.v[k][8], W.w_min), W.w_max);
+      else s.ub[k][1] = fmin(fmax(u1v + s.u.q.v[k][8], s.w.w_min), s.w.w_max);
     }
     test = s.flag[2] != 0;  // from an iterate outside the domain: the full step, untested
     tries = 1;
