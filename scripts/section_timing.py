@@ -17,7 +17,7 @@ from vcmpc.workload import kinematic_batch  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 tol = float(sys.argv[2]) if len(sys.argv) > 2 else 1e-10
-names = ["sweep", "setup", "resid", "build", "chol", "solve", "update", "polish", "out"]
+names = ["S1 rollout", "setup", "resid", "build", "chol", "solve", "update", "polish", "out", "S2 jac", "S3 sens", "S4 hess"]
 dev = torch.device("cuda:0")
 d = kinematic_batch(B, seed=31)
 t = {k: torch.from_numpy(v).to(dev) for k, v in d.items()}
@@ -29,7 +29,7 @@ with Context(N=20, max_batch=B, params=p) as c:
     u0 = torch.empty((B, 2), dtype=torch.float64, device=dev)
     st = torch.empty((B,), dtype=torch.int32, device=dev)
     it = torch.empty((B,), dtype=torch.int32, device=dev)
-    diag = torch.zeros((B, 13), dtype=torch.float64, device=dev)
+    diag = torch.zeros((B, 16), dtype=torch.float64, device=dev)
     ptrs = [C for C in (t["x0"], t["kappa"], t["ds"], xbar, t["ubar"].clone(), u0, st, it, diag)]
     import ctypes as C
     for _ in range(2):
@@ -48,4 +48,5 @@ with Context(N=20, max_batch=B, params=p) as c:
     print(f"  total stamped cycles/problem: mean {tot.mean():.0f}  max {tot.max():.0f}")
     for i, nm in enumerate(names):
         per_it = cyc[:, i].sum() / max(its.sum(), 1) if nm in ("resid", "build", "chol", "solve") else float("nan")
-        print(f"  {nm:7s} mean {cyc[:, i].mean():10.0f}  ({100 * cyc[:, i].mean() / tot.mean():5.1f} %)  per IPM iter {per_it:9.0f}")
+        print(f"  {nm:10s} mean {cyc[:, i].mean():10.0f}  ({100 * cyc[:, i].mean() / tot.mean():5.1f} %)  per IPM iter {per_it:9.0f}"
+              f"   slowest problem {cyc[tot.argmax(), i]:10.0f}")

@@ -113,7 +113,8 @@ __device__ __forceinline__ lds_cdouble* lds_opaque(const double* p) {
 #define VC_TSTAMP(var)
 #define VC_TACC(slot, t0)
 #endif
-enum { T_SWEEP = 0, T_SETUP, T_RESID, T_BUILD, T_CHOL, T_SOLVE, T_UPDATE, T_POLISH, T_OUT, T_NSLOT };
+// T_SWEEP = the serial rollout S1; T_S2 / T_S3 / T_S4 the sweep's other three parts
+enum { T_SWEEP = 0, T_SETUP, T_RESID, T_BUILD, T_CHOL, T_SOLVE, T_UPDATE, T_POLISH, T_OUT, T_S2, T_S3, T_S4, T_NSLOT };
 
 
 template <int N>
@@ -535,6 +536,8 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
     }
   }
   wave_sync();
+  VC_TACC(T_SWEEP, t_sweep0)
+  VC_TSTAMP(t_s20)
   {  // S2: lane k < N linearises stage k
     const int k = lane < N ? lane : 0;
     double xk[KIN_NX];
@@ -554,6 +557,8 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
     }
   }
   wave_sync();
+  VC_TACC(T_S2, t_s20)
+  VC_TSTAMP(t_s30)
   double gj = 0.0;
   double cv = 0, cd = 0, cey = 0, cep = 0, ct = 0;
   {  // S3
@@ -593,6 +598,8 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
     E[(N + 1) * LD + jcol] = cep;
   }
   wave_sync();
+  VC_TACC(T_S3, t_s30)
+  VC_TSTAMP(t_s40)
   double Hr[n];
   {  // S4
     const double vN = s.xb[N][0];
@@ -674,7 +681,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
     return;
   }
 
-  VC_TACC(T_SWEEP, t_sweep0)
+  VC_TACC(T_S4, t_s40)
   VC_TSTAMP(t_setup0)
   // ---- inequality data ------------------------------------------------------
   Side bx, cs;  // box side (lane j < n), state-row side (lane r < NC)

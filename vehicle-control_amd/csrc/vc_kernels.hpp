@@ -11,7 +11,7 @@
 // Columns of vc_solve_diag's diag rows, per kernel family: 4 diagnostics, plus the
 // section-cycle counters in the VC_TIMING build (make timing).
 #ifdef VC_TIMING
-#define VC_DIAG_COLS 13      // 4 diagnostics + 9 section-cycle counters (kin_ltv.hip T_*)
+#define VC_DIAG_COLS 16      // 4 diagnostics + 12 section-cycle counters (kin_ltv.hip T_*)
 #define VC_DYN_DIAG_COLS 19  // 4 diagnostics + 15 section-cycle counters (dyn_sqp.hip DT_*)
 #define VC_CASC_DIAG_COLS 17 // 4 diagnostics + 13 section-cycle counters (casc_sqp.hip CT_*)
 #define VC_ST_DIAG_COLS 13   // 4 diagnostics + 9 section-cycle counters (st_sqp.hip ST_*)
