@@ -56,6 +56,7 @@ def test_kin_sqp_obstacles_vs_oracle(golden, solver):
     ref = KS.kin_sqp_solve(x0, ub, kap, ds, 2.5, W, S)
     with _ctx(cfg, obs, len(x0)) as c:
         u0, xs, us, st, it = c.solve(x0, kap, ds, ub.copy())
+        xr = c.rollout(x0, us, kap, ds)    # the device's own rollout of u* (vc_rollout)
     err = np.abs(us - ref["u_star"]).max(axis=(1, 2))
     alphas = np.array([h["alpha"] for h in ref["hist"]])
     print(f"solver {solver}: |u* - u*_oracle| max {err.max():.2e}; oracle step sizes per iteration "
@@ -63,10 +64,14 @@ def test_kin_sqp_obstacles_vs_oracle(golden, solver):
     assert (st == 0).all(), st
     assert err.max() < U_TOL, np.argsort(err)[-5:]
     np.testing.assert_array_equal(u0, us[:, 0])
+    # x* = rollout(u*): against the device rollout kernel to 1e-12 (same model code), and against
+    # the host rollout to 1e-8 (numpy's cos / tan vs the device's differ by ulps, amplified over 20
+    # stages of trajectories that swerve round obstacles: 8.9e-10 .. 1.2e-9 measured on epsi_N)
+    assert np.abs(xs - xr).max() <= 1e-12 * (1.0 + np.abs(xr).max())
     x_own = Q.kin_predict(x0, us, kap, ds, 2.5)     # x* = rollout(u*) of the kernel's own u*
     dx = np.abs(xs - x_own)
     print("x* vs rollout(u*): max %.2e at %s" % (dx.max(), np.unravel_index(dx.argmax(), dx.shape)))
-    assert dx.max() < 1e-9
+    assert dx.max() < 1e-8
     # the merit of the final iterate never exceeds the start's
     phi_start = KS.merit(x0, ub, kap, ds, 2.5, W)
     phi_end = KS.merit(x0, us, kap, ds, 2.5, W)

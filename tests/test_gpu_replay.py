@@ -29,12 +29,12 @@ def data():
     return dict(np.load(os.path.join(GOLDEN, "replay_kat.npz"), allow_pickle=False))
 
 
-def _replay(data, run, sqp):
+def _replay(data, run, sqp, qp=None):
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(GOLDEN), "..", "scripts"))
     from replay_recorded import replay
     recs = json.loads(str(data["configs"]))
-    return replay(run, data, recs[run], sqp)
+    return replay(run, data, recs[run], sqp, qp=qp)
 
 
 def test_singletrack_replay_matches_ipopt(data):
@@ -42,6 +42,7 @@ def test_singletrack_replay_matches_ipopt(data):
     r = _replay(data, "singletrack_ippodromo", 40)
     print(json.dumps({k: v for k, v in r.items() if k != "example_plan"}))
     assert r["nonsolved"] == 0
+    assert r["plan_nan_steps"] == 0
     assert r["dFx_median"] < 0.01          # N (measured 2e-5)
     assert r["dw_median"] < 1e-5           # rad/s
     assert r["frac_within_1pct"] > 0.8      # measured 0.88
@@ -50,14 +51,22 @@ def test_singletrack_replay_matches_ipopt(data):
 
 
 def test_cascaded_replay_converges_to_ipopt(data):
-    """cascaded7_ippodromo (cascaded.yaml's N = 20 + M = 40 shape and weights), 413 steps:
-    the distance to IPOPT's commands shrinks with the SQP iterations."""
-    r10 = _replay(data, "cascaded7_ippodromo", 10)
-    r40 = _replay(data, "cascaded7_ippodromo", 40)
+    """cascaded7_ippodromo (cascaded.yaml's N = 20 + M = 40 shape and weights), 413 steps, with
+    the converged SQP setting (prox 0.01, 40 SQP iterations; the bench / closed-loop setting is
+    prox 0.1, 3-5 iterations): the median step matches IPOPT's command to ~1 N.  Round 3's sweep
+    (profiles/r03/replay_r03d.json): prox 0.1 / 0.03 / 0.01 / 0.003 at 40 iterations give median
+    |dFx| 24 / 9.2 / 1.2 / 2.7 N; the p90 (~400 N at every setting) comes from contiguous
+    stretches (e.g. steps 15-21, 192-203, 306-337) where the SQP and IPOPT settle in different
+    local optima of the nonconvex NLP (IPOPT at the front-tyre force bound with little steering,
+    the SQP steering more and pulling less), which more iterations do not change."""
+    r10 = _replay(data, "cascaded7_ippodromo", 10, qp={"prox": 0.01})
+    r40 = _replay(data, "cascaded7_ippodromo", 40, qp={"prox": 0.01})
     for r in (r10, r40):
         print(json.dumps({k: v for k, v in r.items() if k != "example_plan"}))
     assert r10["nonsolved"] == 0 and r40["nonsolved"] == 0
-    assert r40["dFx_median"] < 0.5 * r10["dFx_median"]
-    assert r40["dFx_median"] < 50.0         # N (measured 24 of |Fx| <= 6055)
-    assert r40["dw_median"] < 2e-3          # measured 4.5e-4
-    assert r40["plan_dev_median_m"] < 0.01  # measured 2e-3 m
+    assert r40["plan_nan_steps"] == 0 and r10["plan_nan_steps"] == 0   # our plans are finite
+    assert r40["dFx_median"] < 0.1 * r10["dFx_median"]
+    assert r40["dFx_median"] < 2.0          # N (measured 1.22 of |Fx| <= 6055)
+    assert r40["dw_median"] < 1e-4          # measured 4.3e-5
+    assert r40["frac_within_1pct"] > 0.5    # measured 0.53
+    assert r40["plan_dev_median_m"] < 1e-3  # measured 2.7e-4 m
