@@ -137,6 +137,7 @@ struct Smem {
   double kap[N], ds[N];
   double vz[64];            // broadcast: a length-n vector (z, dz, ...)
   double vc[64];            // broadcast: a length-NC vector (weights, residual terms)
+  double dinv[64];          // inverse pivots 1/L_kk of the current factor (uniform reads)
 };
 
 // stage index (1..N-1) of constraint row r
@@ -222,101 +223,149 @@ __device__ double h_dot(const Smem<N>& s, int lane) {
   return lds_dot<n, 1, 1>(lds_opaque(&s.H[j][0]), lds_opaque(&s.vz[0]));
 }
 
-// In-place right-looking Cholesky of the SPD matrix whose row `lane` is Mr.
-// On return Mr holds row `lane` of L (lower part), s.Lc its columns, s.dinv the
-// inverse pivots.  Returns false (uniform) if a pivot is not positive.
-//
-// One-column lookahead: in step k, as soon as column k is visible in LDS, column
-// k+1 is updated first, its pivot taken and column k+1 published to LDS; only
-// then does the rest of step k's trailing update run, so the LDS round trip of
-// column k+1 overlaps those FMAs instead of sitting on the critical path.
-template <int N>
-__device__ __forceinline__ double chol_pivot(double (&Mr)[Dims<N>::n], Smem<N>& s, int lane, int k, bool& ok,
-                                             double& dj) {
-  constexpr int n = Dims<N>::n;
-  const double dkk = lane_bcast(Mr[k], k);
-  ok = ok && (dkk > 0.0);
-  // 1/sqrt(dkk): hardware v_rsq_f64 + two Newton steps (full fp64 accuracy, a
-  // much shorter dependent chain than IEEE sqrt followed by IEEE divide)
-  double inv = __builtin_amdgcn_rsq(dkk);
-  inv = inv * (1.5 - 0.5 * dkk * inv * inv);
-  inv = inv * (1.5 - 0.5 * dkk * inv * inv);
-  const double lik = (lane == k) ? dkk * inv : Mr[k] * inv;
-  Mr[k] = lik;
-  // branch-free stores (dummy slots): lane-divergent ifs in this fully unrolled
-  // code make the register allocator spill hundreds of VGPRs
-  s.Lc[lane >= k && lane < n ? lc_off<n>(k) + lane - k : n * (n + 1) / 2] = lik;
-  dj = (lane == k) ? inv : dj;  // lane k keeps 1/L_kk
-  return lik;
+// 1/sqrt(d): hardware v_rsq_f64 + two Newton steps (full fp64 accuracy, a much shorter
+// dependent chain than IEEE sqrt followed by IEEE divide)
+__device__ __forceinline__ double rsq_nr(double d) {
+  double inv = __builtin_amdgcn_rsq(d);
+  inv = inv * (1.5 - 0.5 * d * inv * inv);
+  inv = inv * (1.5 - 0.5 * d * inv * inv);
+  return inv;
 }
 
+// In-place right-looking Cholesky of the SPD matrix whose row `lane` is Mr (the lower
+// part: entries above the diagonal are not kept).  On return Mr holds row `lane` of L,
+// s.Lc its columns and s.dinv the inverse pivots 1/L_kk (uniform reads).
+// Returns false (uniform) if a pivot is not positive.
+//
+// Two columns per step (the same operations in the same order as the column-by-column
+// algorithm, so the factor is bit-identical to it): the 2x2 diagonal block comes from
+// lanes k, k+1 by readlane, both pivots are taken in registers, both columns published to
+// LDS, and one LDS round trip serves the rank-2 trailing update -- half the round trips of
+// one column per step, whose latency (store -> load ~85 cycles, rsq + Newton ~52) set the
+// factorisation time (scripts/ubench/lat.hip, profiles/r03/ubench_r03d.txt).  Columns k+2,
+// k+3 are updated first (lookahead), so the next block's pivots overlap this block's FMAs.
 template <int N>
-__device__ bool cholesky(double (&Mr)[Dims<N>::n], Smem<N>& s, int lane, double& dj) {
+__device__ bool cholesky(double (&Mr)[Dims<N>::n], Smem<N>& s, int lane) {
   constexpr int n = Dims<N>::n;
+  static_assert(n % 2 == 0, "two-column blocks");
+  constexpr int DUMMY = n * (n + 1) / 2;
   bool ok = true;
-  double lik = chol_pivot<N>(Mr, s, lane, 0, ok, dj);
 #pragma unroll
-  for (int k = 0; k < n - 1; ++k) {
-    wave_sync();  // column k visible
-    fence();
-    const double* col = &s.Lc[lc_off<n>(k) - k];  // col[j] = L[j][k]
-    double cv[n];  // column k, issued at once so the loads overlap the pivot chain
+  for (int k = 0; k < n; k += 2) {
+    const double a = lane_bcast(Mr[k], k), b = lane_bcast(Mr[k], k + 1), c = lane_bcast(Mr[k + 1], k + 1);
+    const double i1 = rsq_nr(a);
+    const double l21 = b * i1;                      // L[k+1][k]
+    const double d2 = fma(-l21, l21, c);            // lane k+1's pivot after column k's update
+    const double i2 = rsq_nr(d2);
+    ok = ok && (a > 0.0) && (d2 > 0.0);
+    const double x = (lane == k) ? a * i1 : Mr[k] * i1;   // L[lane][k]
+    const double y = fma(-x, l21, Mr[k + 1]) * i2;         // L[lane][k+1] (lane k+1: d2 / sqrt(d2))
+    Mr[k] = x;
+    Mr[k + 1] = y;
+    // branch-free stores (dummy slots): lane-divergent ifs in this fully unrolled code make
+    // the register allocator spill hundreds of VGPRs
+    s.Lc[lane >= k && lane < n ? lc_off<n>(k) + lane - k : DUMMY] = x;
+    s.Lc[lane >= k + 1 && lane < n ? lc_off<n>(k + 1) + lane - k - 1 : DUMMY] = y;
+    s.dinv[k] = i1;
+    s.dinv[k + 1] = i2;
+    if (k + 2 < n) {
+      wave_sync();  // columns k, k+1 visible
+      fence();
+      const double* c0 = &s.Lc[lc_off<n>(k) - k];          // c0[j] = L[j][k]
+      const double* c1 = &s.Lc[lc_off<n>(k + 1) - k - 1];  // c1[j] = L[j][k+1]
+      // the columns' entries in chunks of CH rows, each chunk loaded one chunk ahead of its
+      // FMAs (all at once would hold 4 (n - k) more VGPRs next to Mr and spill)
+      constexpr int CH = 4;
+      const int J0 = k + 2, NCH = (n - J0 + CH - 1) / CH;  // compile-time after unrolling
+      double u0[2][CH], u1[2][CH];
+      auto load = [&](int ch, int buf) {
 #pragma unroll
-    for (int j = k + 1; j < n; ++j) cv[j] = col[j];
-    // lookahead: column k+1 and its pivot
-    Mr[k + 1] -= lik * cv[k + 1];
-    const double lik_next = chol_pivot<N>(Mr, s, lane, k + 1, ok, dj);
-    fence();
-    // rest of step k's trailing update
+        for (int q = 0; q < CH; ++q) {
+          const int j = J0 + ch * CH + q;
+          u0[buf][q] = j < n ? c0[j] : 0.0;
+          u1[buf][q] = j < n ? c1[j] : 0.0;
+        }
+      };
+      load(0, 0);
 #pragma unroll
-    for (int j = k + 2; j < n; ++j) Mr[j] -= lik * cv[j];
-    fence();
-    lik = lik_next;
+      for (int ch = 0; ch < NCH; ++ch) {
+        if (ch + 1 < NCH) load(ch + 1, (ch + 1) & 1);
+        fence();
+        // chunk 0 starts with columns k+2, k+3: the next block's pivots (lookahead)
+#pragma unroll
+        for (int q = 0; q < CH; ++q) {
+          const int j = J0 + ch * CH + q;
+          if (j < n) Mr[j] = fma(-y, u1[ch & 1][q], fma(-x, u0[ch & 1][q], Mr[j]));
+        }
+        fence();
+      }
+    }
   }
+  wave_sync();  // factor and inverse pivots visible to the solves
   return ok;
 }
 
-// Solve (L L') x = b, lane j holding b_j and its inverse pivot dj = 1/L_jj;
-// returns x_j.  The forward sweep reads L[i][k] from the row registers and
-// broadcasts y_k = acc_k d_k from lane k (no LDS on the chain); the backward
-// sweep reads L[k][i] (column i of the packed factor) from LDS, prefetched one
-// 8-step chunk ahead so the LDS latency stays off the dependent chain.
+// Solve (L L') x = b, lane j holding b_j; returns x_j.  Four unknowns per step: their
+// accumulators come from lanes k..k+3 by readlane, the 4x4 diagonal block of L and the
+// inverse pivots are uniform LDS reads (issued off the chain), the block is solved in
+// registers (the same operations in the same order as one unknown per step: bit-identical),
+// then every lane applies the four columns.  The forward sweep reads L[j][k] from the row
+// registers, the backward sweep L[k][j] (column j of the packed factor) from LDS, prefetched
+// one block ahead.  A 40-step readlane chain per sweep becomes a 10-step one.
 template <int N>
-__device__ double chol_solve(const double (&Lr)[Dims<N>::n], const Smem<N>& s, double dj, double b, int lane) {
+__device__ double chol_solve(const double (&Lr)[Dims<N>::n], const Smem<N>& s, double b, int lane) {
   constexpr int n = Dims<N>::n;
-  constexpr int CH = 8;
-  static_assert(n % CH == 0, "backward prefetch chunks");
+  constexpr int BB = 4;
+  static_assert(n % BB == 0, "four-unknown blocks");
   const int row = lane < n ? lane : 0;
   const int off = lc_off<n>(row) - row;
+  struct Blk {
+    double d0, d1, d2, d3, l10, l20, l30, l21, l31, l32;
+  };
+  auto blk = [&](int k) {
+    Blk o;
+    o.d0 = s.dinv[k]; o.d1 = s.dinv[k + 1]; o.d2 = s.dinv[k + 2]; o.d3 = s.dinv[k + 3];
+    o.l10 = s.Lc[lc_off<n>(k) + 1]; o.l20 = s.Lc[lc_off<n>(k) + 2]; o.l30 = s.Lc[lc_off<n>(k) + 3];
+    o.l21 = s.Lc[lc_off<n>(k + 1) + 1]; o.l31 = s.Lc[lc_off<n>(k + 1) + 2];
+    o.l32 = s.Lc[lc_off<n>(k + 2) + 1];
+    return o;
+  };
   double acc = b, y = 0.0;
 #pragma unroll
-  for (int k = 0; k < n; ++k) {  // L y = b
-    const double yk = lane_bcast(acc * dj, k);
-    y = (lane == k) ? yk : y;
-    acc -= Lr[k] * yk;
+  for (int k = 0; k < n; k += BB) {  // L y = b
+    const Blk cb = blk(k);
+    const double a0 = lane_bcast(acc, k), a1 = lane_bcast(acc, k + 1), a2 = lane_bcast(acc, k + 2),
+                 a3 = lane_bcast(acc, k + 3);
+    const double y0 = a0 * cb.d0;
+    const double y1 = fma(-cb.l10, y0, a1) * cb.d1;
+    const double y2 = fma(-cb.l21, y1, fma(-cb.l20, y0, a2)) * cb.d2;
+    const double y3 = fma(-cb.l32, y2, fma(-cb.l31, y1, fma(-cb.l30, y0, a3))) * cb.d3;
+    y = (lane == k) ? y0 : ((lane == k + 1) ? y1 : ((lane == k + 2) ? y2 : ((lane == k + 3) ? y3 : y)));
+    acc = fma(-Lr[k + 3], y3, fma(-Lr[k + 2], y2, fma(-Lr[k + 1], y1, fma(-Lr[k], y0, acc))));
   }
   acc = y;
   double x = 0.0;
-  double lk[2][CH];
-  auto fetch = [&](int c, int buf) {  // L[k][row] for k = n-1-c*CH ... n-CH-c*CH
+  double lk[2][BB];
+  auto fetch = [&](int k, int buf) {  // L[k+q][row] for the block starting at k
 #pragma unroll
-    for (int q = 0; q < CH; ++q) {
-      const int k = n - 1 - c * CH - q;
-      lk[buf][q] = s.Lc[k >= row ? off + k : 0];
-    }
+    for (int q = 0; q < BB; ++q) lk[buf][q] = s.Lc[k + q >= row ? off + k + q : 0];
   };
-  fetch(0, 0);
+  fetch(n - BB, 0);
 #pragma unroll
-  for (int c = 0; c < n / CH; ++c) {  // L' x = y: lane i < k needs L[k][i]
-    if (c + 1 < n / CH) fetch(c + 1, (c + 1) & 1);
+  for (int c = 0; c < n / BB; ++c) {  // L' x = y: lane i < k needs L[k][i]
+    const int k = n - BB - c * BB;
+    const Blk cb = blk(k);
+    if (k >= BB) fetch(k - BB, (c + 1) & 1);
     fence();
-#pragma unroll
-    for (int q = 0; q < CH; ++q) {
-      const int k = n - 1 - c * CH - q;
-      const double xk = lane_bcast(acc * dj, k);
-      x = (lane == k) ? xk : x;
-      acc -= lk[c & 1][q] * xk;
-    }
+    const double a0 = lane_bcast(acc, k), a1 = lane_bcast(acc, k + 1), a2 = lane_bcast(acc, k + 2),
+                 a3 = lane_bcast(acc, k + 3);
+    const double x3 = a3 * cb.d3;
+    const double x2 = fma(-cb.l32, x3, a2) * cb.d2;
+    const double x1 = fma(-cb.l21, x2, fma(-cb.l31, x3, a1)) * cb.d1;
+    const double x0 = fma(-cb.l10, x1, fma(-cb.l20, x2, fma(-cb.l30, x3, a0))) * cb.d0;
+    x = (lane == k) ? x0 : ((lane == k + 1) ? x1 : ((lane == k + 2) ? x2 : ((lane == k + 3) ? x3 : x)));
+    const double* L = lk[c & 1];
+    acc = fma(-L[0], x0, fma(-L[1], x1, fma(-L[2], x2, fma(-L[3], x3, acc))));
     fence();
   }
   return x;
@@ -781,8 +830,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
       build_normal_mfma<N>(Mr, s, wlo_b + whi_b, lane);
       VC_TACC(T_BUILD, t_build0)
       VC_TSTAMP(t_chol0)
-      double dj = 1.0;
-      const bool chol_ok = cholesky<N>(Mr, s, lane, dj);
+      const bool chol_ok = cholesky<N>(Mr, s, lane);
       VC_TACC(T_CHOL, t_chol0)
       if (!chol_ok) {
         // The barrier weights lambda/s of the active set (~1/mu) have made the
@@ -816,7 +864,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
         wave_sync();
         const double rhs = (lane < n) ? (-rd - eb - gt_dot<N>(s, lane)) : 0.0;
         VC_TSTAMP(t_sol0)
-        const double dz = chol_solve<N>(Mr, s, dj, rhs, lane);
+        const double dz = chol_solve<N>(Mr, s, rhs, lane);
         VC_TACC(T_SOLVE, t_sol0)
         wave_sync();
         s.vz[lane] = (lane < n) ? dz : 0.0;
@@ -913,8 +961,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
         const bool fi = (fmask >> i) & 1ull;
         Mr[i] = fixed ? (i == lane ? 1.0 : 0.0) : (fi ? 0.0 : Mr[i]);
       }
-      double dj = 1.0;
-      if (!cholesky<N>(Mr, s, lane, dj)) {
+      if (!cholesky<N>(Mr, s, lane)) {
         pchol_fail = true;
         break;
       }
@@ -926,7 +973,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
         s.vc[lane] = (lane < NC) ? (nu_c - rho_c * bnd_c) : 0.0;
         wave_sync();
         const double rhs = (lane < n) ? (fixed ? zfix : (base - gt_dot<N>(s, lane))) : 0.0;
-        zp = chol_solve<N>(Mr, s, dj, rhs, lane);
+        zp = chol_solve<N>(Mr, s, rhs, lane);
         wave_sync();
         s.vz[lane] = (lane < n) ? zp : 0.0;
         wave_sync();
