@@ -305,67 +305,50 @@ __device__ bool cholesky(double (&Mr)[Dims<N>::n], Smem<N>& s, int lane) {
   return ok;
 }
 
-// Solve (L L') x = b, lane j holding b_j; returns x_j.  Four unknowns per step: their
-// accumulators come from lanes k..k+3 by readlane, the 4x4 diagonal block of L and the
-// inverse pivots are uniform LDS reads (issued off the chain), the block is solved in
-// registers (the same operations in the same order as one unknown per step: bit-identical),
-// then every lane applies the four columns.  The forward sweep reads L[j][k] from the row
-// registers, the backward sweep L[k][j] (column j of the packed factor) from LDS, prefetched
-// one block ahead.  A 40-step readlane chain per sweep becomes a 10-step one.
+// Solve (L L') x = b, lane j holding b_j; returns x_j.  The forward sweep reads L[i][k]
+// from the row registers and broadcasts y_k = acc_k / L_kk from lane k (no LDS on the chain);
+// the backward sweep reads L[k][i] (column i of the packed factor) from LDS, prefetched one
+// 8-step chunk ahead so the LDS latency stays off the dependent chain.  (Round 3 measured a
+// four-unknown blocked variant -- uniform 4x4 diagonal blocks from LDS, a 10-step readlane
+// chain per sweep -- 13 % slower: the sweeps are bound by instruction issue, not by the chain,
+// profiles/r03/section_cycles_r03g.txt.)
 template <int N>
 __device__ double chol_solve(const double (&Lr)[Dims<N>::n], const Smem<N>& s, double b, int lane) {
   constexpr int n = Dims<N>::n;
-  constexpr int BB = 4;
-  static_assert(n % BB == 0, "four-unknown blocks");
+  constexpr int CH = 8;
+  static_assert(n % CH == 0, "backward prefetch chunks");
   const int row = lane < n ? lane : 0;
   const int off = lc_off<n>(row) - row;
-  struct Blk {
-    double d0, d1, d2, d3, l10, l20, l30, l21, l31, l32;
-  };
-  auto blk = [&](int k) {
-    Blk o;
-    o.d0 = s.dinv[k]; o.d1 = s.dinv[k + 1]; o.d2 = s.dinv[k + 2]; o.d3 = s.dinv[k + 3];
-    o.l10 = s.Lc[lc_off<n>(k) + 1]; o.l20 = s.Lc[lc_off<n>(k) + 2]; o.l30 = s.Lc[lc_off<n>(k) + 3];
-    o.l21 = s.Lc[lc_off<n>(k + 1) + 1]; o.l31 = s.Lc[lc_off<n>(k + 1) + 2];
-    o.l32 = s.Lc[lc_off<n>(k + 2) + 1];
-    return o;
-  };
+  const double dj = s.dinv[row];
   double acc = b, y = 0.0;
 #pragma unroll
-  for (int k = 0; k < n; k += BB) {  // L y = b
-    const Blk cb = blk(k);
-    const double a0 = lane_bcast(acc, k), a1 = lane_bcast(acc, k + 1), a2 = lane_bcast(acc, k + 2),
-                 a3 = lane_bcast(acc, k + 3);
-    const double y0 = a0 * cb.d0;
-    const double y1 = fma(-cb.l10, y0, a1) * cb.d1;
-    const double y2 = fma(-cb.l21, y1, fma(-cb.l20, y0, a2)) * cb.d2;
-    const double y3 = fma(-cb.l32, y2, fma(-cb.l31, y1, fma(-cb.l30, y0, a3))) * cb.d3;
-    y = (lane == k) ? y0 : ((lane == k + 1) ? y1 : ((lane == k + 2) ? y2 : ((lane == k + 3) ? y3 : y)));
-    acc = fma(-Lr[k + 3], y3, fma(-Lr[k + 2], y2, fma(-Lr[k + 1], y1, fma(-Lr[k], y0, acc))));
+  for (int k = 0; k < n; ++k) {  // L y = b
+    const double yk = lane_bcast(acc * dj, k);
+    y = (lane == k) ? yk : y;
+    acc -= Lr[k] * yk;
   }
   acc = y;
   double x = 0.0;
-  double lk[2][BB];
-  auto fetch = [&](int k, int buf) {  // L[k+q][row] for the block starting at k
+  double lk[2][CH];
+  auto fetch = [&](int c, int buf) {  // L[k][row] for k = n-1-c*CH ... n-CH-c*CH
 #pragma unroll
-    for (int q = 0; q < BB; ++q) lk[buf][q] = s.Lc[k + q >= row ? off + k + q : 0];
+    for (int q = 0; q < CH; ++q) {
+      const int k = n - 1 - c * CH - q;
+      lk[buf][q] = s.Lc[k >= row ? off + k : 0];
+    }
   };
-  fetch(n - BB, 0);
+  fetch(0, 0);
 #pragma unroll
-  for (int c = 0; c < n / BB; ++c) {  // L' x = y: lane i < k needs L[k][i]
-    const int k = n - BB - c * BB;
-    const Blk cb = blk(k);
-    if (k >= BB) fetch(k - BB, (c + 1) & 1);
+  for (int c = 0; c < n / CH; ++c) {  // L' x = y: lane i < k needs L[k][i]
+    if (c + 1 < n / CH) fetch(c + 1, (c + 1) & 1);
     fence();
-    const double a0 = lane_bcast(acc, k), a1 = lane_bcast(acc, k + 1), a2 = lane_bcast(acc, k + 2),
-                 a3 = lane_bcast(acc, k + 3);
-    const double x3 = a3 * cb.d3;
-    const double x2 = fma(-cb.l32, x3, a2) * cb.d2;
-    const double x1 = fma(-cb.l21, x2, fma(-cb.l31, x3, a1)) * cb.d1;
-    const double x0 = fma(-cb.l10, x1, fma(-cb.l20, x2, fma(-cb.l30, x3, a0))) * cb.d0;
-    x = (lane == k) ? x0 : ((lane == k + 1) ? x1 : ((lane == k + 2) ? x2 : ((lane == k + 3) ? x3 : x)));
-    const double* L = lk[c & 1];
-    acc = fma(-L[0], x0, fma(-L[1], x1, fma(-L[2], x2, fma(-L[3], x3, acc))));
+#pragma unroll
+    for (int q = 0; q < CH; ++q) {
+      const int k = n - 1 - c * CH - q;
+      const double xk = lane_bcast(acc * dj, k);
+      x = (lane == k) ? xk : x;
+      acc -= lk[c & 1][q] * xk;
+    }
     fence();
   }
   return x;
