@@ -220,7 +220,14 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
   // (oracle/casc_sqp.py, oracle/dyn_sqp.py domain_step)
   int tries = 0, sq = 0;
   bool first = true, test = false;  // test: the iterate's own rollout is inside the domain
+  const int l_out = l, k_out = k;
   for (;;) {
+    // lane coordinates re-laundered every SQP iteration: lane masks derived from them are
+    // recomputed inside the loop instead of being hoisted out of it and spilled
+    int l = l_out, k = k_out;
+    asm volatile("" : "+v"(l), "+v"(k));
+    const bool stl = l < H;
+    const bool pm = k >= N;
     // ---------------- predict (lane 0: RK4, switch, point-mass Euler) ----------------
     // the only rollout site; flag[2]: finite and inside both models' domain (casc_in_domain)
     if (l == 0) {

@@ -242,7 +242,23 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
   // (the iterate in uo, the scaled step in u.q.v[k][7..8], untouched by the rollout)
   int tries = 0, sq = 0;
   bool first = true, test = false;  // test: the iterate's own rollout is inside the domain
+  const int l_out = l, k_out = k, hi_out = hi, hj_out = hj, pi_out = pi, pj_out = pj;
   for (;;) {
+    // The lane coordinates, lane roles and the kernel-argument pointer are re-laundered every
+    // SQP iteration: whatever the body derives from them (lane masks, scaled weights, ...) is
+    // then recomputed inside the loop instead of being hoisted out of it and held -- spilled --
+    // across the linearisation (528 B/lane of scratch for the Fiala tyre before).
+    int l = l_out, k = k_out, hi = hi_out, hj = hj_out, pi = pi_out, pj = pj_out;
+    asm volatile("" : "+v"(l), "+v"(k), "+v"(hi), "+v"(hj), "+v"(pi), "+v"(pj));
+    const bool stl = l < N;
+    const int hslot = qslot(hi, hj), hci = vcol(hi), hcj = vcol(hj);
+    const int sc = l < 9 ? vcol(l) : -1;
+    const StSqpArgs* Ap = (const StSqpArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(Ap));
+    const StSqpArgs& A = *Ap;
+    const vc_dyn_mpc& W = A.w;
+    DynCoef<double> c = A.car;
+    c.tyre = TYRE;
     // ---------------- predict (lane 0, serial RK4): xs = rollout(ubar) ----------------
     // the only rollout site (a second one makes the compiler outline it and spill);
     // flag[1]: finite, flag[2]: inside the spatial model's domain (Ux > 0, s' > 0)
