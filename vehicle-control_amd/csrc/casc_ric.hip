@@ -65,16 +65,27 @@ struct CrSmem {
   static constexpr int H = N + M;
   double xs[H][8];    // prediction: single-track states k < N, point-mass (V, s, ey, epsi, t) k >= N
   double ub[H][2];    // current ubar
-  double uo[H][2];    // the iterate before the SQP step under test (domain cut-back)
   double kap[H], dsv[H];
   double J[H][6][8];  // [A6 | B6 diag(S, 1 or S)] of the transition out of stage k
   union {
     struct {
       double Qt[H][NQ];  // stage Hessian + barrier, this iteration
-      double gr[H][9];   // stage gradient Q v + q + C' lam
-      double h[H][9];    // linear term of the current LQ solve
-      double v[H][9];    // QP iterate (xt, u)
-      double dv[H][9];   // Newton direction
+      // stage vector, three lives per interior-point iteration: the gradient Q v + q + C' lam
+      // (residuals -> dual residual sweep), the LQ right-hand side h (set_h -> backward pass),
+      // the direction dv (forward pass -> step); after the QP: the pre-step iterate uo in
+      // [0..1] and the step dz in [2..3] (SQP update -> domain cut-back).  The QP iterate v
+      // itself lives in its lane's registers.  During the Riccati factorisation (between the
+      // dual residual sweep and set_h: g dead) the same space holds the factorisation's
+      // scratch f: cost-to-go P, T = P [A B], stage Hessian Hm.  (At M = 40 the block drops from
+      // 68 KB to 52 KB: three one-wave workgroups per CU instead of two.)
+      union {
+        double g[H][9];
+        struct {
+          double P[7][7];
+          double T[7][8];
+          double Hm[9][9];
+        } f;
+      };
       double K[H][2][7];
       double Hi[H][3];   // Huu^-1 (00, 01, 11)
       double kk[H][2];
@@ -85,9 +96,6 @@ struct CrSmem {
       double gfy[6];         // Fy_f + Fy_r at stage N-1: value + gradient over (Ux, Uy, r, delta, Fx)
     } l;
   } u;
-  double P[7][7];
-  double T[7][8];
-  double Hm[9][9];
   // model coefficients and weights: each phase loads its own register copy from here (held in
   // registers across the SQP loop they were spilled to scratch)
   DynCoef<double> car;
@@ -215,8 +223,8 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
   double last_res = 0.0, last_mu = 0.0;
   const double tol_r = 1e-10, tol_mu = 1e-13;
 
-  // SQP update state: a step under test (tries > 0) is ub = uo + 2^-(tries-1) du (du in
-  // u.q.v[k][7..8], untouched by the rollout), the last try the unchanged iterate
+  // SQP update state: a step under test (tries > 0) is ub = uo + 2^-(tries-1) du (uo, du in
+  // u.q.g[k][0..3], untouched by the rollout), the last try the unchanged iterate
   // (oracle/casc_sqp.py, oracle/dyn_sqp.py domain_step)
   int tries = 0, sq = 0;
   bool first = true, test = false;  // test: the iterate's own rollout is inside the domain
@@ -278,10 +286,11 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       if (test && s.flag[2] == 0 && tries <= DOM_HALVINGS) {
         const double a = tries < DOM_HALVINGS ? ldexp(1.0, -tries) : 0.0;
         if (stl) {
-          const double u0v = s.uo[k][0], u1v = s.uo[k][1];
-          s.ub[k][0] = a > 0.0 ? u0v + a * (s.u.q.v[k][7] * S) : u0v;
-          if (pm) s.ub[k][1] = a > 0.0 ? u1v + a * (s.u.q.v[k][8] * S) : u1v;
-          else s.ub[k][1] = a > 0.0 ? fmin(fmax(u1v + a * s.u.q.v[k][8], s.w.w_min), s.w.w_max) : u1v;
+          const double u0v = s.u.q.g[k][0], u1v = s.u.q.g[k][1];  // uo
+          const double d0 = s.u.q.g[k][2], d1 = s.u.q.g[k][3];
+          s.ub[k][0] = a > 0.0 ? u0v + a * (d0 * S) : u0v;
+          if (pm) s.ub[k][1] = a > 0.0 ? u1v + a * (d1 * S) : u1v;
+          else s.ub[k][1] = a > 0.0 ? fmin(fmax(u1v + a * d1, s.w.w_min), s.w.w_max) : u1v;
         }
         ++tries;
         WSYNC();
@@ -610,11 +619,9 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     for (int e = 0; e < 9; ++e) qm = fmax(qm, fabs(qc[e]));
     const double rtol = tol_r * (1.0 + wmax(stl ? qm : 0.0));
     WSYNC();  // the linearisation scratch is dead from here: the QP arrays alias it
-    if (stl) {
+    double vk[9];  // the QP iterate (xt, u) of this lane's stage
 #pragma unroll
-      for (int e = 0; e < 9; ++e) s.u.q.v[k][e] = 0.0;
-    }
-    WSYNC();
+    for (int e = 0; e < 9; ++e) vk[e] = 0.0;
 
     // ---- LQ machinery (st_sqp.hip's, over H stages) -----------------------------------
     // Riccati lane roles: H entry (hi, hj), hi <= hj, for lanes < 45; P entry (pi, pj) for
@@ -655,22 +662,22 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     auto fac_stage = [&](int kk, const FacOps& o) -> bool {
       double hv = hq * o.qv;
       if (kk < H - 1) {  // uniform
-        double acc = tpm * s.P[ta][6];
+        double acc = tpm * s.u.q.f.P[ta][6];
 #pragma unroll
-        for (int e = 0; e < 6; ++e) acc += s.P[ta][e] * o.JT[e];
-        if (l < 56) s.T[ta][tj] = acc;
+        for (int e = 0; e < 6; ++e) acc += s.u.q.f.P[ta][e] * o.JT[e];
+        if (l < 56) s.u.q.f.T[ta][tj] = acc;
         WSYNC();
-        double a2 = hpm * s.T[6][hcjc];
+        double a2 = hpm * s.u.q.f.T[6][hcjc];
 #pragma unroll
-        for (int e = 0; e < 6; ++e) a2 += o.JH[e] * s.T[e][hcjc];
+        for (int e = 0; e < 6; ++e) a2 += o.JH[e] * s.u.q.f.T[e][hcjc];
         hv += hdyn * a2;
       }
       if (l < 45) {
-        s.Hm[hi][hj] = hv;
-        s.Hm[hj][hi] = hv;
+        s.u.q.f.Hm[hi][hj] = hv;
+        s.u.q.f.Hm[hj][hi] = hv;
       }
       WSYNC();
-      const double h00 = s.Hm[7][7], h01 = s.Hm[7][8], h11 = s.Hm[8][8];
+      const double h00 = s.u.q.f.Hm[7][7], h01 = s.u.q.f.Hm[7][8], h11 = s.u.q.f.Hm[8][8];
       const double det = h00 * h11 - h01 * h01;
       // IEEE-exact reciprocal (tests/test_gpu_numerics.py): the plain v_rcp_f64 + Newton form turns
       // det = +inf (h00 h11 overflowing at barrier weights ~1e154) into NaN where 1/det = 0
@@ -679,12 +686,12 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       {
         const int kc = l >= 28 && l < 42 ? (l - 28) / 7 : 0, ki = l >= 28 && l < 42 ? (l - 28) % 7 : 0;
         const int ci = l < 28 ? pi : ki;
-        const double x0 = s.Hm[7][ci], x1 = s.Hm[8][ci], y0 = s.Hm[7][pj], y1 = s.Hm[8][pj];
-        const double hpp = s.Hm[pi][pj];
+        const double x0 = s.u.q.f.Hm[7][ci], x1 = s.u.q.f.Hm[8][ci], y0 = s.u.q.f.Hm[7][pj], y1 = s.u.q.f.Hm[8][pj];
+        const double hpp = s.u.q.f.Hm[pi][pj];
         if (l < 28) {
           const double pv = hpp - (x0 * (i00 * y0 + i01 * y1) + x1 * (i01 * y0 + i11 * y1));
-          s.P[pi][pj] = pv;
-          s.P[pj][pi] = pv;
+          s.u.q.f.P[pi][pj] = pv;
+          s.u.q.f.P[pj][pi] = pv;
         } else if (l < 42) {
           s.u.q.K[kk][kc][ki] = kc == 0 ? -(i00 * x0 + i01 * x1) : -(i01 * x0 + i11 * x1);
         } else if (l == 42) {
@@ -765,13 +772,13 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       for (int e = 0; e < 6; ++e) acc += o.w[e] * xb[e];
       const double uk = acc + o.w[6] * xb[6] + o.w[7];
       const double u0 = bcast(uk, 7), u1 = bcast(uk, 8);
-      if (l < 9) s.u.q.dv[kk][l] = fk ? uk : X;
+      if (l < 9) s.u.q.g[kk][l] = fk ? uk : X;
       const double xn = acc + o.w[6] * u0 + o.w[7] * u1;
       return l < 6 ? xn : (l == 6 ? u0 : 0.0);
     };
     auto lq_solve = [&]() {
       BwdOps A1, B1;
-      bwd_load(H - 1, s.u.q.h, A1);
+      bwd_load(H - 1, s.u.q.g, A1);
       double pv = 0.0;
       auto bstage = [&](int kk, const BwdOps& o) {
         const double g = bwd_g(kk, o, pv);
@@ -783,10 +790,10 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
 #pragma unroll 1
       for (int kk = H - 1; kk >= 0; kk -= 2) {
         const int k1 = kk >= 1 ? kk - 1 : 0, k2 = kk >= 2 ? kk - 2 : 0;
-        bwd_load(k1, s.u.q.h, B1);
+        bwd_load(k1, s.u.q.g, B1);
         bstage(kk, A1);
         if (kk >= 1) {
-          bwd_load(k2, s.u.q.h, A1);
+          bwd_load(k2, s.u.q.g, A1);
           bstage(kk - 1, B1);
         }
       }
@@ -808,7 +815,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     };
     auto dual_residual = [&]() -> double {
       BwdOps A3, B3;
-      bwd_load(H - 1, s.u.q.gr, A3);
+      bwd_load(H - 1, s.u.q.g, A3);
       double rho = 0.0, rmax = 0.0;
       auto rstage = [&](int kk, const BwdOps& o) {
         const double g = bwd_g(kk, o, rho);
@@ -818,10 +825,10 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
 #pragma unroll 1
       for (int kk = H - 1; kk >= 0; kk -= 2) {
         const int k1 = kk >= 1 ? kk - 1 : 0, k2 = kk >= 2 ? kk - 2 : 0;
-        bwd_load(k1, s.u.q.gr, B3);
+        bwd_load(k1, s.u.q.g, B3);
         rstage(kk, A3);
         if (kk >= 1) {
-          bwd_load(k2, s.u.q.gr, A3);
+          bwd_load(k2, s.u.q.g, A3);
           rstage(kk - 1, B3);
         }
       }
@@ -833,10 +840,8 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     bool conv = false, fail = false;
 #pragma unroll 1
     for (; it < s.qp.max_iter; ++it) {
-      double vk[9], rp[NR], wg[NR], grk[9], val[NR];
+      double rp[NR], wg[NR], grk[9], val[NR];
       double rpm = 0.0, mus = 0.0;
-#pragma unroll
-      for (int e = 0; e < 9; ++e) vk[e] = s.u.q.v[k][e];
       row_values(R, vk, val);
 #pragma unroll
       for (int i = 0; i < NR; ++i) {
@@ -856,7 +861,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       }
       if (stl) {
 #pragma unroll
-        for (int e = 0; e < 9; ++e) s.u.q.gr[k][e] = grk[e];
+        for (int e = 0; e < 9; ++e) s.u.q.g[k][e] = grk[e];
         double Qt[NQ];
 #pragma unroll
         for (int e = 0; e < NQ; ++e) Qt[e] = Qc[e];
@@ -904,7 +909,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
           for (int e = 0; e < 9; ++e) hk[e] = grk[e];
           row_adjoint(R, y, hk);
 #pragma unroll
-          for (int e = 0; e < 9; ++e) s.u.q.h[k][e] = hk[e];
+          for (int e = 0; e < 9; ++e) s.u.q.g[k][e] = hk[e];
         }
         WSYNC();
       };
@@ -913,7 +918,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       double dsa[NR], dla[NR], cdv[NR], dvk[9];
       double amin = 1.0;
 #pragma unroll
-      for (int e = 0; e < 9; ++e) dvk[e] = s.u.q.dv[k][e];
+      for (int e = 0; e < 9; ++e) dvk[e] = s.u.q.g[k][e];
       row_values(R, dvk, cdv);
 #pragma unroll
       for (int i = 0; i < NR; ++i) {
@@ -937,7 +942,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       set_h(rcs);
       lq_solve();
 #pragma unroll
-      for (int e = 0; e < 9; ++e) dvk[e] = s.u.q.dv[k][e];
+      for (int e = 0; e < 9; ++e) dvk[e] = s.u.q.g[k][e];
       row_values(R, dvk, cdv);
       amin = 1.0;
 #pragma unroll
@@ -956,7 +961,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
           }
         }
 #pragma unroll
-        for (int e = 0; e < 9; ++e) s.u.q.v[k][e] = vk[e] + alpha * dvk[e];
+        for (int e = 0; e < 9; ++e) vk[e] += alpha * dvk[e];
       }
       WSYNC();
     }
@@ -969,11 +974,13 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     // tested by the next rollout (domain cut-back above)
     if (stl) {
       const double u0v = s.ub[k][0], u1v = s.ub[k][1];
-      s.uo[k][0] = u0v;
-      s.uo[k][1] = u1v;
-      s.ub[k][0] = u0v + s.u.q.v[k][7] * S;
-      if (pm) s.ub[k][1] = u1v + s.u.q.v[k][8] * S;
-      else s.ub[k][1] = fmin(fmax(u1v + s.u.q.v[k][8], s.w.w_min), s.w.w_max);
+      s.u.q.g[k][0] = u0v;
+      s.u.q.g[k][1] = u1v;
+      s.u.q.g[k][2] = vk[7];
+      s.u.q.g[k][3] = vk[8];
+      s.ub[k][0] = u0v + vk[7] * S;
+      if (pm) s.ub[k][1] = u1v + vk[8] * S;
+      else s.ub[k][1] = fmin(fmax(u1v + vk[8], s.w.w_min), s.w.w_max);
     }
     test = s.flag[2] != 0;  // from an iterate outside the domain: the full step, untested
     tries = 1;

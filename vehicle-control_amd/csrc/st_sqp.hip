@@ -56,32 +56,54 @@ __host__ __device__ constexpr int qslot(int i, int j) {
 // stage vector index -> column of [A6 | B6] (-1 for p: no dynamics enters through it)
 __host__ __device__ constexpr int vcol(int i) { return i < 6 ? i : (i == 6 ? -1 : i - 1); }
 
+// LDS layout.  Strides: every array a lane-per-stage phase reads or writes (residuals, stage
+// data, linearisation) has an odd number of doubles per stage (or per matrix row read across
+// lanes), so the 32 lanes of a ds_read_b64 group land on 32 distinct bank pairs ((a/4) mod 64)
+// and the 16 lanes of a ds_write_b64 group on 16 ((a/4) mod 32); pad slots are never touched.
+// Size: one stage vector g carries the dual-residual gradient, the LQ right-hand side, the
+// Newton direction and the SQP cut-back's data in turn, and the Riccati scratch between them
+// (disjoint live ranges, below); the QP iterate stays in registers.  N = 40 then fits 4 one-wave
+// workgroups per CU (one per SIMD; 48.5 KB before left one SIMD idle), N = 60 fits 3 (was 2).
+struct StJ {  // [A6 | B6 diag(S, 1)] of one step, rows Ux, Uy, r, delta, ey, epsi; + 1 pad
+  double m[6][8];
+  double pad;
+  __device__ __forceinline__ double* operator[](int r) { return m[r]; }
+  __device__ __forceinline__ const double* operator[](int r) const { return m[r]; }
+};
 template <int N>
 struct StSmem {
-  double xs[N][8];    // prediction (N columns, dynamics for k < N-1)
-  double ub[N][2];    // current ubar
-  double uo[N][2];    // the iterate before the SQP step under test (domain cut-back)
+  double xs[N][9];    // prediction (N columns, dynamics for k < N-1); [8] pad
+  double ub[N][3];    // current ubar; [2] pad
   double kap[N], dsv[N];
-  double J[N][6][8];  // [A6 | B6 diag(S, 1)] of step k (rows/cols Ux, Uy, r, delta, ey, epsi | dFx, dw)
+  StJ J[N];            // J[k][row][col], cols Ux, Uy, r, delta, ey, epsi | dFx, dw
   union {
     struct {
-      double Qt[N][NQ];  // stage Hessian + barrier, this iteration
-      double gr[N][9];   // stage gradient Q v + q + C' lam
-      double h[N][9];    // linear term of the current LQ solve
-      double v[N][9];    // QP iterate (xt, u)
-      double dv[N][9];   // Newton direction
+      double Qt[N][NQ + 1];  // stage Hessian + barrier, this iteration; [NQ] pad
+      // stage vector, three lives per interior-point iteration: the gradient Q v + q + C' lam
+      // (residuals -> dual residual sweep), the LQ right-hand side h (set_h -> backward pass),
+      // the direction dv (forward pass -> step); after the QP: the pre-step iterate uo in
+      // [0..1] and the step dz in [2..3] (SQP update -> domain cut-back).  The QP iterate v
+      // itself lives in its lane's registers.  During the Riccati factorisation (between the
+      // dual residual sweep and set_h: g dead) the same space holds the factorisation's
+      // scratch f: cost-to-go P, T = P [A B], stage Hessian Hm.
+      union {
+        double g[N][9];
+        struct {
+          double P[7][7];
+          double T[7][8];
+          double Hm[9][9];
+        } f;
+      };
       double K[N][2][7];
       double Hi[N][3];   // Huu^-1 (00, 01, 11)
       double kk[N][2];
     } q;
     struct {
+      // (unpadded: this member sets the union's size; its reads are once per SQP iteration)
       double trow[N][8];     // t-row of step k over (y | dFx, dw)
       double st[N][7][6];    // stage functions: value + gradient over (Ux, Uy, r, delta, Fx)
     } l;
   } u;
-  double P[7][7];
-  double T[7][8];
-  double Hm[9][9];
   int flag[4];
 };
 
@@ -221,7 +243,6 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     hi = i;
     hj = i + q;
   }
-  const int hslot = qslot(hi, hj), hci = vcol(hi), hcj = vcol(hj);
   // P entry (pi, pj) for lanes < 28
   int pi = 0, pj = 0;
   {
@@ -230,7 +251,6 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     pi = i;
     pj = i + q;
   }
-  const int sc = l < 9 ? vcol(l) : -1;  // sweep lanes 0..8: column of [A6 | B6] of v index l
 
   int it_total = 0, it_max = 0;
   bool all_conv = true, any_fail = false;
@@ -239,7 +259,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
 
   // SQP update state: a step under test (tries > 0) is ub = u + 2^-(tries-1) du, the last try
   // the unchanged iterate (oracle/dyn_sqp.py domain_step)
-  // (the iterate in uo, the scaled step in u.q.v[k][7..8], untouched by the rollout)
+  // (the iterate uo in u.q.g[k][0..1], the scaled step in u.q.g[k][2..3], untouched by the rollout)
   int tries = 0, sq = 0;
   bool first = true, test = false;  // test: the iterate's own rollout is inside the domain
   const int l_out = l, k_out = k, hi_out = hi, hj_out = hj, pi_out = pi, pj_out = pj;
@@ -252,7 +272,6 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     asm volatile("" : "+v"(l), "+v"(k), "+v"(hi), "+v"(hj), "+v"(pi), "+v"(pj));
     const bool stl = l < N;
     const int hslot = qslot(hi, hj), hci = vcol(hi), hcj = vcol(hj);
-    const int sc = l < 9 ? vcol(l) : -1;
     const StSqpArgs* Ap = (const StSqpArgs*)__builtin_amdgcn_kernarg_segment_ptr();
     asm volatile("" : "+s"(Ap));
     const StSqpArgs& A = *Ap;
@@ -295,9 +314,10 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       if (test && s.flag[2] == 0 && tries <= DOM_HALVINGS) {
         const double a = tries < DOM_HALVINGS ? ldexp(1.0, -tries) : 0.0;
         if (stl) {
-          const double uF = s.uo[k][0], uW = s.uo[k][1];
-          s.ub[k][0] = a > 0.0 ? uF + a * (s.u.q.v[k][7] * S) : uF;
-          s.ub[k][1] = a > 0.0 ? fmin(fmax(uW + a * s.u.q.v[k][8], W.w_min), W.w_max) : uW;
+          const double uF = s.u.q.g[k][0], uW = s.u.q.g[k][1];  // uo: the pre-step iterate
+          const double d0 = s.u.q.g[k][2], d1 = s.u.q.g[k][3];
+          s.ub[k][0] = a > 0.0 ? uF + a * (d0 * S) : uF;
+          s.ub[k][1] = a > 0.0 ? fmin(fmax(uW + a * d1, W.w_min), W.w_max) : uW;
         }
         ++tries;
         WSYNC();
@@ -481,11 +501,9 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     for (int e = 0; e < 9; ++e) qm = fmax(qm, fabs(qc[e]));
     const double rtol = tol_r * (1.0 + wmax(stl ? qm : 0.0));
     WSYNC();  // the linearisation scratch is dead from here: the QP arrays alias it
-    if (stl) {
+    double vk[9];  // the QP iterate (xt, u) of this lane's stage
 #pragma unroll
-      for (int e = 0; e < 9; ++e) s.u.q.v[k][e] = 0.0;
-    }
-    WSYNC();
+    for (int e = 0; e < 9; ++e) vk[e] = 0.0;
     ST_ACC(ST_SETUP, t_s0)
 
     // ---- LQ machinery -----------------------------------------------------------------
@@ -520,22 +538,22 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     auto fac_stage = [&](int kk, const FacOps& o) -> bool {
       double hv = hq * o.qv;
       if (kk < N - 1) {  // uniform
-        double acc = tpm * s.P[ta][6];
+        double acc = tpm * s.u.q.f.P[ta][6];
 #pragma unroll
-        for (int e = 0; e < 6; ++e) acc += s.P[ta][e] * o.JT[e];
-        if (l < 56) s.T[ta][tj] = acc;
+        for (int e = 0; e < 6; ++e) acc += s.u.q.f.P[ta][e] * o.JT[e];
+        if (l < 56) s.u.q.f.T[ta][tj] = acc;
         WSYNC();
-        double a2 = hpm * s.T[6][hcjc];
+        double a2 = hpm * s.u.q.f.T[6][hcjc];
 #pragma unroll
-        for (int e = 0; e < 6; ++e) a2 += o.JH[e] * s.T[e][hcjc];
+        for (int e = 0; e < 6; ++e) a2 += o.JH[e] * s.u.q.f.T[e][hcjc];
         hv += hdyn * a2;
       }
       if (l < 45) {
-        s.Hm[hi][hj] = hv;
-        s.Hm[hj][hi] = hv;
+        s.u.q.f.Hm[hi][hj] = hv;
+        s.u.q.f.Hm[hj][hi] = hv;
       }
       WSYNC();
-      const double h00 = s.Hm[7][7], h01 = s.Hm[7][8], h11 = s.Hm[8][8];
+      const double h00 = s.u.q.f.Hm[7][7], h01 = s.u.q.f.Hm[7][8], h11 = s.u.q.f.Hm[8][8];
       const double det = h00 * h11 - h01 * h01;
       // 1 / det: v_rcp_f64 + two Newton steps (full fp64 accuracy, no IEEE divide sequence)
       // IEEE-exact reciprocal (tests/test_gpu_numerics.py): the plain v_rcp_f64 + Newton form turns
@@ -546,12 +564,12 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
         // lanes 0..27: P entry (pi, pj); lanes 28..41: K entry; lane 42: Huu^-1
         const int kc = l >= 28 && l < 42 ? (l - 28) / 7 : 0, ki = l >= 28 && l < 42 ? (l - 28) % 7 : 0;
         const int ci = l < 28 ? pi : ki;
-        const double x0 = s.Hm[7][ci], x1 = s.Hm[8][ci], y0 = s.Hm[7][pj], y1 = s.Hm[8][pj];
-        const double hpp = s.Hm[pi][pj];
+        const double x0 = s.u.q.f.Hm[7][ci], x1 = s.u.q.f.Hm[8][ci], y0 = s.u.q.f.Hm[7][pj], y1 = s.u.q.f.Hm[8][pj];
+        const double hpp = s.u.q.f.Hm[pi][pj];
         if (l < 28) {
           const double pv = hpp - (x0 * (i00 * y0 + i01 * y1) + x1 * (i01 * y0 + i11 * y1));
-          s.P[pi][pj] = pv;
-          s.P[pj][pi] = pv;
+          s.u.q.f.P[pi][pj] = pv;
+          s.u.q.f.P[pj][pi] = pv;
         } else if (l < 42) {
           s.u.q.K[kk][kc][ki] = kc == 0 ? -(i00 * x0 + i01 * x1) : -(i01 * x0 + i11 * x1);
         } else if (l == 42) {
@@ -596,7 +614,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     struct BwdOps {
       double J6[6], h, a, b;
     };
-    // vec: s.u.q.h (solve) or s.u.q.gr (dual residual)
+    // vec: s.u.q.g, the right-hand side h (solve) or the gradient gr (dual residual)
     auto bwd_load = [&](int kk, const double (*vec)[9], BwdOps& o) {
 #pragma unroll
       for (int e = 0; e < 6; ++e) o.J6[e] = s.J[kk][e][scol];
@@ -642,16 +660,17 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       for (int e = 0; e < 6; ++e) acc += o.w[e] * xb[e];
       const double uk = acc + o.w[6] * xb[6] + o.w[7];  // lanes 7, 8: u_c = K_c xt + kk_c
       const double u0 = bcast(uk, 7), u1 = bcast(uk, 8);
-      if (l < 9) s.u.q.dv[kk][l] = fk ? uk : X;
+      if (l < 9) s.u.q.g[kk][l] = fk ? uk : X;
       const double xn = acc + o.w[6] * u0 + o.w[7] * u1;  // lanes 0..5
       return l < 6 ? xn : (l == 6 ? u0 : 0.0);
     };
 
-    // LQ solve with linear terms s.u.q.h -> direction s.u.q.dv (backward vector pass with the
-    // factor, then the forward rollout u = K xt + kk)
+    // LQ solve with linear terms h -> direction dv (backward vector pass with the factor, then
+    // the forward rollout u = K xt + kk); both live in s.u.q.g: the forward pass overwrites h
+    // once the backward pass is done with it
     auto lq_solve = [&]() {
       BwdOps A1, B1;
-      bwd_load(N - 1, s.u.q.h, A1);
+      bwd_load(N - 1, s.u.q.g, A1);
       double pv = 0.0;  // lanes 0..6: p_{k+1}
       auto bstage = [&](int kk, const BwdOps& o) {
         const double g = bwd_g(kk, o, pv);
@@ -663,10 +682,10 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
 #pragma unroll 1
       for (int kk = N - 1; kk >= 0; kk -= 2) {
         const int k1 = kk >= 1 ? kk - 1 : 0, k2 = kk >= 2 ? kk - 2 : 0;
-        bwd_load(k1, s.u.q.h, B1);
+        bwd_load(k1, s.u.q.g, B1);
         bstage(kk, A1);
         if (kk >= 1) {
-          bwd_load(k2, s.u.q.h, A1);
+          bwd_load(k2, s.u.q.g, A1);
           bstage(kk - 1, B1);
         }
       }
@@ -690,7 +709,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     // condensed dual residual max |d/du (sum_k gr_k . v_k)| through the dynamics (adjoint sweep)
     auto dual_residual = [&]() -> double {
       BwdOps A3, B3;
-      bwd_load(N - 1, s.u.q.gr, A3);
+      bwd_load(N - 1, s.u.q.g, A3);
       double rho = 0.0, rmax = 0.0;
       auto rstage = [&](int kk, const BwdOps& o) {
         const double g = bwd_g(kk, o, rho);
@@ -700,10 +719,10 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
 #pragma unroll 1
       for (int kk = N - 1; kk >= 0; kk -= 2) {
         const int k1 = kk >= 1 ? kk - 1 : 0, k2 = kk >= 2 ? kk - 2 : 0;
-        bwd_load(k1, s.u.q.gr, B3);
+        bwd_load(k1, s.u.q.g, B3);
         rstage(kk, A3);
         if (kk >= 1) {
-          bwd_load(k2, s.u.q.gr, A3);
+          bwd_load(k2, s.u.q.g, A3);
           rstage(kk - 1, B3);
         }
       }
@@ -717,10 +736,8 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     for (; it < A.qp.max_iter; ++it) {
       // (a) residuals, stage gradients, barrier-augmented stage Hessians
       ST_STAMP(t_r0)
-      double vk[9], rp[NR], wg[NR], grk[9], val[NR];
+      double rp[NR], wg[NR], grk[9], val[NR];
       double rpm = 0.0, mus = 0.0;
-#pragma unroll
-      for (int e = 0; e < 9; ++e) vk[e] = s.u.q.v[k][e];
       row_values(R, vk, val);
 #pragma unroll
       for (int i = 0; i < NR; ++i) {
@@ -740,7 +757,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       }
       if (stl) {
 #pragma unroll
-        for (int e = 0; e < 9; ++e) s.u.q.gr[k][e] = grk[e];
+        for (int e = 0; e < 9; ++e) s.u.q.g[k][e] = grk[e];
         double Qt[NQ];
 #pragma unroll
         for (int e = 0; e < NQ; ++e) Qt[e] = Qc[e];
@@ -795,7 +812,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
           for (int e = 0; e < 9; ++e) hk[e] = grk[e];
           row_adjoint(R, y, hk);
 #pragma unroll
-          for (int e = 0; e < 9; ++e) s.u.q.h[k][e] = hk[e];
+          for (int e = 0; e < 9; ++e) s.u.q.g[k][e] = hk[e];
         }
         WSYNC();
       };
@@ -809,7 +826,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       double dsa[NR], dla[NR], cdv[NR], dvk[9];
       double amin = 1.0;
 #pragma unroll
-      for (int e = 0; e < 9; ++e) dvk[e] = s.u.q.dv[k][e];
+      for (int e = 0; e < 9; ++e) dvk[e] = s.u.q.g[k][e];
       row_values(R, dvk, cdv);
 #pragma unroll
       for (int i = 0; i < NR; ++i) {
@@ -838,7 +855,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       ST_ACC(ST_SOLVE, t_q3)
       ST_STAMP(t_q4)
 #pragma unroll
-      for (int e = 0; e < 9; ++e) dvk[e] = s.u.q.dv[k][e];
+      for (int e = 0; e < 9; ++e) dvk[e] = s.u.q.g[k][e];
       row_values(R, dvk, cdv);
       amin = 1.0;
 #pragma unroll
@@ -857,7 +874,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
           }
         }
 #pragma unroll
-        for (int e = 0; e < 9; ++e) s.u.q.v[k][e] = vk[e] + alpha * dvk[e];
+        for (int e = 0; e < 9; ++e) vk[e] += alpha * dvk[e];
       }
       WSYNC();
       ST_ACC(ST_STEP, t_q4)
@@ -872,10 +889,12 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     // keeps a non-converged iterate (infeasible-start interior point) from leaving it
     if (stl) {
       const double uF = s.ub[k][0], uW = s.ub[k][1];
-      s.uo[k][0] = uF;
-      s.uo[k][1] = uW;
-      s.ub[k][0] = uF + s.u.q.v[k][7] * S;
-      s.ub[k][1] = fmin(fmax(uW + s.u.q.v[k][8], W.w_min), W.w_max);
+      s.u.q.g[k][0] = uF;
+      s.u.q.g[k][1] = uW;
+      s.u.q.g[k][2] = vk[7];
+      s.u.q.g[k][3] = vk[8];
+      s.ub[k][0] = uF + vk[7] * S;
+      s.ub[k][1] = fmin(fmax(uW + vk[8], W.w_min), W.w_max);
     }
     test = s.flag[2] != 0;  // from an iterate outside the domain: the full step, untested
     tries = 1;
