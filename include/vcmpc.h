@@ -58,7 +58,7 @@
 extern "C" {
 #endif
 
-#define VCMPC_ABI_VERSION 8
+#define VCMPC_ABI_VERSION 9
 #define VC_MAX_OBSTACLES 16
 
 typedef struct vc_ctx vc_ctx;
@@ -136,6 +136,11 @@ typedef struct vc_qp {
                        warm-start states xbar (read from vc_solve's xbar, x0 replacing its first
                        column) instead of the rollout of ubar; the defects enter as a linear
                        offset (oracle/ltv_qp.py kin_qp(..., x_ws=)) */
+  double elastic;   /* ABI 9, kinematic stagewise kernel: rho > 0 makes the v / delta state rows
+                       elastic -- row i gets a slack t_i >= 0 at cost rho t_i + 1e-8 t_i^2 (the QP
+                       model of kin_merit's L1 penalty), so every QP has a solution; the plain
+                       step whenever that is feasible with multipliers below rho
+                       (oracle/ltv_qp.py elastic_qp).  0 = hard rows */
 } vc_qp;
 
 /* Cascaded controller: single-track stages followed by a point-mass tail

@@ -37,8 +37,13 @@ def phase1(C, d, tol=1e-9, t_min=0.0):
     c = np.zeros(n + 1)
     c[-1] = 1.0
     bounds = [(None, None)] * n + [(t_min, None)]
-    res = linprog(c, A_ub=A, b_ub=ds_, bounds=bounds, method="highs",
-                  options=dict(primal_feasibility_tolerance=1e-10, dual_feasibility_tolerance=1e-10))
+    # tight HiGHS tolerances first; the simplex occasionally stops without a status at 1e-10
+    # ("Not Set"), then looser ones -- the returned point / Farkas vector is checked below either way
+    for tol_lp in (1e-10, 1e-9, None):
+        opts = {} if tol_lp is None else dict(primal_feasibility_tolerance=tol_lp, dual_feasibility_tolerance=tol_lp)
+        res = linprog(c, A_ub=A, b_ub=ds_, bounds=bounds, method="highs", options=opts)
+        if res.status == 0:
+            break
     if res.status != 0:
         raise RuntimeError(f"phase-1 LP: {res.message}")
     z, t = res.x[:n], float(res.x[-1])

@@ -172,35 +172,19 @@ def line_search_ms(x0, ubar, dz, x, dx, kappa, ds, L, W):
     return alpha, phi0, phia, D, reset
 
 
-def elastic_qp_step(x0, ubar, kappa, ds, L, W, rho=RHO, eps_t=1e-8, **qp_kw):
-    """The LTV-QP step with *elastic* state rows (v >= v_min, delta bounds): each row gets its own
-    slack t >= 0 with cost rho t (+ eps_t t^2 so the oracle's solver sees a definite Hessian), the
-    QP model of the merit's L1 penalty (Fletcher's Sl1QP).  Always feasible; equal to the plain
-    step whenever that is feasible with multipliers below rho.  Returns (u_star, kkt, t)."""
-    from .qp import solve_qp_batch
-    Qd = Q.kin_qp(x0, ubar, kappa, ds, L, W)
-    H, g, C, d = Qd["H"], Qd["g"], Qd["C"], Qd["d"]
-    B, n = g.shape
-    N = n // 2
-    ne = 3 * (N - 1)
-    nb = C.shape[1] - ne
-    H2 = np.zeros((B, n + ne, n + ne))
-    H2[:, :n, :n] = H
-    H2[:, n:, n:] = 2.0 * eps_t * np.eye(ne)
-    g2 = np.concatenate([g, np.full((B, ne), rho)], axis=1)
-    C2 = np.zeros((B, nb + 2 * ne, n + ne))
-    C2[:, :nb + ne, :n] = C
-    C2[:, nb:nb + ne, n:] = -np.eye(ne)
-    C2[:, nb + ne:, n:] = -np.eye(ne)
-    d2 = np.concatenate([d, np.zeros((B, ne))], axis=1)
-    sol = solve_qp_batch(H2, g2, C2, d2, **qp_kw)
-    dz = sol["z"][:, :n]
-    return np.asarray(ubar, np.float64) + dz.reshape(B, N, 2), sol["kkt"], sol["z"][:, n:]
+def elastic_qp_step(x0, ubar, kappa, ds, L, W, rho=RHO, **qp_kw):
+    """The single-shooting LTV-QP step with elastic state rows (ltv_qp.elastic_qp: v >= v_min
+    and the delta bounds get slacks t >= 0 at cost rho t + eps_t t^2, the QP model of the
+    merit's L1 penalty).  Returns (u_star, kkt, t)."""
+    sol = Q.kin_ltv_solve(x0, ubar, kappa, ds, L, W, elastic=rho, **qp_kw)
+    return sol["u_star"], sol["kkt"], sol["t"]
 
 
-def kin_sqp_solve(x0, ubar, kappa, ds, L, W, sqp_iters, x_ws=None, **qp_kw):
+def kin_sqp_solve(x0, ubar, kappa, ds, L, W, sqp_iters, x_ws=None, elastic=0.0, **qp_kw):
     """The globalised step: u_star[B,N,2], x_star[B,N+1,6] (x at u_star; under multiple
-    shooting, x_ws given, the state iterate), per-iteration (alpha, phi0, phi, D, QP certificates)."""
+    shooting, x_ws given, the state iterate), per-iteration (alpha, phi0, phi, D, QP certificates).
+    elastic = rho > 0 (vc_qp.elastic): every QP's state rows are elastic (ltv_qp.elastic_qp),
+    so every step has a QP solution; with rho = RHO the QP's L1 model is the merit's own."""
     u = np.array(ubar, np.float64, copy=True)
     x = None
     if x_ws is not None:
@@ -209,7 +193,7 @@ def kin_sqp_solve(x0, ubar, kappa, ds, L, W, sqp_iters, x_ws=None, **qp_kw):
         x[:, 1:, IS] = x0[:, None, IS] + np.cumsum(ds, axis=1)     # s' = 1 (kin_ric.hip)
     hist = []
     for _ in range(sqp_iters):
-        sol = Q.kin_ltv_solve(x0, u, kappa, ds, L, W, x_ws=x, **qp_kw)
+        sol = Q.kin_ltv_solve(x0, u, kappa, ds, L, W, x_ws=x, elastic=elastic, **qp_kw)
         dz = sol["u_star"] - u
         if x is None:
             alpha, phi0, phia, D = line_search(x0, u, dz, kappa, ds, L, W)

@@ -42,6 +42,7 @@ from . import obstacles as OB
 
 IV, ID, IS, IEY, IEP, IT = range(6)
 IA, IW = 0, 1
+ELASTIC_EPS_T = 1e-8   # elastic slacks' quadratic cost (elastic_qp; kin_ric.hip uses the same)
 
 
 def kin_weights(cfg: dict) -> dict:
@@ -183,14 +184,42 @@ def kin_qp(x0, ubar, kappa, ds, L, W, x_ws=None):
     return dict(xbar=xbar, e=eo, A=A, Bm=Bm, G=G, H=H, g=g, C=C, d=d)
 
 
-def kin_ltv_solve(x0, ubar, kappa, ds, L, W, x_ws=None, **qp_kw):
+def elastic_qp(H, g, C, d, ne, rho, eps_t=ELASTIC_EPS_T):
+    """The QP with its last `ne` rows made *elastic*: row i gets its own slack t_i >= 0,
+    C_i z - t_i <= d_i, at cost rho t_i + eps_t t_i^2 (the QP model of an exact L1 penalty,
+    Fletcher's Sl1QP; eps_t keeps the Hessian definite).  Always feasible; its z equals the plain
+    QP's whenever that is feasible with the elastic rows' multipliers below rho.  Returns
+    (H2, g2, C2, d2) over (z, t) -- csrc/kin_ric.hip's elastic rows (vc_qp.elastic = rho)."""
+    B, n = g.shape
+    m = C.shape[1]
+    nb = m - ne
+    H2 = np.zeros((B, n + ne, n + ne))
+    H2[:, :n, :n] = H
+    H2[:, n:, n:] = 2.0 * eps_t * np.eye(ne)
+    g2 = np.concatenate([g, np.full((B, ne), rho)], axis=1)
+    C2 = np.zeros((B, m + ne, n + ne))
+    C2[:, :m, :n] = C
+    C2[:, nb:m, n:] = -np.eye(ne)
+    C2[:, m:, n:] = -np.eye(ne)
+    d2 = np.concatenate([d, np.zeros((B, ne))], axis=1)
+    return H2, g2, C2, d2
+
+
+def kin_ltv_solve(x0, ubar, kappa, ds, L, W, x_ws=None, elastic=0.0, **qp_kw):
     """Steps 1-5 with the exact oracle QP solver.  Returns dict with u_star[B,N,2],
-    x_star[B,N+1,6], u0[B,2], dz, lam, kkt (certificate), plus the QP data."""
+    x_star[B,N+1,6], u0[B,2], dz, lam, kkt (certificate), plus the QP data.  elastic = rho > 0:
+    the v / delta state rows are elastic (elastic_qp; the slacks in `t`)."""
     from .qp import solve_qp_batch
 
     Q = kin_qp(x0, ubar, kappa, ds, L, W, x_ws=x_ws)
     B, N = np.asarray(ubar).shape[:2]
-    sol = solve_qp_batch(Q["H"], Q["g"], Q["C"], Q["d"], **qp_kw)
+    if elastic > 0.0:
+        n = 2 * N
+        sol = solve_qp_batch(*elastic_qp(Q["H"], Q["g"], Q["C"], Q["d"], 3 * (N - 1), elastic), **qp_kw)
+        sol["t"] = sol["z"][:, n:]
+        sol["z"] = sol["z"][:, :n]
+    else:
+        sol = solve_qp_batch(Q["H"], Q["g"], Q["C"], Q["d"], **qp_kw)
     dz = sol["z"]
     u_star = np.asarray(ubar, np.float64) + dz.reshape(B, N, 2)
     x_star = Q["xbar"] + Q["e"] + np.einsum("bkin,bn->bki", Q["G"], dz)

@@ -3,7 +3,7 @@
 libvcmpc_timing.so, diag[b][4 + slot]).  Prints cycles per problem (lane-0 clock of the
 problem's wavefront) and per interior-point iteration, at B problems of the C3 sampler.
 
-    VCMPC_LIB=vehicle-control_amd/vcmpc/libvcmpc_timing.so python scripts/st_section_timing.py [B] [N]
+    VCMPC_LIB=vehicle-control_amd/vcmpc/libvcmpc_timing.so python scripts/st_section_timing.py [B] [N] [tyre]
 """
 import os
 import sys
@@ -21,16 +21,17 @@ SLOTS = ["predict", "linearize", "setup", "residuals", "dual residual", "riccati
          "rhs + steps", "total"]
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 40
+TYRE = sys.argv[3] if len(sys.argv) > 3 else "linear"
 cfg = load_config("dynamic_mpc" if N == 40 else "singletrack_mpc")
-d = {k: v.astype(np.float64) for k, v in dynamic_batch(B, N=N, seed=3).items()}
-p = make_params(dyn_car=load_config("dynamic_car"), dyn_mpc=cfg, tyre="linear")
+d = {k: v.astype(np.float64) for k, v in dynamic_batch(B, N=N, seed=3, tyre=TYRE).items()}
+p = make_params(dyn_car=load_config("dynamic_car"), dyn_mpc=cfg, tyre=TYRE)
 with Context(model=_abi.VC_MODEL_DYNAMIC, N=N, max_batch=B, dtype=_abi.VC_F64, params=p) as ctx:
     diag = np.zeros((B, 4 + len(SLOTS)))
     u0, xs, us, st, it, dg = ctx.solve(d["x0"], d["kappa"], d["ds"], d["ubar"].copy(), diag=diag)
 cyc = dg[:, 4:]
 tot = cyc[:, -1].mean()
 iters = it.mean()
-print(f"B={B} N={N}: solved {(st == 0).mean():.4f}, IPM iterations per problem {iters:.1f} (max {it.max()})")
+print(f"B={B} N={N} {TYRE}: solved {(st == 0).mean():.4f}, IPM iterations per problem {iters:.1f} (max {it.max()})")
 print(f"{'section':<18}{'cycles/problem':>16}{'share':>9}{'per IPM iter':>14}")
 for i, name in enumerate(SLOTS):
     c = cyc[:, i].mean()

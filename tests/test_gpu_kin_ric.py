@@ -221,3 +221,36 @@ def test_kin_ric_multiple_shooting_vs_oracle(N):
     assert (r[3] == 0).all() and (rc[3] == 0).all()
     assert err < 1e-5 and err_c < 1e-5
     assert np.abs(r[1] - ref["x_star"]).max() < 1e-6
+
+
+@pytest.mark.parametrize("N", [20, 50])
+def test_kin_ric_elastic_rows_vs_oracle(N):
+    """vc_qp.elastic = rho: the v / delta rows get slacks t >= 0 at cost rho t + 1e-8 t^2
+    (oracle/ltv_qp.py elastic_qp, the QP of the kinematic obstacle SQP).  Problems: the C2
+    sampler with the delta box tightened to +-0.05 rad and the closed loop's trust region
+    (1.0 / 0.1), so most QPs have no feasible point with hard rows (phase-1 LP certificates,
+    oracle/feasibility.py) and every elastic QP has a solution.  Bar: solved, u* within the
+    north star's 1e-5 of the oracle's elastic optimum."""
+    from oracle.feasibility import phase1
+    from vcmpc import Context, _abi
+    from vcmpc.config import load_config, make_params
+    from vcmpc.workload import kinematic_batch
+    cfg = load_config("kinematic_mpc")
+    cfg["qp"] = dict(cfg.get("qp") or {}, solver=1, trust_a=1.0, trust_w=0.1, elastic=1e3)
+    cfg["state_constraints"] = dict(cfg["state_constraints"], delta_max=0.05, delta_min=-0.05)
+    W = Q.kin_weights(cfg)
+    d = kinematic_batch(48, N=N, seed=77)
+    Qd = Q.kin_qp(d["x0"], d["ubar"], d["kappa"], d["ds"], L, W)
+    infeasible = sum(not phase1(Qd["C"][b], Qd["d"][b])["feasible"] for b in range(len(d["x0"])))
+    ref = Q.kin_ltv_solve(d["x0"], d["ubar"], d["kappa"], d["ds"], L, W, elastic=1e3)
+    assert ref["polished"].all() and ref["kkt"]["pfeas"].max() < 1e-9
+    p = make_params(kin_car=load_config("kinematic_car"), kin_mpc=cfg)
+    with Context(model=_abi.VC_MODEL_KINEMATIC, N=N, max_batch=48, dtype=_abi.VC_F64, params=p) as c:
+        u0, xs, us, st, it, dg = c.solve(d["x0"], d["kappa"], d["ds"], d["ubar"].copy(), diag=True)
+    err = np.abs(us - ref["u_star"]).max(axis=(1, 2))
+    print(f"N={N}: {infeasible} of {len(err)} hard-row QPs infeasible; elastic |u* - u*_oracle| max "
+          f"{err.max():.2e}, t max {ref['t'].max():.3f}, iterations {it.min()}..{it.max()}, "
+          f"polished {(dg[:, 2].astype(int) & 4 > 0).mean():.2f}")
+    assert infeasible >= len(err) // 2
+    assert (st == 0).all(), (st, dg[st != 0])
+    assert err.max() < U_TOL, err

@@ -45,6 +45,7 @@ constexpr double RHO_AL = 1e4;     // augmented-Lagrangian weight of the polish
 constexpr int AL_PASSES = 16;
 constexpr double MU_POLISH = 1e-7;  // complementarity at which the polish is first tried
 constexpr double TOL_CERT = 1e-9;   // feasibility / multiplier sign tolerance of the certificate
+constexpr double EPS_T = 1e-8;      // elastic slacks' quadratic cost (oracle/ltv_qp.py ELASTIC_EPS_T)
 
 // Row i: sign * v[var] <= d:  da <=, -da <=, dw <=, -dw <=, -dv <=, ddelta <=, -ddelta <=
 __host__ __device__ constexpr int row_var(int i) { return i < 2 ? 5 : (i < 4 ? 6 : (i == 4 ? 0 : 1)); }
@@ -321,9 +322,24 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
     sl[i] = m[i] > 0.0 ? fmax(d[i], 1.0) : 1.0;
     la[i] = m[i];
   }
+  // elastic state rows (vc_qp.elastic = rho > 0): the slack t >= 0 of row 4 + j and its
+  // multiplier le; me = 1 where the row is present and elastic
+  const double rho_el = A.qp.elastic;
+  double me[3], te[3], le[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    me[j] = rho_el > 0.0 ? m[4 + j] : 0.0;
+    // start on the t-stationarity (la + le = rho): from le = 1 the multipliers have to grow
+    // three decades through the fraction to the boundary (45 iterations instead of 18 in the
+    // dense restatement of this elimination)
+    te[j] = 1.0;
+    le[j] = me[j] * fmax(rho_el - 1.0, 0.5 * rho_el);
+  }
   double mc = 0.0;
 #pragma unroll
   for (int i = 0; i < NRW; ++i) mc += m[i];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) mc += me[j];
   const double mcount = fmax(wsum(mc), 1.0);
   if (stl) {
 #pragma unroll
@@ -554,13 +570,20 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
   };
 
   // ---------------- active-set polish ----------------
-  // true when certified; the polished stage vectors are then in s.v
+  // true when certified; the polished stage vectors are then in s.v.  Elastic rows (el) have a
+  // third state besides active / inactive: violated at the penalty, t = sgn v - d > 0 at cost
+  // rho t + EPS_T t^2 (a stage-local quadratic in v, no multiplier to find).
   int rounds_used = 0;
   bool pol_fact_fail = false;
   auto polish = [&]() -> bool {
-    bool act[NRW];
+    bool act[NRW], elr[3];
 #pragma unroll
     for (int i = 0; i < NRW; ++i) act[i] = m[i] > 0.0 && la[i] > sl[i];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      elr[j] = me[j] > 0.0 && te[j] > le[j];
+      act[4 + j] = act[4 + j] && !elr[j];
+    }
 #pragma unroll 1
     for (int r = 0; r < A.qp.polish; ++r) {
       ++rounds_used;
@@ -570,6 +593,8 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
         for (int e = 0; e < NQK; ++e) Qt[e] = Qc[e];
 #pragma unroll
         for (int i = 0; i < NRW; ++i) Qt[D0 + row_var(i)] += act[i] ? RHO_AL : 0.0;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) Qt[D0 + row_var(4 + j)] += elr[j] ? 2.0 * EPS_T : 0.0;
 #pragma unroll
         for (int e = 0; e < NQK; ++e) s.Qt[k][e] = Qt[e];
       }
@@ -584,13 +609,16 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
       for (int i = 0; i < NRW; ++i) lm[i] = act[i] ? la[i] : 0.0;
 #pragma unroll 1
       for (int p = 0; p < AL_PASSES; ++p) {
-        // min 1/2 v'Qv + q'v + lm'(C_A v - d_A) + rho/2 |C_A v - d_A|^2
+        // min 1/2 v'Qv + q'v + lm'(C_A v - d_A) + rho/2 |C_A v - d_A|^2 (+ the elastic rows' penalty)
         if (stl) {
           double hk[NV];
 #pragma unroll
           for (int e = 0; e < NV; ++e) hk[e] = qc[e];
 #pragma unroll
           for (int i = 0; i < NRW; ++i) hk[row_var(i)] += act[i] ? row_sgn(i) * (lm[i] - RHO_AL * d[i]) : 0.0;
+#pragma unroll
+          for (int j = 0; j < 3; ++j)
+            hk[row_var(4 + j)] += elr[j] ? row_sgn(4 + j) * (rho_el - 2.0 * EPS_T * d[4 + j]) : 0.0;
 #pragma unroll
           for (int e = 0; e < NV; ++e) s.h[k][e] = hk[e];
         }
@@ -607,17 +635,24 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
         al_conv = wmax(stl ? dmax : 0.0) <= 1e-13 * (1.0 + qmax);
         if (al_conv) break;
       }
-      // certificate: inactive rows feasible, multipliers of the active ones >= 0
-      bool bad_v = false, bad_n = false;
-      bool viol[NRW], neg[NRW];
+      // certificate: inactive rows feasible, multipliers of the active ones >= 0 (and <= rho on
+      // elastic rows), elastic rows violated
+      bool bad = false;
+      bool viol[NRW], neg[NRW], over[3], under[3];
 #pragma unroll
       for (int i = 0; i < NRW; ++i) {
-        viol[i] = stl && m[i] > 0.0 && !act[i] && cv[i] - d[i] > TOL_CERT * (1.0 + fabs(d[i]));
+        const bool free_row = i < 4 || !elr[i >= 4 ? i - 4 : 0];
+        viol[i] = stl && m[i] > 0.0 && !act[i] && free_row && cv[i] - d[i] > TOL_CERT * (1.0 + fabs(d[i]));
         neg[i] = stl && act[i] && lm[i] < -TOL_CERT * (1.0 + qmax);
-        bad_v = bad_v || viol[i];
-        bad_n = bad_n || neg[i];
+        bad = bad || viol[i] || neg[i];
       }
-      const bool good = al_conv && __all((bad_v || bad_n) ? 0 : 1) != 0;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        over[j] = stl && me[j] > 0.0 && act[4 + j] && lm[4 + j] > rho_el + TOL_CERT * (1.0 + qmax);
+        under[j] = stl && elr[j] && cv[4 + j] - d[4 + j] < -TOL_CERT * (1.0 + fabs(d[4 + j]));
+        bad = bad || over[j] || under[j];
+      }
+      const bool good = al_conv && __all(bad ? 0 : 1) != 0;
       if (good) {
         if (stl) {
 #pragma unroll
@@ -628,11 +663,23 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
       }
 #pragma unroll
       for (int i = 0; i < NRW; ++i) act[i] = (act[i] || viol[i]) && !neg[i];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        act[4 + j] = (act[4 + j] || under[j]) && !over[j];
+        elr[j] = (elr[j] || over[j]) && !under[j];
+      }
     }
     return false;
   };
 
   // ---------------- interior point (Mehrotra predictor-corrector) ----------------
+  // Elastic row i = 4 + j (el): sgn v - t + s = d, t >= 0, cost rho t + EPS_T t^2, multipliers
+  // la (row) and le (t >= 0).  The slack t is eliminated stage-locally: with w1 = la / s,
+  // w2 = le / t, D = 2 EPS_T + w1 + w2 the row enters the Newton system like a hard row with
+  // weight weff = w1 (2 EPS_T + w2) / D and the complementarity term
+  //   rco = (rc1 / s) (2 EPS_T + w2) / D - (w1 / D) (rc2 / t + rt),   rt = rho + 2 EPS_T t - la - le,
+  // and after the solve  dt = (w1 (C dv + rp) - rc1 / s - rc2 / t - rt) / D,  ds = -rp - C dv + dt,
+  // dla = weff (C dv + rp) - rco,  dle = -rc2 / t - w2 dt.
   const double tol_r = A.qp.tol * (1.0 + qmax), tol_mu = 1e-13;
   int it = 0;
   bool conv = false, fail = false, polished = false, tried_polish = false;
@@ -641,17 +688,30 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
 #pragma unroll 1
   for (; finite_pred && it < A.qp.max_iter; ++it) {
     // (a) residuals, stage gradients, barrier-augmented stage Hessians
-    double vk[NV], rp[NRW], wg[NRW], grk[NV];
+    double vk[NV], rp[NRW], wg[NRW], grk[NV], rt[3], fE[3], gE[3], ieD[3], w2[3];
     double rpm = 0.0, mus = 0.0;
 #pragma unroll
     for (int e = 0; e < NV; ++e) vk[e] = s.v[k][e];
 #pragma unroll
     for (int i = 0; i < NRW; ++i) {
-      rp[i] = m[i] * (row_sgn(i) * vk[row_var(i)] + sl[i] - d[i]);
+      rp[i] = m[i] * (row_sgn(i) * vk[row_var(i)] + sl[i] - d[i]) - (i >= 4 ? me[i - 4] * te[i - 4] : 0.0);
       wg[i] = m[i] * la[i] / sl[i];
       rpm = fmax(rpm, fabs(rp[i]));
       mus += m[i] * sl[i] * la[i];
     }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      rt[j] = me[j] * (rho_el + 2.0 * EPS_T * te[j] - la[4 + j] - le[j]);
+      rpm = fmax(rpm, fabs(rt[j]));
+      mus += me[j] * te[j] * le[j];
+      w2[j] = me[j] * le[j] / te[j];
+      ieD[j] = me[j] / (2.0 * EPS_T + wg[4 + j] + w2[j]);
+      fE[j] = me[j] > 0.0 ? (2.0 * EPS_T + w2[j]) * ieD[j] : 1.0;
+      gE[j] = wg[4 + j] * ieD[j];
+    }
+    double wgE[NRW];  // the rows' weights in the Newton system (effective on elastic rows)
+#pragma unroll
+    for (int i = 0; i < NRW; ++i) wgE[i] = i < 4 ? wg[i] : wg[i] * fE[i - 4];
     qmul(Qc, vk, grk);
 #pragma unroll
     for (int e = 0; e < NV; ++e) grk[e] += qc[e];
@@ -664,7 +724,7 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
 #pragma unroll
       for (int e = 0; e < NQK; ++e) Qt[e] = Qc[e];
 #pragma unroll
-      for (int i = 0; i < NRW; ++i) Qt[D0 + row_var(i)] += wg[i];
+      for (int i = 0; i < NRW; ++i) Qt[D0 + row_var(i)] += wgE[i];
 #pragma unroll
       for (int e = 0; e < NQK; ++e) s.Qt[k][e] = Qt[e];
     } else {
@@ -693,7 +753,7 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
 #pragma unroll
       for (int e = 0; e < NQK; ++e) Qt[e] = Qc[e];
 #pragma unroll
-      for (int i = 0; i < NRW; ++i) Qt[D0 + row_var(i)] += wg[i];
+      for (int i = 0; i < NRW; ++i) Qt[D0 + row_var(i)] += wgE[i];
 #pragma unroll
       for (int e = 0; e < NQK; ++e) s.Qt[k][e] = Qt[e];
     }
@@ -709,30 +769,43 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
       break;
     }
 
-    // (c) predictor: h = gr + C'(W rp - lam)
+    // (c) predictor: h = gr + C'(W rp - rco), rco = lam on hard rows (rc = s lam)
     auto set_h = [&](const double* rc_over_s) {
       if (stl) {
         double hk[NV];
 #pragma unroll
         for (int e = 0; e < NV; ++e) hk[e] = grk[e];
 #pragma unroll
-        for (int i = 0; i < NRW; ++i) hk[row_var(i)] += row_sgn(i) * m[i] * (wg[i] * rp[i] - rc_over_s[i]);
+        for (int i = 0; i < NRW; ++i) hk[row_var(i)] += row_sgn(i) * m[i] * (wgE[i] * rp[i] - rc_over_s[i]);
 #pragma unroll
         for (int e = 0; e < NV; ++e) s.h[k][e] = hk[e];
       }
       WSYNC();
     };
-    set_h(la);
+    double rco[NRW], rc2t[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) rc2t[j] = me[j] * le[j];  // rc2 / t with rc2 = t le
+#pragma unroll
+    for (int i = 0; i < NRW; ++i) rco[i] = i < 4 ? la[i] : la[i] * fE[i - 4] - gE[i - 4] * (rc2t[i - 4] + rt[i - 4]);
+    set_h(rco);
     lq_solve();
-    double dsa[NRW], dla[NRW], cdv[NRW], dvk[NV];
+    double dsa[NRW], dla[NRW], cdv[NRW], dvk[NV], dta[3], dlea[3];
     double amin = 1.0;
 #pragma unroll
     for (int e = 0; e < NV; ++e) dvk[e] = s.dv[k][e];
 #pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int i = 4 + j;
+      const double c = row_sgn(i) * dvk[row_var(i)];
+      dta[j] = ieD[j] * (wg[i] * (c + rp[i]) - la[i] - rc2t[j] - rt[j]);
+      dlea[j] = me[j] * (-rc2t[j] - w2[j] * dta[j]);
+      if (stl && me[j] > 0.0) amin = fmin(amin, fmin(step_to_bound(te[j], dta[j]), step_to_bound(le[j], dlea[j])));
+    }
+#pragma unroll
     for (int i = 0; i < NRW; ++i) {
       cdv[i] = row_sgn(i) * dvk[row_var(i)];
-      dsa[i] = m[i] * (-rp[i] - cdv[i]);
-      dla[i] = m[i] * (wg[i] * (cdv[i] + rp[i]) - la[i]);
+      dsa[i] = m[i] * (-rp[i] - cdv[i]) + (i >= 4 ? dta[i - 4] : 0.0);
+      dla[i] = m[i] * (wgE[i] * (cdv[i] + rp[i]) - rco[i]);
       if (stl && m[i] > 0.0) amin = fmin(amin, fmin(step_to_bound(sl[i], dsa[i]), step_to_bound(la[i], dla[i])));
     }
     amin = wmin(amin);
@@ -740,25 +813,39 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
     if (stl) {
 #pragma unroll
       for (int i = 0; i < NRW; ++i) mua += m[i] * (sl[i] + amin * dsa[i]) * (la[i] + amin * dla[i]);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) mua += me[j] * (te[j] + amin * dta[j]) * (le[j] + amin * dlea[j]);
     }
     mua = wsum(mua) / mcount;
     const double ratio = mu > 0.0 ? fmin(1.0, mua / mu) : 0.0;
     const double smu = ratio * ratio * ratio * mu;
 
-    // (d) corrector: rc = s lam + ds_a dl_a - sigma mu
+    // (d) corrector: rc = s lam + ds_a dl_a - sigma mu (and t le + dt_a dle_a - sigma mu)
     double rcs[NRW];
 #pragma unroll
     for (int i = 0; i < NRW; ++i) rcs[i] = m[i] * (sl[i] * la[i] + dsa[i] * dla[i] - smu) / sl[i];
-    set_h(rcs);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) rc2t[j] = me[j] * (te[j] * le[j] + dta[j] * dlea[j] - smu) / te[j];
+#pragma unroll
+    for (int i = 0; i < NRW; ++i) rco[i] = i < 4 ? rcs[i] : rcs[i] * fE[i - 4] - gE[i - 4] * (rc2t[i - 4] + rt[i - 4]);
+    set_h(rco);
     lq_solve();
 #pragma unroll
     for (int e = 0; e < NV; ++e) dvk[e] = s.dv[k][e];
     amin = 1.0;
 #pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int i = 4 + j;
+      const double c = row_sgn(i) * dvk[row_var(i)];
+      dta[j] = ieD[j] * (wg[i] * (c + rp[i]) - rcs[i] - rc2t[j] - rt[j]);
+      dlea[j] = me[j] * (-rc2t[j] - w2[j] * dta[j]);
+      if (stl && me[j] > 0.0) amin = fmin(amin, fmin(step_to_bound(te[j], dta[j]), step_to_bound(le[j], dlea[j])));
+    }
+#pragma unroll
     for (int i = 0; i < NRW; ++i) {
       cdv[i] = row_sgn(i) * dvk[row_var(i)];
-      dsa[i] = m[i] * (-rp[i] - cdv[i]);
-      dla[i] = m[i] * (wg[i] * (cdv[i] + rp[i]) - rcs[i]);
+      dsa[i] = m[i] * (-rp[i] - cdv[i]) + (i >= 4 ? dta[i - 4] : 0.0);
+      dla[i] = m[i] * (wgE[i] * (cdv[i] + rp[i]) - rco[i]);
       if (stl && m[i] > 0.0) amin = fmin(amin, fmin(step_to_bound(sl[i], dsa[i]), step_to_bound(la[i], dla[i])));
     }
     const double alpha = fmin(1.0, 0.99 * wmin(amin));
@@ -768,6 +855,13 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
         if (m[i] > 0.0) {
           sl[i] = fmax(sl[i] + alpha * dsa[i], 1e-300);
           la[i] = fmax(la[i] + alpha * dla[i], 1e-300);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        if (me[j] > 0.0) {
+          te[j] = fmax(te[j] + alpha * dta[j], 1e-300);
+          le[j] = fmax(le[j] + alpha * dlea[j], 1e-300);
         }
       }
 #pragma unroll

@@ -12,7 +12,7 @@ import os
 
 LIB_NAME = "libvcmpc.so"
 LIB_PATH = os.environ.get("VCMPC_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME))
-ABI_VERSION = 8
+ABI_VERSION = 9
 VC_MAX_OBSTACLES = 16
 OBS_MARGIN_MIN = 0.05  # VC_OBS_MARGIN_MIN (csrc/vc_kernels.hpp)
 
@@ -54,7 +54,7 @@ class vc_dyn_mpc(C.Structure):
 class vc_qp(C.Structure):
     _fields_ = [("prox", C.c_double), ("tol", C.c_double), ("trust_a", C.c_double), ("trust_w", C.c_double),
                 ("max_iter", C.c_int32), ("polish", C.c_int32), ("solver", C.c_int32), ("kin_sqp", C.c_int32),
-                ("shift", C.c_int32), ("ms", C.c_int32)]
+                ("shift", C.c_int32), ("ms", C.c_int32), ("elastic", C.c_double)]
 
 
 class vc_obstacles(C.Structure):

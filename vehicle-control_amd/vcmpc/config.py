@@ -16,10 +16,11 @@ CONFIG_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file
 
 # The build's LTV-QP contract defaults (no reference counterpart).
 QP_DEFAULTS = {"prox": 1e-4, "tol": 1e-10, "max_iter": 40, "polish": 10, "trust_a": 0.0, "trust_w": 0.0,
-               "solver": 0, "kin_sqp": 0, "shift": 0, "ms": 0}
+               "solver": 0, "kin_sqp": 0, "shift": 0, "ms": 0, "elastic": 0.0}
 # The dynamic SQP contract defaults (config/dynamic_mpc.yaml `qp` block).
 DYN_QP_DEFAULTS = {"prox": 0.1, "tol": 1e-5, "max_iter": 60, "polish": 3, "trust_a": 0.0, "trust_w": 0.2,
-                   "fx_scale": 1000.0, "trust_Fx": 2000.0, "sqp_iters": 3, "solver": 0, "kin_sqp": 0, "shift": 0, "ms": 0}
+                   "fx_scale": 1000.0, "trust_Fx": 2000.0, "sqp_iters": 3, "solver": 0, "kin_sqp": 0, "shift": 0, "ms": 0,
+                   "elastic": 0.0}
 
 
 class AttrDict(dict):
@@ -102,7 +103,7 @@ def qp_struct(cfg=None, defaults=None) -> _abi.vc_qp:
     return _abi.vc_qp(prox=float(q["prox"]), tol=float(q["tol"]), trust_a=float(q["trust_a"]),
                       trust_w=float(q["trust_w"]), max_iter=int(q["max_iter"]), polish=int(q["polish"]),
                       solver=int(q["solver"]), kin_sqp=int(q.get("kin_sqp", 0)), shift=int(q.get("shift", 0)),
-                      ms=int(q.get("ms", 0)))
+                      ms=int(q.get("ms", 0)), elastic=float(q.get("elastic", 0.0)))
 
 
 def dyn_car_struct(cfg, tyre: str = "fiala") -> _abi.vc_dyn_car:
