@@ -140,7 +140,10 @@ typedef struct vc_qp {
                        elastic -- row i gets a slack t_i >= 0 at cost rho t_i + 1e-8 t_i^2 (the QP
                        model of kin_merit's L1 penalty), so every QP has a solution; the plain
                        step whenever that is feasible with multipliers below rho
-                       (oracle/ltv_qp.py elastic_qp).  0 = hard rows */
+                       (oracle/ltv_qp.py elastic_qp).  -rho < 0 (kin_sqp > 0): elastic on failure
+                       -- every QP is solved with hard rows and only the ones that solve leaves
+                       non-solved are solved again with elastic rows at rho (SNOPT's elastic mode).
+                       0 = hard rows */
 } vc_qp;
 
 /* Cascaded controller: single-track stages followed by a point-mass tail

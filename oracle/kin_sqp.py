@@ -184,7 +184,9 @@ def kin_sqp_solve(x0, ubar, kappa, ds, L, W, sqp_iters, x_ws=None, elastic=0.0, 
     """The globalised step: u_star[B,N,2], x_star[B,N+1,6] (x at u_star; under multiple
     shooting, x_ws given, the state iterate), per-iteration (alpha, phi0, phi, D, QP certificates).
     elastic = rho > 0 (vc_qp.elastic): every QP's state rows are elastic (ltv_qp.elastic_qp),
-    so every step has a QP solution; with rho = RHO the QP's L1 model is the merit's own."""
+    so every step has a QP solution; with rho = RHO the QP's L1 model is the merit's own.
+    elastic = -rho < 0: elastic on failure -- the hard-row QP, and where that has no certified
+    solution (infeasible: the interior point diverges, the polish fails) the elastic one."""
     u = np.array(ubar, np.float64, copy=True)
     x = None
     if x_ws is not None:
@@ -192,15 +194,30 @@ def kin_sqp_solve(x0, ubar, kappa, ds, L, W, sqp_iters, x_ws=None, elastic=0.0, 
         x[:, 0] = x0
         x[:, 1:, IS] = x0[:, None, IS] + np.cumsum(ds, axis=1)     # s' = 1 (kin_ric.hip)
     hist = []
-    for _ in range(sqp_iters):
-        sol = Q.kin_ltv_solve(x0, u, kappa, ds, L, W, x_ws=x, elastic=elastic, **qp_kw)
+    for it in range(sqp_iters):
+        sol = Q.kin_ltv_solve(x0, u, kappa, ds, L, W, x_ws=x, elastic=max(elastic, 0.0), **qp_kw)
+        if elastic < 0.0:
+            bad = ~sol["polished"] | sol["diverged"]
+            if bad.any():
+                xs = None if x is None else x[bad]
+                se = Q.kin_ltv_solve(x0[bad], u[bad], np.asarray(kappa)[bad], np.asarray(ds)[bad], L, W,
+                                     x_ws=xs, elastic=-elastic, **qp_kw)
+                for key in ("u_star", "x_star", "polished"):
+                    sol[key][bad] = se[key]
+                for key in sol["kkt"]:
+                    sol["kkt"][key][bad] = se["kkt"][key]
+            sol["elastic_retry"] = bad
         dz = sol["u_star"] - u
         if x is None:
             alpha, phi0, phia, D = line_search(x0, u, dz, kappa, ds, L, W)
         else:
             dx = sol["x_star"] - x
             alpha, phi0, phia, D, reset = line_search_ms(x0, u, dz, x, dx, kappa, ds, L, W)
-        hist.append(dict(alpha=alpha, phi0=phi0, phi=phia, D=D, kkt=sol["kkt"], polished=sol["polished"]))
+        # a QP without a certified solution refuses its step (kin_merit.hip qp_ok)
+        ok = sol["polished"] | (sol["converged"] & ~sol["diverged"])
+        alpha = np.where(ok, alpha, 0.0)
+        hist.append(dict(alpha=alpha, phi0=phi0, phi=phia, D=D, kkt=sol["kkt"], polished=sol["polished"],
+                         elastic_retry=sol.get("elastic_retry", np.zeros(len(alpha), bool)), qp_ok=ok))
         # a refused step (alpha = 0) keeps the iterate as it is: u + 0 * dz would carry a failed
         # QP's non-finite output into it (kin_merit.hip step_to)
         acc = (alpha > 0.0)[:, None, None]
@@ -210,5 +227,12 @@ def kin_sqp_solve(x0, ubar, kappa, ds, L, W, sqp_iters, x_ws=None, elastic=0.0, 
             x[reset] = Q.kin_predict(np.asarray(x0, np.float64)[reset], u[reset], np.asarray(kappa)[reset],
                                      np.asarray(ds)[reset], L)
             hist[-1]["reset"] = reset
+        # a first QP without a solution restarts the iterate from the neutral guess (u = 0, the
+        # state iterate x0 at every stage); the next QP's status is then the step's (kin_merit.hip)
+        if it == 0 and sqp_iters > 1 and not ok.all():
+            u[~ok] = 0.0
+            if x is not None:
+                x[~ok] = np.asarray(x0, np.float64)[~ok, None, :]
+            hist[-1]["restart"] = ~ok
     x_star = Q.kin_predict(np.asarray(x0, np.float64), u, kappa, ds, L) if x is None else x
     return dict(u_star=u, x_star=x_star, u0=u[:, 0].copy(), hist=hist)

@@ -20,7 +20,7 @@ run() {  # run <log> <timeout> cmd...
   return 0
 }
 cd "$ROOT"
-run pytest_gpu_$TAG.log 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+run pytest_gpu_$TAG.log 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread
 run smoke_$TAG.log 300 python -c "import __graft_entry__ as g; g.smoke()"
 run bench_$TAG.log 600 python bench.py --steps "$STEPS" --warmup 3
 cd /tmp

@@ -171,3 +171,39 @@ def test_kin_sqp_later_qp_failure_keeps_iterate(golden, ms):
     assert np.array_equal(xs[bad], xsr[bad]) or np.abs(xs[bad] - roll).max() < 1e-9
     np.testing.assert_array_equal(u0[bad], u0r[bad])
     assert (st == 0).all(), st
+
+
+@pytest.mark.parametrize("N", [20, 50])
+def test_kin_sqp_elastic_on_failure_vs_oracle(N):
+    """vc_qp.elastic = -rho (the obstacle controller's setting): the SQP iteration solves the
+    hard-row QP and re-solves the ones it leaves non-solved with elastic rows.  Problems: the C2
+    sampler with the delta box tightened to +-0.05 rad and the closed loop's trust region, so
+    most first QPs are infeasible with hard rows.  Before, those steps were non-solved; now every
+    step is solved.  One SQP iteration, so the kernel's retry decision is its hard pass's status:
+    it must agree with oracle/kin_sqp.py's (a diverged or unpolished hard interior point) and
+    u* must match the oracle's elastic-on-failure step to 1e-5."""
+    from vcmpc import Context, _abi
+    from vcmpc.config import load_config, make_params
+    from vcmpc.workload import kinematic_batch
+    S = 1
+    cfg = _cfg(S, solver=1, N=N)
+    cfg["qp"] = dict(cfg["qp"], trust_a=1.0, trust_w=0.1, elastic=-1e3, max_iter=80)
+    cfg["state_constraints"] = dict(cfg["state_constraints"], delta_max=0.05, delta_min=-0.05)
+    W = Q.kin_weights(cfg)
+    d = kinematic_batch(32, N=N, seed=91)
+    ref = KS.kin_sqp_solve(d["x0"], d["ubar"], d["kappa"], d["ds"], 2.5, W, S, elastic=-1e3)
+    p = make_params(kin_car=load_config("kinematic_car"), kin_mpc=cfg)
+    with Context(model=_abi.VC_MODEL_KINEMATIC, N=N, max_batch=32, dtype=_abi.VC_F64, params=p) as c:
+        u0, xs, us, st, it = c.solve(d["x0"], d["kappa"], d["ds"], d["ubar"].copy())
+    cfg_h = dict(cfg, qp=dict(cfg["qp"], elastic=0.0))
+    with Context(model=_abi.VC_MODEL_KINEMATIC, N=N, max_batch=32, dtype=_abi.VC_F64,
+                 params=make_params(kin_car=load_config("kinematic_car"), kin_mpc=cfg_h)) as c:
+        st_hard = c.solve(d["x0"], d["kappa"], d["ds"], d["ubar"].copy())[3]
+    retried = ref["hist"][0]["elastic_retry"]
+    err = np.abs(us - ref["u_star"]).max(axis=(1, 2))
+    print(f"N={N}: hard rows non-solved {int((st_hard != 0).sum())} of {len(st)} (oracle {int(retried.sum())}); "
+          f"elastic on failure non-solved {int((st != 0).sum())}; |u* - u*_oracle| max {err.max():.2e}")
+    assert (st_hard != 0).sum() >= len(st) // 2
+    np.testing.assert_array_equal(st_hard != 0, retried)
+    assert (st == 0).all(), st
+    assert err.max() < U_TOL, err

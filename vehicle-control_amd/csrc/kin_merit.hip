@@ -13,7 +13,8 @@
 // sufficient decrease (none, or a failed QP: alpha = 0), then the wavefront writes the
 // accepted inputs, lane 0 their rollout x* and u0, and the solve status / iteration count
 // accumulate over the SQP iterations (status: the first QP's -- a later QP's failure only
-// refuses its step; iterations: summed).
+// refuses its step; iterations: summed).  A first QP without a solution restarts the iterate
+// from the neutral guess, and the next QP's status becomes the step's (kin_sqp > 1).
 // With multiple shooting (vc_qp.ms) the iterate is the pair (x, u): the candidates are
 // (x_prev, u_prev) + alpha (x* - x_prev, u* - u_prev), the terms are evaluated on the state
 // candidate instead of a rollout (s = s0 + sum ds, s' = 1), plus RHO_DEF |F(x_n, u_n) - x_{n+1}|_1
@@ -34,6 +35,7 @@ constexpr double EPS_FD = 1e-7;  // directional-derivative step
 constexpr double RHO = 1e3;      // L1 penalty on the state rows
 constexpr double RHO_DEF = 1e3;  // L1 penalty on the multiple-shooting defects
 constexpr double TIE = 1e-9;     // the rollout wins unless the state iterate's merit is lower by more
+constexpr int32_t RESTART_PENDING = -1;  // st_acc: the iterate restarted, the next QP's status is the step's
 
 __device__ __forceinline__ double bcast(double v, int l) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
@@ -131,6 +133,11 @@ __global__ __launch_bounds__(64) void kin_merit_kernel(KinMeritArgs A) {
   const double phi0 = roll ? ps0 : pm0;
   const double D = (bcast(phi, LS) - phi0) / EPS_FD;
   const bool qp_ok = A.qp_status[b] == VC_SOLVED;
+  // a first QP without a solution (infeasible, or linearised where the model is near-singular)
+  // cannot be fixed by further SQP iterations from the same iterate: the iterate restarts from
+  // the neutral guess (u = 0, the state iterate the current state at every stage, the plan
+  // vc_simulate's failure restart would give) and the remaining iterations solve from there
+  const bool restart = A.restart && A.first && !qp_ok;
   // lane 0..LS-1: sufficient decrease?  the first such lane (largest alpha) wins
   const bool good = l < LS && qp_ok && D < 0.0 && isfinite(phi) && phi <= phi0 + ARMIJO * alpha * D;
   const uint64_t mask = __ballot(good);
@@ -175,10 +182,11 @@ __global__ __launch_bounds__(64) void kin_merit_kernel(KinMeritArgs A) {
       }
     }
     // the step's status is the first QP's: a later QP that fails only stops the progress (its
-    // step is refused, alpha = 0), the accepted iterate never has a larger merit than the start
-    const int32_t st = A.first ? A.qp_status[b] : A.st_acc[b];
+    // step is refused, alpha = 0), the accepted iterate never has a larger merit than the start.
+    // A failed first QP restarts the iterate (below): then the next QP's status is the step's.
+    const int32_t st = (A.first || A.st_acc[b] == RESTART_PENDING) ? A.qp_status[b] : A.st_acc[b];
     const int32_t it = (A.first ? 0 : A.it_acc[b]) + A.qp_iters[b];
-    A.st_acc[b] = st;
+    A.st_acc[b] = restart ? RESTART_PENDING : st;
     A.it_acc[b] = it;
     A.status[b] = st;
     A.iters[b] = it;
@@ -190,7 +198,11 @@ __global__ __launch_bounds__(64) void kin_merit_kernel(KinMeritArgs A) {
     }
   }
   __syncthreads();  // lane 0's reads of u* have completed
-  for (int e = l; e < 2 * N; e += 64) ub[e] = step_to(up[e], ub[e], al);
+  for (int e = l; e < 2 * N; e += 64) ub[e] = restart ? 0.0 : step_to(up[e], ub[e], al);
+  if (restart && A.ms) {
+    double* xo = A.x_out + (size_t)b * (N + 1) * KIN_NX;
+    for (int e = l; e < (N + 1) * KIN_NX; e += 64) xo[e] = A.x0[(size_t)b * KIN_NX + e % KIN_NX];
+  }
 }
 
 // a QP that failed with non-finite output (the case kin_ric reports as VC_NONFINITE)

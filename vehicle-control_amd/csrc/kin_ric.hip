@@ -119,6 +119,9 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
   __shared__ KrSmem<N> s;
   const int l = threadIdx.x;
   const int b = blockIdx.x;  // identity placement: xcd_problem measured 21 % slower at N = 50
+  // elastic-on-failure pass (qp.elastic < 0, launched by vc_solve after the hard-row pass): only
+  // the problems that pass left non-solved are solved again, with elastic rows at -qp.elastic
+  if (A.qp.elastic < 0.0 && A.status[b] == VC_SOLVED) return;
   const vc_kin_mpc& W = A.w;
   const bool stl = l <= N;   // lane owns stage l = 0..N
   const int k = stl ? l : N;
@@ -324,7 +327,7 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
   }
   // elastic state rows (vc_qp.elastic = rho > 0): the slack t >= 0 of row 4 + j and its
   // multiplier le; me = 1 where the row is present and elastic
-  const double rho_el = A.qp.elastic;
+  const double rho_el = fabs(A.qp.elastic);
   double me[3], te[3], le[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
@@ -404,7 +407,13 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
     const double det = h00 * h11 - h01 * h01;
     // IEEE-exact reciprocal (tests/test_gpu_numerics.py): the plain v_rcp_f64 + Newton form turns
     // det = +inf (h00 h11 overflowing at barrier weights ~1e154) into NaN where 1/det = 0
+#ifdef VC_KIN_RIC_RAW_RCP  // diagnostic build only (scripts/: the round-2 inverse)
+    double id = __builtin_amdgcn_rcp(det);
+    id = id * (2.0 - det * id);
+    id = id * (2.0 - det * id);
+#else
     const double id = rcp_nr(det);
+#endif
     const double i00 = h11 * id, i01 = -h01 * id, i11 = h00 * id;
     {
       const int kc = l >= 15 && l < 25 ? (l - 15) / NXT : 0, ki = l >= 15 && l < 25 ? (l - 15) % NXT : 0;
@@ -424,7 +433,9 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
       }
     }
     WSYNC();
-    return h00 > 0.0 && det > 0.0;
+    // det = +inf (h00 h11 overflowing: a diverging barrier) is a failed factorisation: its exact
+    // reciprocal 0 would silently drop the input block (Hi = K = 0) from the Newton step
+    return h00 > 0.0 && det >= 0x1p-1022 && isfinite(det);  // (and a subnormal det)
   };
   // Riccati factorisation of the stage Hessians s.Qt (backward from P_N = Qt_N on xt)
   auto factor = [&]() -> bool {

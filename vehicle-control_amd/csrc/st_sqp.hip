@@ -579,7 +579,9 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
         }
       }
       WSYNC();
-      return h00 > 0.0 && det > 0.0;
+      // det = +inf (h00 h11 overflowing: a diverging barrier) is a failed factorisation: its exact
+      // reciprocal 0 would silently drop the input block (Hi = K = 0) from the Newton step
+      return h00 > 0.0 && det >= 0x1p-1022 && isfinite(det);  // (and a subnormal det)
     };
     // Riccati factorisation of the stage Hessians s.u.q.Qt (backward): K, Hi per stage.
     auto factor = [&]() -> bool {

@@ -148,6 +148,7 @@ struct KinMeritArgs {
   double* ls_diag;         // [B][4] optional: alpha, phi(u_prev), phi(accepted), directional derivative
   int B, N;
   int first;               // 1 on the first SQP iteration
+  int restart;             // 1: a failed first QP restarts the iterate from the neutral guess
   int ms;                  // multiple shooting (vc_qp.ms)
   double L;
   vc_kin_mpc w;

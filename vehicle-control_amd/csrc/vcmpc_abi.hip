@@ -508,6 +508,7 @@ int vc_solve_diag(vc_ctx* c, int B, const void* x0, const void* kappa, const voi
   a.x_in = a.x_out;  // multiple shooting (qp.ms): the warm-start states arrive in xbar
   const int S = c->p.qp.kin_sqp;
   if (S <= 0) {  // the LTV-QP contract: one QP step
+    if (a.qp.elastic < 0.0) a.qp.elastic = 0.0;  // elastic on failure is an SQP-step option
     if (kin_condensed(c)) VC_HIP(c, vc::launch_kin_ltv(a, N, c->stream));
     else VC_HIP(c, vc::launch_kin_ric(a, N, c->stream));
   } else {
@@ -539,12 +540,16 @@ int vc_solve_diag(vc_ctx* c, int B, const void* x0, const void* kappa, const voi
     m.it_acc = (int32_t*)(base + o_it);
     m.ls_diag = nullptr;
     m.ms = c->p.qp.ms;
+    m.restart = S > 1;
     m.x_prev = (const double*)(base + o_xp);
     m.B = B;
     m.N = N;
     m.L = a.L;
     m.w = a.w;
     m.obs = a.obs;
+    // qp.elastic < 0: hard rows first, elastic rows only where those fail (stagewise kernel only)
+    const bool elastic_retry = c->p.qp.elastic < 0.0 && !kin_condensed(c);
+    if (c->p.qp.elastic < 0.0) a.qp.elastic = 0.0;
     for (int i = 0; i < S; ++i) {
       VC_HIP(c, hipMemcpyAsync(base + o_up, a.u_out, (size_t)B * N * nu * 8, hipMemcpyDeviceToDevice, c->stream));
       if (m.ms)
@@ -552,6 +557,15 @@ int vc_solve_diag(vc_ctx* c, int B, const void* x0, const void* kappa, const voi
                                  c->stream));
       if (kin_condensed(c)) VC_HIP(c, vc::launch_kin_ltv(a, N, c->stream));
       else VC_HIP(c, vc::launch_kin_ric(a, N, c->stream));
+      if (elastic_retry) {
+        // elastic on failure: the QPs the hard-row pass left non-solved, again from the same
+        // iterate (the pre-step copies: the first pass has overwritten ubar / xbar in place)
+        vc::KinLtvArgs e = a;
+        e.qp.elastic = c->p.qp.elastic;
+        e.ubar = (const double*)(base + o_up);
+        if (m.ms) e.x_in = (const double*)(base + o_xp);
+        VC_HIP(c, vc::launch_kin_ric(e, N, c->stream));
+      }
       if (i == c->fault_iter && c->fault_problem >= 0 && c->fault_problem < B)
         VC_HIP(c, vc::launch_kin_qp_fault(a, N, c->fault_problem, c->stream));
       m.first = i == 0;

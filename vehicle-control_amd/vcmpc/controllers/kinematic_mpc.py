@@ -50,29 +50,35 @@ KIN_SHIFT_FROM_N = 30
 # N = 30 2 / 1 / 0.7 % vs 0 / 0 / 0.02 %; N = 20 0 / 0 / 0.04 % vs 0 / 0 / 0.03 %).
 KIN_OBS_MS = 1
 
-# ... and its QPs' v / delta rows are elastic (vc_qp.elastic): a slack t >= 0 per row at cost
-# KIN_OBS_ELASTIC t, the QP model of the merit's own L1 penalty (oracle/kin_sqp.py RHO), so every
-# SQP step has a QP solution -- a hard-row QP that the trust region or a far-off warm start makes
-# infeasible would otherwise end the control step non-solved (u = 0 and a neutral restart).
-KIN_OBS_ELASTIC = 1e3
+# A first QP without a solution (infeasible with the hard v / delta rows, or linearised where the
+# spatial model is near-singular) restarts the step's iterate from the neutral guess and the
+# remaining SQP iterations solve from there (kin_merit.hip, oracle/kin_sqp.py), instead of ending
+# the control step non-solved.  Elastic rows (vc_qp.elastic: a slack per row at the merit's own
+# L1 price, always or only on failure) make every QP solvable but were measured worse in closed
+# loop at N >= 30 (64 vehicles x 400 steps x 4 seeds, hard + restart / elastic on failure +
+# restart: N = 20 0 / 0 off track, 0 / 0 non-solved; N = 30 0 / 6 off, 14 / 319 non-solved,
+# max |ey| 3.6 / 43 m; N = 50 36 / 40 off, 813 / 763 non-solved, 0 / 5 obstacle hits; DESIGN.md
+# 2c), so the controller keeps hard rows; elastic stays available through the qp block.
+KIN_OBS_ELASTIC = 0.0
 # The elastic rows' interior point needs about twice the plain one's iterations (the multipliers
-# start on rho = la + le): its cap is raised with them.
+# start on rho = la + le): with elastic rows the cap is raised.
 KIN_OBS_MAX_ITER = 80
 
 
 def kin_qp_block(config) -> dict:
     """The kinematic controller's `qp` block: RTI_TRUST, the globalised multiple-shooting step
-    with elastic state rows when obstacles are on, the shifted warm start at long horizons, then the config's own `qp`
+    when obstacles are on, the shifted warm start at long horizons, then the config's own `qp`
     entries."""
     qp = dict(RTI_TRUST)
     if config.get("obstacles"):
         qp["kin_sqp"] = KIN_OBS_SQP
         qp["ms"] = KIN_OBS_MS
-        qp["elastic"] = KIN_OBS_ELASTIC
+        if KIN_OBS_ELASTIC:
+            qp["elastic"] = KIN_OBS_ELASTIC
     if int(config["horizon"]) >= KIN_SHIFT_FROM_N:
         qp["shift"] = 1
     qp.update(config.get("qp") or {})
-    if qp.get("elastic", 0.0) > 0.0:
+    if qp.get("elastic", 0.0) != 0.0:
         qp["max_iter"] = max(int(qp.get("max_iter", 0)), KIN_OBS_MAX_ITER)
     return qp
 
