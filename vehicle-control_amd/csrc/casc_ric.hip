@@ -249,7 +249,8 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
         const double u2[2] = {s.ub[kk][0], s.ub[kk][1]};
         const double kp = s.kap[kk];
         double xn[8];
-        rk4_apply<double, 8>(x, s.dsv[kk], [&](const double* xx, double* f) { dyn_spatial_ode_alg<double, double>(xx, u2, kp, c, f); }, xn);
+        const double th = dyn_fx_split(u2[0]);  // one tanh per step, not per evaluation
+        rk4_apply<double, 8>(x, s.dsv[kk], [&](const double* xx, double* f) { dyn_spatial_ode_alg_th<double, double>(xx, u2, th, kp, c, f); }, xn);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           x[i] = xn[i];
@@ -328,7 +329,8 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
           u2[0].d[0] = col == 6 ? 1.0 : 0.0;
           u2[1].d[0] = col == 7 ? 1.0 : 0.0;
           const D1 kp(s.kap[kk]);
-          rk4_apply<D1, 8>(x, D1(s.dsv[kk]), [&](const D1* xx, D1* f) { dyn_spatial_ode_alg<D1, double>(xx, u2, kp, c, f); }, xn);
+          const D1 th = dyn_fx_split(u2[0]);
+          rk4_apply<D1, 8>(x, D1(s.dsv[kk]), [&](const D1* xx, D1* f) { dyn_spatial_ode_alg_th<D1, double>(xx, u2, th, kp, c, f); }, xn);
           const double s0 = col == 6 ? S : 1.0;
           const int yr[6] = {0, 1, 2, 3, 5, 6};
 #pragma unroll

@@ -553,7 +553,8 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
         const double u2[2] = {s.ub[k][0], s.ub[k][1]};
         const double kp = s.kap[k];
         double xn[8];
-        rk4_apply<double, 8>(x, s.dsv[k], [&](const double* xx, double* f) { dyn_spatial_ode_alg<double, double>(xx, u2, kp, c, f); }, xn);
+        const double th = dyn_fx_split(u2[0]);  // one tanh per step, not per evaluation
+        rk4_apply<double, 8>(x, s.dsv[k], [&](const double* xx, double* f) { dyn_spatial_ode_alg_th<double, double>(xx, u2, th, kp, c, f); }, xn);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           x[i] = xn[i];

@@ -140,7 +140,8 @@ __device__ __forceinline__ void predict(DynSmem<N>& s, const DynCoef<float>& p, 
     const float u[2] = {s.ub[k][0], s.ub[k][1]};
     const float kap = s.kap[k];
     float xn[8];
-    rk4_apply<float, 8>(x, s.dsv[k], [&](const float* xs, float* f) { dyn_spatial_ode_alg(xs, u, kap, p, f); }, xn);
+    const float th = dyn_fx_split(u[0]);  // one tanh per step, not per evaluation
+    rk4_apply<float, 8>(x, s.dsv[k], [&](const float* xs, float* f) { dyn_spatial_ode_alg_th(xs, u, th, kap, p, f); }, xn);
 #pragma unroll
     for (int i = 0; i < 8; ++i) x[i] = xn[i];
     dom = dom && dyn_in_domain(x, s.kap[k + 1]);
@@ -177,7 +178,8 @@ __device__ __forceinline__ void linearize(DynSmem<N>& s, const DynCoef<float>& p
   const T kap(s.kap[k]);
   const T h(s.dsv[k]);
   T xn[8];
-  rk4_apply<T, 8>(x, h, [&](const T* xs, T* f) { dyn_spatial_ode_alg(xs, u, kap, p, f); }, xn);
+  const T th = dyn_fx_split(u[0]);
+  rk4_apply<T, 8>(x, h, [&](const T* xs, T* f) { dyn_spatial_ode_alg_th(xs, u, th, kap, p, f); }, xn);
   constexpr int row_of[7] = {0, 1, 2, 3, 5, 6, 7};
 #pragma unroll
   for (int r = 0; r < 7; ++r)

@@ -291,7 +291,8 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
         const double u2[2] = {s.ub[kk][0], s.ub[kk][1]};
         const double kp = s.kap[kk];
         double xn[8];
-        rk4_apply<double, 8>(x, s.dsv[kk], [&](const double* xx, double* f) { dyn_spatial_ode_alg<double, double>(xx, u2, kp, c, f); }, xn);
+        const double th = dyn_fx_split(u2[0]);  // one tanh per step, not per evaluation
+        rk4_apply<double, 8>(x, s.dsv[kk], [&](const double* xx, double* f) { dyn_spatial_ode_alg_th<double, double>(xx, u2, th, kp, c, f); }, xn);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           x[i] = xn[i];
@@ -353,7 +354,8 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
           u2[0].d[0] = pr == 3 ? 1.0 : 0.0;
           u2[1].d[1] = pr == 3 ? 1.0 : 0.0;
           const D2 kp(s.kap[kk]);
-          rk4_apply<D2, 8>(x, D2(s.dsv[kk]), [&](const D2* xx, D2* f) { dyn_spatial_ode_alg<D2, double>(xx, u2, kp, c, f); }, xn);
+          const D2 th = dyn_fx_split(u2[0]);
+          rk4_apply<D2, 8>(x, D2(s.dsv[kk]), [&](const D2* xx, D2* f) { dyn_spatial_ode_alg_th<D2, double>(xx, u2, th, kp, c, f); }, xn);
           // columns of [A6 | B6] (y index of the seeds) and the t-row
           const int c0 = pr < 3 ? 2 * pr : 6, c1 = c0 + 1;
           const double s0 = pr == 3 ? S : 1.0;

@@ -99,6 +99,13 @@ __device__ __forceinline__ Dual<K, S> vsin(const Dual<K, S>& a) { return dmap(a,
 template <int K, typename S>
 __device__ __forceinline__ Dual<K, S> vcos(const Dual<K, S>& a) { return dmap(a, S(vcos(a.v)), S(-vsin(a.v))); }
 template <int K, typename S>
+__device__ __forceinline__ void vsincos(const Dual<K, S>& a, Dual<K, S>& s, Dual<K, S>& c) {
+  S sv, cv;
+  vsincos(a.v, sv, cv);
+  s = dmap(a, sv, cv);
+  c = dmap(a, cv, S(-sv));
+}
+template <int K, typename S>
 __device__ __forceinline__ Dual<K, S> vtan(const Dual<K, S>& a) {
   const S t = vtan(a.v);
   return dmap(a, t, S(1) + t * t);

@@ -21,6 +21,9 @@ __host__ __device__ inline double vatan(double x) { return atan(x); }
 __host__ __device__ inline double vtanh(double x) { return tanh(x); }
 __host__ __device__ inline double vsqrt(double x) { return sqrt(x); }
 __host__ __device__ inline double vfabs(double x) { return fabs(x); }
+// sin and cos of one argument from one range reduction: bit-identical to sin(x), cos(x)
+// (scripts/ubench/model.hip: 0 of 4.2 M inputs differ) at 409 instead of 691 cycles of latency
+__host__ __device__ inline void vsincos(double x, double& s, double& c) { sincos(x, &s, &c); }
 #if defined(__HIP_DEVICE_COMPILE__)
 __device__ inline float vsin(float x) { return __sinf(x); }
 __device__ inline float vcos(float x) { return __cosf(x); }
@@ -35,6 +38,10 @@ inline float vtanh(float x) { return tanhf(x); }
 __host__ __device__ inline float vatan(float x) { return atanf(x); }
 __host__ __device__ inline float vsqrt(float x) { return sqrtf(x); }
 __host__ __device__ inline float vfabs(float x) { return fabsf(x); }
+__host__ __device__ inline void vsincos(float x, float& s, float& c) {
+  s = vsin(x);
+  c = vcos(x);
+}
 
 constexpr int KIN_NX = 6, KIN_NU = 2;
 constexpr int DYN_NX = 8, DYN_NU = 2;
@@ -273,11 +280,20 @@ __host__ __device__ inline void dyn_stage_terms(const T* X5, const DynCoef<R>& c
 // (identities exact for |alpha| < pi/2); the fp64 plant and the oracle keep the
 // reference's literal form.
 // ---------------------------------------------------------------------------
+// the input-only transcendental of the algebraic model: the front / rear Fx split
+// tanh(2 (Fx / 1000 + 1/2)) (tanh(-y) = -tanh(y) gives the rear share)
+template <typename T>
+__host__ __device__ inline T dyn_fx_split(T Fx) {
+  return vtanh(T(2) * (Fx * T(1e-3) + T(0.5)));
+}
+
 template <typename T, typename R>
 struct DynForcesAlg {
   T Fx_f, Fx_r, Fz_f, Fz_r, ta_f, ta_r, cd, sd, iU;
-  __host__ __device__ DynForcesAlg(T Ux, T Uy, T r, T delta, T Fx, const DynCoef<R>& c) {
-    const T th = vtanh(T(2) * (Fx * T(1e-3) + T(0.5)));   // tanh(-y) = -tanh(y) for the rear split
+  __host__ __device__ DynForcesAlg(T Ux, T Uy, T r, T delta, T Fx, const DynCoef<R>& c)
+      : DynForcesAlg(Ux, Uy, r, delta, Fx, dyn_fx_split(Fx), c) {}
+  // th = dyn_fx_split(Fx), precomputed by callers that evaluate one input several times (RK4)
+  __host__ __device__ DynForcesAlg(T Ux, T Uy, T r, T delta, T Fx, T th, const DynCoef<R>& c) {
     Fx_f = Fx * (T(c.xf_a) * th + T(c.xf_b));
     Fx_r = Fx * (T(c.xr_b) - T(c.xr_a) * th);
     const T gz = T(c.gz0) + T(c.Av2) * (Ux * Ux);
@@ -286,8 +302,7 @@ struct DynForcesAlg {
     iU = T(1) / Ux;
     const T zf = (Uy + T(c.a) * r) * iU;
     ta_r = (Uy - T(c.b) * r) * iU;
-    cd = vcos(delta);
-    sd = vsin(delta);
+    vsincos(delta, sd, cd);
     // tan(atan zf - delta) = (zf cd - sd) / (cd + zf sd)
     ta_f = (zf * cd - sd) / (cd + zf * sd);
   }
@@ -311,10 +326,11 @@ __host__ __device__ inline T fiala_fy_alg(T ta, R Ca, T Fymax, R tam_k, R fi1, R
 }
 
 template <typename T, typename R>
-__host__ __device__ inline void dyn_temporal_ode_alg(const T* x, const T* u, T kappa, const DynCoef<R>& c, T* f) {
+__host__ __device__ inline void dyn_temporal_ode_alg(const T* x, const T* u, T th, T kappa, const DynCoef<R>& c,
+                                                     T* f) {
   const T Ux = x[0], Uy = x[1], r = x[2], ey = x[5], epsi = x[6];
   const T Fx = u[0], w = u[1];
-  const DynForcesAlg<T, R> F(Ux, Uy, r, x[3], Fx, c);
+  const DynForcesAlg<T, R> F(Ux, Uy, r, x[3], Fx, th, c);
   T Fy_f, Fy_r;
   if (c.tyre == VC_TYRE_LINEAR) {
     Fy_f = -T(c.Caf) * F.ta_f;
@@ -329,12 +345,31 @@ __host__ __device__ inline void dyn_temporal_ode_alg(const T* x, const T* u, T k
   f[1] = (lat_f + Fy_r) * T(c.inv_m) - r * Ux;
   f[2] = (T(c.a) * lat_f - T(c.b) * Fy_r) * T(c.inv_Izz);
   f[3] = w;
-  const T ce = vcos(epsi), se = vsin(epsi);
+  T se, ce;
+  vsincos(epsi, se, ce);
   const T s_dot = (Ux * ce - Uy * se) / (T(1) - kappa * ey);
   f[4] = s_dot;
   f[5] = Ux * se + Uy * ce;
   f[6] = r - kappa * s_dot;
   f[7] = T(1);
+}
+
+template <typename T, typename R>
+__host__ __device__ inline void dyn_temporal_ode_alg(const T* x, const T* u, T kappa, const DynCoef<R>& c, T* f) {
+  dyn_temporal_ode_alg(x, u, dyn_fx_split(u[0]), kappa, c, f);
+}
+
+// spatial form; th = dyn_fx_split(u[0]) (the RK4 steps compute it once for their 4 evaluations:
+// the same value, so the same result as the plain form)
+template <typename T, typename R>
+__host__ __device__ inline void dyn_spatial_ode_alg_th(const T* x, const T* u, T th, T kappa, const DynCoef<R>& c,
+                                                       T* f) {
+  dyn_temporal_ode_alg(x, u, th, kappa, c, f);
+  const T inv = T(1) / f[4];
+#pragma unroll
+  for (int i = 0; i < DYN_NX; ++i) f[i] = f[i] * inv;
+  f[4] = T(1);
+  f[7] = inv;
 }
 
 template <typename T, typename R>
