@@ -216,15 +216,18 @@ __host__ __device__ inline void dyn_temporal_ode(const T* x, const T* u, T kappa
     Fy_r = fiala_fy(F.alpha_r, T(c.Car), F.fymax_r(c), T(c.eps));
   }
   const T Fd = T(c.Frr) + T(c.Cd) * (Ux * Ux);
-  const T cd = vcos(delta), sd = vsin(delta);
+  T sd, cd;
+  vsincos(delta, sd, cd);
   const T m = T(c.m);
   f[0] = (F.Fx_f * cd - Fy_f * sd + F.Fx_r - Fd) / m + r * Uy;
   f[1] = (Fy_f * cd + F.Fx_f * sd + Fy_r) / m - r * Ux;
   f[2] = (T(c.a) * (Fy_f * cd + F.Fx_f * sd) - T(c.b) * Fy_r) / T(c.Izz);
   f[3] = w;
-  const T s_dot = (Ux * vcos(epsi) - Uy * vsin(epsi)) / (T(1) - kappa * ey);
+  T se, ce;
+  vsincos(epsi, se, ce);
+  const T s_dot = (Ux * ce - Uy * se) / (T(1) - kappa * ey);
   f[4] = s_dot;
-  f[5] = Ux * vsin(epsi) + Uy * vcos(epsi);
+  f[5] = Ux * se + Uy * ce;
   f[6] = r - kappa * s_dot;
   f[7] = T(1);
 }
@@ -404,9 +407,11 @@ template <typename T, typename R>
 __host__ __device__ inline void pm_spatial_ode(const T* x, const T* u, T kappa, const DynCoef<R>& c, T* f) {
   const T V = x[0], ey = x[2], epsi = x[3];
   const T Fd = T(c.Frr) + T(c.Cd) * (V * V);
-  const T s_dot = (V * vcos(epsi)) / (T(1) - kappa * ey);
+  T se, ce;
+  vsincos(epsi, se, ce);
+  const T s_dot = (V * ce) / (T(1) - kappa * ey);
   const T V_dot = (u[0] - Fd) / T(c.m);
-  const T ey_dot = V * vsin(epsi);
+  const T ey_dot = V * se;
   const T epsi_dot = u[1] / (T(c.m) * V) - kappa * s_dot;
   f[0] = V_dot / s_dot;
   f[1] = T(1);
