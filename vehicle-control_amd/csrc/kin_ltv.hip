@@ -45,6 +45,14 @@ __device__ __forceinline__ double lane_bcast(double v, int src) {
   const int hi = __builtin_amdgcn_readlane(__double2hiint(v), src);
   return __hiloint2double(hi, lo);
 }
+// `old` with lane `dst` replaced by the wave-uniform v (v_writelane: no lane-mask compare,
+// whose 40 per-sweep SGPR masks the compiler hoists and spills)
+__device__ int amdgcn_writelane(int v, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+__device__ __forceinline__ double lane_put(double old, double v, int dst) {
+  const int lo = amdgcn_writelane(__double2loint(v), dst, __double2loint(old));
+  const int hi = amdgcn_writelane(__double2hiint(v), dst, __double2hiint(old));
+  return __hiloint2double(hi, lo);
+}
 // v of lane (i - K) within each 16-lane DPP row, `ident` where that leaves the row
 template <int K>
 __device__ __forceinline__ double dpp_row_shr(double v, double ident) {
@@ -125,12 +133,34 @@ struct Dims {
   static_assert(n <= 64 && N >= 2, "one wavefront per problem needs 2 <= N <= 32");
 };
 
+// Column k of the Cholesky factor, L[j][k] for j = k..n-1, is stored at Lc[lc_base(k) + j].
+// lc_base(k) is even, so the entry pairs (j, j+1) with j even sit on 16-byte boundaries: both
+// columns of a trailing-update chunk load as ds_read_b128 at immediate offsets (a packed layout
+// left every other column odd, and its pairs became ds_read2_b64 behind a v_mov of the address).
+// Closed form (n even; a loop here became a divergent runtime loop where k is a lane's row):
+// column k starts at lc_start(k) = lc_base(k) + k, one padding slot after every even column.
+template <int n>
+__host__ __device__ constexpr int lc_base(int k) {
+  static_assert(n % 2 == 0, "even n");
+  return k * (n - 1) - k * (k - 1) / 2 + (k + 1) / 2;
+}
+template <int n>
+__host__ __device__ constexpr int lc_start(int k) {
+  return lc_base<n>(k) + k;
+}
+
 template <int N>
 struct Smem {
   using D = Dims<N>;
-  double G[D::NC][D::LD];   // constraint rows of the condensed sensitivity (row r: stage crow_stage(r))
+  static constexpr int LC_DUMMY = lc_start<D::n>(D::n);  // branch-free stores of inactive lanes
+  static constexpr int LC_ZERO = LC_DUMMY + 1;           // always 0.0 (solve reads above the factor)
+  // constraint rows of the condensed sensitivity (row r: stage crow_stage(r)); rows NC, NC+1 are
+  // zero (the normal-matrix build's last k-step), row NC+2 takes the sweep's dummy stores;
+  // column n is zero in every row
+  double G[D::NC + 3][D::LD];
   double H[D::n + 1][D::LD];  // condensed Hessian (constant over the solve); row n: dummy
-  double Lc[D::n * (D::n + 1) / 2 + 1];  // packed columns of the Cholesky factor (+1 dummy slot)
+  alignas(16) double Lc[LC_ZERO + 1];  // columns of the Cholesky factor (lc_base), dummy, zero
+  alignas(16) double zrow[48];  // zeros: the normal-matrix transpose reads it for other block rows
   double xb[N + 1][KIN_NX + 1];  // predicted trajectory (+1: dummy column for branch-free stores)
   double jac[N + 1][9];     // Jacobian data per stage (KinJac); row N: dummy
   double ub[D::n];          // warm-start inputs, interleaved (a_0, w_0, a_1, ...)
@@ -144,12 +174,6 @@ struct Smem {
 template <int N>
 __host__ __device__ constexpr int crow_stage(int r) {
   return r < N - 1 ? r + 1 : r - (N - 1) + 1;
-}
-
-// packed-column offset of column k of the factor (rows k..n-1)
-template <int n>
-__host__ __device__ constexpr int lc_off(int k) {
-  return k * n - k * (k - 1) / 2;
 }
 
 // sum_{i<LEN} a[i*SA] b[i*SB] over LDS operands, loaded one CH-chunk ahead of
@@ -233,109 +257,129 @@ __device__ __forceinline__ double rsq_nr(double d) {
 }
 
 // In-place right-looking Cholesky of the SPD matrix whose row `lane` is Mr (the lower
-// part: entries above the diagonal are not kept).  On return Mr holds row `lane` of L,
-// s.Lc its columns and s.dinv the inverse pivots 1/L_kk (uniform reads).
-// Returns false (uniform) if a pivot is not positive.
+// part: entries above the diagonal are not kept).  On return s.Lc holds the columns of L,
+// s.dinv the inverse pivots 1/L_kk (uniform reads), and Mr row `lane` of L strictly below
+// the diagonal with zeros on and above it -- the form chol_solve's select-free forward sweep
+// reads.  Returns false (uniform) if a pivot is not positive.
 //
-// Two columns per step (the same operations in the same order as the column-by-column
-// algorithm, so the factor is bit-identical to it): the 2x2 diagonal block comes from
-// lanes k, k+1 by readlane, both pivots are taken in registers, both columns published to
-// LDS, and one LDS round trip serves the rank-2 trailing update -- half the round trips of
-// one column per step, whose latency (store -> load ~85 cycles, rsq + Newton ~52) set the
-// factorisation time (scripts/ubench/lat.hip, profiles/r03/ubench_r03d.txt).  Columns k+2,
-// k+3 are updated first (lookahead), so the next block's pivots overlap this block's FMAs.
+// Two columns per step: the 2x2 diagonal block comes from lanes k, k+1 by readlane, both
+// pivots are taken in registers, both columns published to LDS, and one LDS round trip serves
+// the rank-2 trailing update.  Software-pipelined: the pivot block k+2, k+3 depends only on
+// the lookahead columns (chunk 0 of step k's update), so its chain -- readlanes, two rsq +
+// Newton, the column scaling and its LDS stores -- is split in three parts placed in the fence
+// regions of step k's update chunks 1, 2, 3, where the scheduler interleaves it with
+// independent FMAs.  Same operations in the same order as one column per step (bit-identical
+// factor).  The kernel is bound by instruction issue (every VALU instruction ~5 s_memtime
+// ticks at one wave per SIMD, scripts/ubench/thr.hip), so the layout keeps the count down:
+// both update columns load as ds_read_b128 at immediate offsets (lc_base), stores are
+// branch-free (dummy slot: lane-divergent ifs in this unrolled code make the allocator spill).
 template <int N>
 __device__ bool cholesky(double (&Mr)[Dims<N>::n], Smem<N>& s, int lane) {
   constexpr int n = Dims<N>::n;
   static_assert(n % 2 == 0, "two-column blocks");
-  constexpr int DUMMY = n * (n + 1) / 2;
+  constexpr int DUMMY = Smem<N>::LC_DUMMY;
   bool ok = true;
+  double pa, pb, pc, pi1, pl21, pi2;  // chain state of the pending pivot block
+  auto part = [&](int p, int k) {
+    if (p == 0) {  // 2x2 diagonal block from lanes k, k+1; first inverse pivot
+      pa = lane_bcast(Mr[k], k);
+      pb = lane_bcast(Mr[k], k + 1);
+      pc = lane_bcast(Mr[k + 1], k + 1);
+      pi1 = rsq_nr(pa);
+    } else if (p == 1) {  // second pivot after column k's update
+      pl21 = pb * pi1;
+      const double d2 = fma(-pl21, pl21, pc);
+      pi2 = rsq_nr(d2);
+      ok = ok && (pa > 0.0) && (d2 > 0.0);
+    } else {  // columns k, k+1 of this lane's row, published
+      const double x = Mr[k] * pi1;  // lane k: a / sqrt(a)
+      const double y = fma(-x, pl21, Mr[k + 1]) * pi2;
+      Mr[k] = x;
+      Mr[k + 1] = y;
+      s.Lc[lane >= k && lane < n ? lc_base<n>(k) + lane : DUMMY] = x;
+      s.Lc[lane >= k + 1 && lane < n ? lc_base<n>(k + 1) + lane : DUMMY] = y;
+      s.dinv[k] = pi1;
+      s.dinv[k + 1] = pi2;
+    }
+  };
+  part(0, 0);
+  part(1, 0);
+  part(2, 0);
 #pragma unroll
-  for (int k = 0; k < n; k += 2) {
-    const double a = lane_bcast(Mr[k], k), b = lane_bcast(Mr[k], k + 1), c = lane_bcast(Mr[k + 1], k + 1);
-    const double i1 = rsq_nr(a);
-    const double l21 = b * i1;                      // L[k+1][k]
-    const double d2 = fma(-l21, l21, c);            // lane k+1's pivot after column k's update
-    const double i2 = rsq_nr(d2);
-    ok = ok && (a > 0.0) && (d2 > 0.0);
-    const double x = (lane == k) ? a * i1 : Mr[k] * i1;   // L[lane][k]
-    const double y = fma(-x, l21, Mr[k + 1]) * i2;         // L[lane][k+1] (lane k+1: d2 / sqrt(d2))
-    Mr[k] = x;
-    Mr[k + 1] = y;
-    // branch-free stores (dummy slots): lane-divergent ifs in this fully unrolled code make
-    // the register allocator spill hundreds of VGPRs
-    s.Lc[lane >= k && lane < n ? lc_off<n>(k) + lane - k : DUMMY] = x;
-    s.Lc[lane >= k + 1 && lane < n ? lc_off<n>(k + 1) + lane - k - 1 : DUMMY] = y;
-    s.dinv[k] = i1;
-    s.dinv[k + 1] = i2;
-    if (k + 2 < n) {
-      wave_sync();  // columns k, k+1 visible
-      fence();
-      const double* c0 = &s.Lc[lc_off<n>(k) - k];          // c0[j] = L[j][k]
-      const double* c1 = &s.Lc[lc_off<n>(k + 1) - k - 1];  // c1[j] = L[j][k+1]
-      // the columns' entries in chunks of CH rows, each chunk loaded one chunk ahead of its
-      // FMAs (all at once would hold 4 (n - k) more VGPRs next to Mr and spill)
-      constexpr int CH = 4;
-      const int J0 = k + 2, NCH = (n - J0 + CH - 1) / CH;  // compile-time after unrolling
-      double u0[2][CH], u1[2][CH];
-      auto load = [&](int ch, int buf) {
+  for (int k = 0; k + 2 < n; k += 2) {
+    wave_sync();  // columns k, k+1 visible
+    fence();
+    const double x = Mr[k], y = Mr[k + 1];
+    // this lane's entries of columns k, k+1 are final: keep them strictly below the diagonal
+    // (lanes <= k hold the diagonal or the unkept upper part, which only the forward sweep reads)
+    Mr[k] = lane > k ? x : 0.0;
+    Mr[k + 1] = lane > k + 1 ? y : 0.0;
+    const double* c0 = &s.Lc[lc_base<n>(k)];      // c0[j] = L[j][k]
+    const double* c1 = &s.Lc[lc_base<n>(k + 1)];  // c1[j] = L[j][k+1]
+    constexpr int CH = 4;
+    const int J0 = k + 2, NCH = (n - J0 + CH - 1) / CH;  // compile-time after unrolling
+    double u0[2][CH], u1[2][CH];
+    auto load = [&](int ch, int buf) {
 #pragma unroll
-        for (int q = 0; q < CH; ++q) {
-          const int j = J0 + ch * CH + q;
-          u0[buf][q] = j < n ? c0[j] : 0.0;
-          u1[buf][q] = j < n ? c1[j] : 0.0;
-        }
-      };
-      load(0, 0);
-#pragma unroll
-      for (int ch = 0; ch < NCH; ++ch) {
-        if (ch + 1 < NCH) load(ch + 1, (ch + 1) & 1);
-        fence();
-        // chunk 0 starts with columns k+2, k+3: the next block's pivots (lookahead)
-#pragma unroll
-        for (int q = 0; q < CH; ++q) {
-          const int j = J0 + ch * CH + q;
-          if (j < n) Mr[j] = fma(-y, u1[ch & 1][q], fma(-x, u0[ch & 1][q], Mr[j]));
-        }
-        fence();
+      for (int q = 0; q < CH; ++q) {
+        const int j = J0 + ch * CH + q;
+        u0[buf][q] = j < n ? c0[j] : 0.0;
+        u1[buf][q] = j < n ? c1[j] : 0.0;
       }
+    };
+    load(0, 0);
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      if (ch + 1 < NCH) load(ch + 1, (ch + 1) & 1);
+      fence();
+      // chunk 0 starts with columns k+2, k+3: the next block's pivots (lookahead)
+#pragma unroll
+      for (int q = 0; q < CH; ++q) {
+        const int j = J0 + ch * CH + q;
+        if (j < n) Mr[j] = fma(-y, u1[ch & 1][q], fma(-x, u0[ch & 1][q], Mr[j]));
+      }
+      if (ch >= 1 && ch <= 3) part(ch - 1, k + 2);
+      fence();
+    }
+#pragma unroll
+    for (int p = NCH - 1; p < 3; ++p) {  // parts no chunk was left to hide
+      part(p < 0 ? 0 : p, k + 2);
+      fence();
     }
   }
+  Mr[n - 2] = lane > n - 2 ? Mr[n - 2] : 0.0;
+  Mr[n - 1] = 0.0;
   wave_sync();  // factor and inverse pivots visible to the solves
   return ok;
 }
 
-// Solve (L L') x = b, lane j holding b_j; returns x_j.  The forward sweep reads L[i][k]
-// from the row registers and broadcasts y_k = acc_k / L_kk from lane k (no LDS on the chain);
-// the backward sweep reads L[k][i] (column i of the packed factor) from LDS, prefetched one
-// 8-step chunk ahead so the LDS latency stays off the dependent chain.  (Round 3 measured a
-// four-unknown blocked variant -- uniform 4x4 diagonal blocks from LDS, a 10-step readlane
-// chain per sweep -- 13 % slower: the sweeps are bound by instruction issue, not by the chain,
-// profiles/r03/section_cycles_r03g.txt.)
+// Solve (L L') x = b, lane j holding b_j; returns x_j.  Forward sweep: y_k = acc_k / L_kk is
+// broadcast from lane k, and every lane subtracts L[lane][k] y_k from its accumulator with the
+// row registers zero on and above the diagonal (cholesky), so lane k's accumulator stops
+// changing once y_k is taken and y = acc / L_kk at the end -- no per-step select (a finite
+// factor times 0 subtracts exactly 0: the same values as collecting y_k per step).  Backward
+// sweep: lane i reads L[k][i] (column i of the factor) from LDS at immediate offsets of one
+// per-lane base, prefetched one 8-step chunk ahead, and x_i is written into lane i at step i
+// by v_writelane (entries k < i of the read are the previous column's storage: after step i
+// they no longer matter) -- cheaper than a zero-or-entry address select per element.  (A four-unknown blocked variant
+// was 13 % slower: the sweeps are bound by instruction issue, profiles/r03/section_cycles_r03g.txt.)
 template <int N>
 __device__ double chol_solve(const double (&Lr)[Dims<N>::n], const Smem<N>& s, double b, int lane) {
   constexpr int n = Dims<N>::n;
   constexpr int CH = 8;
   static_assert(n % CH == 0, "backward prefetch chunks");
   const int row = lane < n ? lane : 0;
-  const int off = lc_off<n>(row) - row;
+  lds_cdouble* col = lds_opaque(&s.Lc[lc_base<n>(row)]);  // col[k] = L[k][row] for k > row
   const double dj = s.dinv[row];
-  double acc = b, y = 0.0;
+  double acc = b;
 #pragma unroll
-  for (int k = 0; k < n; ++k) {  // L y = b
-    const double yk = lane_bcast(acc * dj, k);
-    y = (lane == k) ? yk : y;
-    acc -= Lr[k] * yk;
-  }
-  acc = y;
+  for (int k = 0; k < n; ++k) acc -= Lr[k] * lane_bcast(acc * dj, k);  // L y = b
+  acc *= dj;                                                           // y
   double x = 0.0;
   double lk[2][CH];
   auto fetch = [&](int c, int buf) {  // L[k][row] for k = n-1-c*CH ... n-CH-c*CH
 #pragma unroll
-    for (int q = 0; q < CH; ++q) {
-      const int k = n - 1 - c * CH - q;
-      lk[buf][q] = s.Lc[k >= row ? off + k : 0];
-    }
+    for (int q = 0; q < CH; ++q) lk[buf][q] = col[n - 1 - c * CH - q];
   };
   fetch(0, 0);
 #pragma unroll
@@ -346,50 +390,12 @@ __device__ double chol_solve(const double (&Lr)[Dims<N>::n], const Smem<N>& s, d
     for (int q = 0; q < CH; ++q) {
       const int k = n - 1 - c * CH - q;
       const double xk = lane_bcast(acc * dj, k);
-      x = (lane == k) ? xk : x;
+      x = lane_put(x, xk, k);
       acc -= lk[c & 1][q] * xk;
     }
     fence();
   }
   return x;
-}
-
-// Mr = row `lane` of H + diag(wb) + sum_r wc_r g_r g_r'  (wc broadcast in s.vc;
-// row r of G has 2 crow_stage(r) nonzero columns)
-template <int N>
-__device__ __forceinline__ void build_normal(double (&Mr)[Dims<N>::n], const Smem<N>& s, double wb, int lane) {
-  constexpr int n = Dims<N>::n, NC = Dims<N>::NC;
-  constexpr int LD = Dims<N>::LD;
-  const int j = lane < n ? lane : 0;
-  lds_cdouble* Hrow = lds_opaque(&s.H[j][0]);
-#pragma unroll
-  for (int i = 0; i < n; ++i) {
-    Mr[i] = Hrow[i] + (i == lane ? wb : 0.0);
-    if ((i & 7) == 7) fence();
-  }
-  lds_cdouble* G = lds_opaque(&s.G[0][0]);
-  lds_cdouble* Gcol = lds_opaque(&s.G[0][j]);
-  lds_cdouble* vc = lds_opaque(&s.vc[0]);
-#pragma unroll
-  for (int r = 0; r < NC; ++r) {
-    // each row's broadcast operands are loaded into registers at once, so their
-    // LDS latency is paid once per row rather than once per few FMAs.
-    // unconditional (clamped-index) loads: a `lane < n ? load : 0` select becomes
-    // a divergent branch, and branches inside this unrolled block make the
-    // register allocator spill; rows of lanes >= n are discarded below
-    constexpr int dummy = 0;
-    (void)dummy;
-    double gr[2 * (N - 1)];
-#pragma unroll
-    for (int i = 0; i < 2 * crow_stage<N>(r); ++i) gr[i] = G[r * LD + i];
-    const double t = vc[r] * Gcol[r * LD];
-    fence();
-#pragma unroll
-    for (int i = 0; i < 2 * crow_stage<N>(r); ++i) Mr[i] += t * gr[i];
-    fence();
-  }
-#pragma unroll
-  for (int i = 0; i < n; ++i) Mr[i] = (lane < n) ? Mr[i] : 0.0;
 }
 
 // Does MFMA k-step ks (G rows 4 ks .. 4 ks + 3) touch block-row I of the lower block
@@ -406,21 +412,46 @@ __host__ __device__ constexpr bool kstep_hits(int ks, int I) {
   return false;
 }
 
-// The same normal matrix with the constraint part C'WC on the matrix cores:
-// M_c = (W G)' G as 16x16 tiles of v_mfma_f64_16x16x4_f64 (K = the NC rows of G,
-// 4 per step; only the lower block triangle), then moved from the MFMA
-// accumulator layout to the row-per-lane layout one 16-row block at a time
-// through a 16 x 49 LDS buffer that aliases the (not yet written) factor storage.
+// The normal matrix M = H + diag(wb) + (W G)' G, row `lane` into Mr.  The constraint part on
+// the matrix cores: 16x16 tiles of v_mfma_f64_16x16x4_f64 (K = the NC rows of G, 4 per step;
+// only the lower block triangle), accumulated onto H + diag(wb) loaded in the accumulator
+// layout (lane l, element q of tile (I, J): row 16 I + (l >> 4) + 4 q, column 16 J + (l & 15)),
+// then moved to the row-per-lane layout one 16-row block at a time through a 16 x 49 LDS
+// buffer that aliases the (not yet written) factor storage.  Select-free (every VALU
+// instruction costs the same ~5 ticks as an fp64 FMA here): diag(wb) enters through lane j's
+// own H[j][j] slot (written before the tile loads, restored after), padding comes from zero
+// rows / columns in LDS (G rows NC, NC+1, H column n), and lanes outside the block row being
+// moved read the zero row zrow.  hjj: this lane's H[j][j].
 template <int N>
-__device__ __forceinline__ void build_normal_mfma(double (&Mr)[Dims<N>::n], Smem<N>& s, double wb, int lane) {
+__device__ __forceinline__ void build_normal_mfma(double (&Mr)[Dims<N>::n], Smem<N>& s, double wb, double hjj,
+                                                  int lane) {
   constexpr int n = Dims<N>::n, NC = Dims<N>::NC, LD = Dims<N>::LD;
   constexpr int NB = (n + 15) / 16, KS = (NC + 3) / 4, NT = NB * (NB + 1) / 2, BLD = 16 * NB + 1;
-  static_assert(16 * BLD <= n * (n + 1) / 2 + 1, "transpose buffer must fit the factor storage");
+  static_assert(16 * BLD <= Smem<N>::LC_DUMMY, "transpose buffer must fit the factor storage");
+  static_assert(4 * KS <= NC + 2, "G zero rows cover the last k-step");
+  static_assert(16 * NB <= 48, "zero row length");
   using d4 = __attribute__((ext_vector_type(4))) double;
   const int lr = lane >> 4, lc = lane & 15;
+  const int jd = lane < n ? lane : n;  // lanes >= n: the dummy row's padding slot
+  s.H[jd][jd] = hjj + wb;
+  wave_sync();
   d4 acc[NT];
+  {
+    lds_cdouble* H = lds_opaque(&s.H[0][0]);
 #pragma unroll
-  for (int t = 0; t < NT; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int I = 0, t = 0; I < NB; ++I) {
+#pragma unroll
+      for (int J = 0; J <= I; ++J, ++t) {
+        const int c = 16 * J + lc < n ? 16 * J + lc : n;  // column n of H is zero
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r0 = 16 * I + 4 * q;  // row r0 + lr: every lane of this q is padding when r0 >= n
+          acc[t][q] = r0 < n ? H[(r0 + lr) * LD + c] : 0.0;
+        }
+      }
+    }
+  }
+  s.H[jd][jd] = hjj;  // LDS executes in issue order: the loads above saw hjj + wb
   lds_cdouble* G = lds_opaque(&s.G[0][0]);
   lds_cdouble* vc = lds_opaque(&s.vc[0]);
   // all operands loaded up front (Mr is not live yet, so the registers are free):
@@ -428,36 +459,27 @@ __device__ __forceinline__ void build_normal_mfma(double (&Mr)[Dims<N>::n], Smem
   double gk[KS][NB], wk[KS];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
-    // operands of k-step ks: lane l holds row r = 4 ks + (l >> 4), column 16 J + (l & 15)
+    // operands of k-step ks: lane l holds row r = 4 ks + (l >> 4) (rows NC, NC+1 are zero),
+    // column 16 J + (l & 15) (column n is zero)
     const int r = 4 * ks + lr;
-    const int rr = r < NC ? r : 0;
-    wk[ks] = vc[rr];
+    wk[ks] = vc[r];
 #pragma unroll
     for (int J = 0; J < NB; ++J) {
       const int c = 16 * J + lc;
-      gk[ks][J] = G[rr * LD + (c < n ? c : 0)];  // clamped, unconditional load
+      gk[ks][J] = G[r * LD + (c < n ? c : n)];
     }
   }
   fence();
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
-    const bool rv = 4 * ks + lr < NC;
-    double g[NB];
-#pragma unroll
-    for (int J = 0; J < NB; ++J) g[J] = (rv && 16 * J + lc < n) ? gk[ks][J] : 0.0;
 #pragma unroll
     for (int I = 0, t = 0; I < NB; ++I) {
-      const double a = wk[ks] * g[I];
+      const double a = wk[ks] * gk[ks][I];
 #pragma unroll
       for (int J = 0; J <= I; ++J, ++t)
-        if (kstep_hits<N>(ks, I)) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, g[J], acc[t], 0, 0, 0);
+        if (kstep_hits<N>(ks, I)) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, gk[ks][J], acc[t], 0, 0, 0);
     }
   }
-  // Mr = H row + diag, then add this lane's row of M_c block-row by block-row
-  const int j0 = lane < n ? lane : 0;
-  lds_cdouble* Hrow = lds_opaque(&s.H[j0][0]);
-#pragma unroll
-  for (int i = 0; i < n; ++i) Mr[i] = Hrow[i] + (i == lane ? wb : 0.0);
   double* buf = &s.Lc[0];
   const int myI = lane >> 4;
 #pragma unroll
@@ -469,20 +491,16 @@ __device__ __forceinline__ void build_normal_mfma(double (&Mr)[Dims<N>::n], Smem
       for (int q = 0; q < 4; ++q) buf[(lr + 4 * q) * BLD + 16 * J + lc] = acc[t0 + J][q];
     }
     wave_sync();
-    lds_cdouble* brow = lds_opaque(&buf[lc * BLD]);
+    lds_cdouble* brow = lds_opaque(myI == I ? &buf[lc * BLD] : &s.zrow[0]);
     constexpr int dummy = 0;
     (void)dummy;
 #pragma unroll
     for (int i = 0; i < n; ++i) {
-      if (i < 16 * (I + 1)) {
-        const double v = brow[i];
-        Mr[i] += (myI == I) ? v : 0.0;
-      }
+      if (I == 0) Mr[i] = i < 16 ? brow[i] : 0.0;
+      else if (i < 16 * (I + 1)) Mr[i] += brow[i];
     }
   }
   wave_sync();  // buffer reads done before the factorisation overwrites it
-#pragma unroll
-  for (int i = 0; i < n; ++i) Mr[i] = (lane < n) ? Mr[i] : 0.0;
 }
 
 // inequality data of one lane role (box or state row): bounds lo <= y <= hi,
@@ -514,6 +532,9 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
     s.ds[lane] = A.ds[(size_t)b * N + lane];
   }
   if (lane < KIN_NX) s.xb[0][lane] = A.x0[(size_t)b * KIN_NX + lane];
+  for (int i = lane; i < 2 * D::LD; i += 64) (&s.G[NC][0])[i] = 0.0;  // zero rows NC, NC+1
+  if (lane < 48) s.zrow[lane] = 0.0;
+  if (lane == 0) s.Lc[Smem<N>::LC_ZERO] = 0.0;
   wave_sync();
 
 #ifdef VC_TIMING
@@ -540,7 +561,25 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
       const double u2[2] = {s.ub[2 * k], s.ub[2 * k + 1]};
       const double h = s.ds[k];
       double f[KIN_NX];
-      kin_spatial_ode(x, u2, s.kap[k], A.L, f);
+      // kin_spatial_ode (kinematic_car.py:47-64) with its three transcendentals taken in
+      // parallel lanes: lane 0 sincos(epsi), lane 1 sincos(delta) -- one range reduction each
+      // instead of cos(epsi), tan(epsi), tan(delta) one after another on the uniform chain
+      // (S1 is the sweep's only serial transcendental chain); tan = sin / cos
+      {
+        double sn, cs;
+        vsincos((lane & 1) ? x[1] : x[4], sn, cs);
+        const double se = lane_bcast(sn, 0), ce = lane_bcast(cs, 0);
+        const double sd = lane_bcast(sn, 1), cd = lane_bcast(cs, 1);
+        const double kap = s.kap[k];
+        const double rho = 1.0 - x[3] * kap;
+        const double q = rho / (x[0] * ce);
+        f[0] = q * u2[0];
+        f[1] = q * u2[1];
+        f[2] = 1.0;
+        f[3] = rho * (se / ce);
+        f[4] = ((sd / cd) / A.L) * (rho / ce) - kap;
+        f[5] = q;
+      }
       double mine = 0.0;
 #pragma unroll
       for (int i = 0; i < KIN_NX; ++i) {
@@ -619,9 +658,9 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
       ct += h * dq;
       cv = ncv; cd = ncd; cey = ncey; cep = ncep;
       // rows of stage k+1: v and delta constraint rows (k+1 <= N-1), ey cost row
-      const bool has = k + 1 <= N - 1;  // stage N has no constraint rows: padding column
-      s.G[has ? k : 0][has ? jcol : n] = cv;
-      s.G[has ? (N - 1) + k : 0][has ? jcol : n] = cd;
+      const bool has = k + 1 <= N - 1;  // stage N has no constraint rows: dummy row
+      s.G[has ? k : NC + 2][jcol] = cv;
+      s.G[has ? (N - 1) + k : NC + 2][jcol] = cd;
       E[k * LD + jcol] = cey;
       gj += lin2 * cey;
     }
@@ -703,6 +742,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
     const int j = lane < n ? lane : n;  // lanes >= n write the dummy row
 #pragma unroll
     for (int i = 0; i < n; ++i) s.H[j][i] = Hr[i];
+    s.H[j][n] = 0.0;  // zero column (normal-matrix padding)
   }
   if (A.mode == 1) {  // vc_condense: expose the QP data of the fused kernel
     if (lane < n) {
@@ -743,7 +783,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
     }
   }
   const double mtot = double(4 * N + 3 * (N - 1));
-  double scale, hdiag_max;
+  double scale, hdiag_max, hjj = 0.0;  // hjj: this lane's H[j][j]
   {
     double m = fabs(gj);
     if (bx.hasLo) m = fmax(m, fabs(bx.lo));
@@ -751,11 +791,10 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
     if (cs.hasLo) m = fmax(m, fabs(cs.lo));
     if (cs.hasHi) m = fmax(m, fabs(cs.hi));
     scale = 1.0 + wave_max(m);
-    double dg = 0.0;
 #pragma unroll
     for (int i = 0; i < n; ++i)
-      if (i == lane) dg = Hr[i];
-    hdiag_max = fmax(wave_max(dg), 1.0);
+      if (i == lane) hjj = Hr[i];
+    hdiag_max = fmax(wave_max(hjj), 1.0);
   }
   // start point dz = 0, slacks max(d, 1), multipliers 1 (oracle/qp.py uses the same rule)
   double z = 0.0;
@@ -810,7 +849,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
       wave_sync();
       VC_TACC(T_RESID, t_res0)
       VC_TSTAMP(t_build0)
-      build_normal_mfma<N>(Mr, s, wlo_b + whi_b, lane);
+      build_normal_mfma<N>(Mr, s, wlo_b + whi_b, hjj, lane);
       VC_TACC(T_BUILD, t_build0)
       VC_TSTAMP(t_chol0)
       const bool chol_ok = cholesky<N>(Mr, s, lane);
@@ -932,7 +971,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
       s.vc[lane] = rho_c;
       wave_sync();
       if (__ballot(rho_c > 0.0)) {
-        build_normal_mfma<N>(Mr, s, 0.0, lane);
+        build_normal_mfma<N>(Mr, s, 0.0, hjj, lane);
       } else {  // no active state row (most problems): the reduced Hessian only
         const int j0 = lane < n ? lane : 0;
         lds_cdouble* Hrow = lds_opaque(&s.H[j0][0]);
