@@ -35,6 +35,10 @@
 #include "vc_models.hpp"
 #include "vcmpc.h"
 
+#ifndef KIN_CHOL_CH
+#define KIN_CHOL_CH 8  // rows per trailing-update chunk, loaded one chunk ahead (4: +5 % factorisation time)
+#endif
+
 namespace vc {
 namespace {
 
@@ -316,7 +320,7 @@ __device__ bool cholesky(double (&Mr)[Dims<N>::n], Smem<N>& s, int lane) {
     Mr[k + 1] = lane > k + 1 ? y : 0.0;
     const double* c0 = &s.Lc[lc_base<n>(k)];      // c0[j] = L[j][k]
     const double* c1 = &s.Lc[lc_base<n>(k + 1)];  // c1[j] = L[j][k+1]
-    constexpr int CH = 4;
+    constexpr int CH = KIN_CHOL_CH;
     const int J0 = k + 2, NCH = (n - J0 + CH - 1) / CH;  // compile-time after unrolling
     double u0[2][CH], u1[2][CH];
     auto load = [&](int ch, int buf) {
@@ -398,39 +402,123 @@ __device__ double chol_solve(const double (&Lr)[Dims<N>::n], const Smem<N>& s, d
   return x;
 }
 
-// Does MFMA k-step ks (G rows 4 ks .. 4 ks + 3) touch block-row I of the lower block
-// triangle?  Row r of G is zero beyond column 2 crow_stage(r) (stage k's sensitivity sees
-// only the inputs of stages < k), so a k-step whose four rows all end at or before
-// column 16 I adds exact zeros to every tile (I, J <= I) and is skipped.  N = 20: 33 of
-// the 60 tile-steps remain (block-row 0: 10 k-steps, 1: 7, 2: 3).
-template <int N>
+// Nonzero extent of row r of the two LDS row sets the matrix cores take Gram matrices of:
+// ROWS_G, the constraint rows of G (row r is zero beyond column 2 crow_stage(r): stage k's
+// sensitivity sees only the inputs of stages < k; rows NC, NC+1 are the zero rows), and
+// ROWS_E, the ey cost rows E[k] (ey_{k+1}, zero beyond column 2 (k+1)) plus the terminal v_N /
+// epsi_N rows and two zero rows.
+enum { ROWS_G = 0, ROWS_E = 1 };
+template <int N, int KIND>
+__host__ __device__ constexpr int row_extent(int r) {
+  if (KIND == ROWS_G) return r < Dims<N>::NC ? 2 * crow_stage<N>(r) : 0;
+  return r < N ? 2 * (r + 1) : (r < N + 2 ? 2 * N : 0);
+}
+template <int N, int KIND>
+__host__ __device__ constexpr int gram_rows() {
+  return KIND == ROWS_G ? Dims<N>::NC : N + 2;
+}
+// Does MFMA k-step ks (rows 4 ks .. 4 ks + 3) touch block-row I of the lower block triangle?
+// A k-step whose four rows all end at or before column 16 I adds exact zeros to every tile
+// (I, J <= I) and is skipped.  N = 20, G: 33 of the 60 tile-steps remain (block-row 0: 10
+// k-steps, 1: 7, 2: 3); E: 20 of 36.
+template <int N, int KIND>
 __host__ __device__ constexpr bool kstep_hits(int ks, int I) {
-  for (int q = 0; q < 4; ++q) {
-    const int r = 4 * ks + q;
-    if (r < Dims<N>::NC && 2 * crow_stage<N>(r) > 16 * I) return true;
-  }
+  for (int q = 0; q < 4; ++q)
+    if (row_extent<N, KIND>(4 * ks + q) > 16 * I) return true;
   return false;
 }
 
-// The normal matrix M = H + diag(wb) + (W G)' G, row `lane` into Mr.  The constraint part on
-// the matrix cores: 16x16 tiles of v_mfma_f64_16x16x4_f64 (K = the NC rows of G, 4 per step;
-// only the lower block triangle), accumulated onto H + diag(wb) loaded in the accumulator
-// layout (lane l, element q of tile (I, J): row 16 I + (l >> 4) + 4 q, column 16 J + (l & 15)),
-// then moved to the row-per-lane layout one 16-row block at a time through a 16 x 49 LDS
-// buffer that aliases the (not yet written) factor storage.  Select-free (every VALU
-// instruction costs the same ~5 ticks as an fp64 FMA here): diag(wb) enters through lane j's
-// own H[j][j] slot (written before the tile loads, restored after), padding comes from zero
-// rows / columns in LDS (G rows NC, NC+1, H column n), and lanes outside the block row being
-// moved read the zero row zrow.  hjj: this lane's H[j][j].
+using d4 = __attribute__((ext_vector_type(4))) double;
+template <int N>
+struct Tiles {
+  static constexpr int n = Dims<N>::n, NB = (n + 15) / 16, NT = NB * (NB + 1) / 2, BLD = 16 * NB + 1;
+  static constexpr int count(bool full) { return full ? NB * NB : NT; }
+};
+
+// acc += (W R)' R over the rows R of one LDS row set (row stride LD, column n zero, rows up to
+// 4 KS - 1 readable) with weights w[r]: 16x16 tiles of v_mfma_f64_16x16x4_f64, K = 4 rows per
+// step, the lower block triangle (tile t of row I, column J <= I in order) or, FULL, every
+// tile (t = NB I + J).  Operands are loaded up front (the LDS latency paid once): lane l
+// holds row 4 ks + (l >> 4), column 16 J + (l & 15).
+template <int N, int KIND, bool FULL>
+__device__ __forceinline__ void gram_mfma(d4 (&acc)[Tiles<N>::count(FULL)], const double* rows, const double* w,
+                                          int lane) {
+  constexpr int n = Dims<N>::n, LD = Dims<N>::LD, NB = Tiles<N>::NB;
+  constexpr int KS = (gram_rows<N, KIND>() + 3) / 4;
+  const int lr = lane >> 4, lc = lane & 15;
+  lds_cdouble* R = lds_opaque(rows);
+  lds_cdouble* W = lds_opaque(w);
+  double gk[KS][NB], wk[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const int r = 4 * ks + lr;
+    wk[ks] = W[r];
+#pragma unroll
+    for (int J = 0; J < NB; ++J) {
+      const int c = 16 * J + lc;
+      gk[ks][J] = R[r * LD + (c < n ? c : n)];
+    }
+  }
+  fence();
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+    for (int I = 0, t = 0; I < NB; ++I) {
+      const double a = wk[ks] * gk[ks][I];
+#pragma unroll
+      for (int J = 0; J < (FULL ? NB : I + 1); ++J, ++t)
+        if (kstep_hits<N, KIND>(ks, I > J ? I : J))
+          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, gk[ks][J], acc[t], 0, 0, 0);
+    }
+  }
+}
+
+// Accumulator tiles (lane l, element q of tile (I, J): row 16 I + (l >> 4) + 4 q, column
+// 16 J + (l & 15)) to row `lane` in Mr -- its lower block triangle, or the whole row (FULL) --
+// one 16-row block at a time through a 16 x 49 LDS buffer aliasing the (not yet written)
+// factor storage.  Select-free: lanes outside the block row being moved read the zero row.
+template <int N, bool FULL>
+__device__ __forceinline__ void tiles_to_rows(double (&Mr)[Dims<N>::n], const d4 (&acc)[Tiles<N>::count(FULL)],
+                                              Smem<N>& s, int lane) {
+  constexpr int n = Dims<N>::n, NB = Tiles<N>::NB, BLD = Tiles<N>::BLD;
+  static_assert(16 * BLD <= Smem<N>::LC_DUMMY, "transpose buffer must fit the factor storage");
+  static_assert(16 * NB <= 48, "zero row length");
+  const int lr = lane >> 4, lc = lane & 15;
+  double* buf = &s.Lc[0];
+  const int myI = lane >> 4;
+#pragma unroll
+  for (int I = 0, t0 = 0; I < NB; ++I, t0 += FULL ? NB : I) {
+    wave_sync();  // previous block-row consumed
+#pragma unroll
+    for (int J = 0; J < (FULL ? NB : I + 1); ++J) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) buf[(lr + 4 * q) * BLD + 16 * J + lc] = acc[t0 + J][q];
+    }
+    wave_sync();
+    lds_cdouble* brow = lds_opaque(myI == I ? &buf[lc * BLD] : &s.zrow[0]);
+    constexpr int dummy = 0;
+    (void)dummy;
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+      const int iend = FULL ? n : 16 * (I + 1);
+      if (I == 0) Mr[i] = i < iend ? brow[i] : 0.0;
+      else if (i < iend) Mr[i] += brow[i];
+    }
+  }
+  wave_sync();  // buffer reads done before the factorisation overwrites it
+}
+
+// The normal matrix M = H + diag(wb) + (W G)' G, row `lane` into Mr: the constraint part on
+// the matrix cores (gram_mfma over the G rows, weights s.vc), accumulated onto H + diag(wb)
+// loaded in the accumulator layout, then moved to rows (tiles_to_rows).  Select-free (every
+// VALU instruction costs the same ~5 ticks as an fp64 FMA here): diag(wb) enters through
+// lane j's own H[j][j] slot (written before the tile loads, restored after), padding comes
+// from zero rows / columns in LDS (G rows NC, NC+1, H column n).  hjj: this lane's H[j][j].
 template <int N>
 __device__ __forceinline__ void build_normal_mfma(double (&Mr)[Dims<N>::n], Smem<N>& s, double wb, double hjj,
                                                   int lane) {
-  constexpr int n = Dims<N>::n, NC = Dims<N>::NC, LD = Dims<N>::LD;
-  constexpr int NB = (n + 15) / 16, KS = (NC + 3) / 4, NT = NB * (NB + 1) / 2, BLD = 16 * NB + 1;
-  static_assert(16 * BLD <= Smem<N>::LC_DUMMY, "transpose buffer must fit the factor storage");
-  static_assert(4 * KS <= NC + 2, "G zero rows cover the last k-step");
-  static_assert(16 * NB <= 48, "zero row length");
-  using d4 = __attribute__((ext_vector_type(4))) double;
+  constexpr int n = Dims<N>::n, LD = Dims<N>::LD, NB = Tiles<N>::NB, NT = Tiles<N>::NT;
+  static_assert(4 * ((Dims<N>::NC + 3) / 4) <= Dims<N>::NC + 2, "G zero rows cover the last k-step");
   const int lr = lane >> 4, lc = lane & 15;
   const int jd = lane < n ? lane : n;  // lanes >= n: the dummy row's padding slot
   s.H[jd][jd] = hjj + wb;
@@ -452,55 +540,8 @@ __device__ __forceinline__ void build_normal_mfma(double (&Mr)[Dims<N>::n], Smem
     }
   }
   s.H[jd][jd] = hjj;  // LDS executes in issue order: the loads above saw hjj + wb
-  lds_cdouble* G = lds_opaque(&s.G[0][0]);
-  lds_cdouble* vc = lds_opaque(&s.vc[0]);
-  // all operands loaded up front (Mr is not live yet, so the registers are free):
-  // the LDS latency is paid once, not once per k-step
-  double gk[KS][NB], wk[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    // operands of k-step ks: lane l holds row r = 4 ks + (l >> 4) (rows NC, NC+1 are zero),
-    // column 16 J + (l & 15) (column n is zero)
-    const int r = 4 * ks + lr;
-    wk[ks] = vc[r];
-#pragma unroll
-    for (int J = 0; J < NB; ++J) {
-      const int c = 16 * J + lc;
-      gk[ks][J] = G[r * LD + (c < n ? c : n)];
-    }
-  }
-  fence();
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-#pragma unroll
-    for (int I = 0, t = 0; I < NB; ++I) {
-      const double a = wk[ks] * gk[ks][I];
-#pragma unroll
-      for (int J = 0; J <= I; ++J, ++t)
-        if (kstep_hits<N>(ks, I)) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, gk[ks][J], acc[t], 0, 0, 0);
-    }
-  }
-  double* buf = &s.Lc[0];
-  const int myI = lane >> 4;
-#pragma unroll
-  for (int I = 0, t0 = 0; I < NB; t0 += ++I) {
-    wave_sync();  // previous block-row consumed
-#pragma unroll
-    for (int J = 0; J <= I; ++J) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) buf[(lr + 4 * q) * BLD + 16 * J + lc] = acc[t0 + J][q];
-    }
-    wave_sync();
-    lds_cdouble* brow = lds_opaque(myI == I ? &buf[lc * BLD] : &s.zrow[0]);
-    constexpr int dummy = 0;
-    (void)dummy;
-#pragma unroll
-    for (int i = 0; i < n; ++i) {
-      if (I == 0) Mr[i] = i < 16 ? brow[i] : 0.0;
-      else if (i < 16 * (I + 1)) Mr[i] += brow[i];
-    }
-  }
-  wave_sync();  // buffer reads done before the factorisation overwrites it
+  gram_mfma<N, ROWS_G, false>(acc, &s.G[0][0], &s.vc[0], lane);
+  tiles_to_rows<N, false>(Mr, acc, s, lane);
 }
 
 // inequality data of one lane role (box or state row): bounds lo <= y <= hi,
@@ -561,10 +602,11 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
       const double u2[2] = {s.ub[2 * k], s.ub[2 * k + 1]};
       const double h = s.ds[k];
       double f[KIN_NX];
-      // kin_spatial_ode (kinematic_car.py:47-64) with its three transcendentals taken in
-      // parallel lanes: lane 0 sincos(epsi), lane 1 sincos(delta) -- one range reduction each
-      // instead of cos(epsi), tan(epsi), tan(delta) one after another on the uniform chain
-      // (S1 is the sweep's only serial transcendental chain); tan = sin / cos
+      // kin_spatial_ode (kinematic_car.py:47-64) with its transcendentals and divides taken in
+      // parallel lanes (S1 is the sweep's only serial chain): lane 0 sincos(epsi), lane 1
+      // sincos(delta) -- one range reduction each instead of cos(epsi), tan(epsi), tan(delta)
+      // one after another -- then the four quotients tan(epsi) = sin/cos, tan(delta) / L,
+      // rho / cos(epsi) and q = rho / (v cos(epsi)) as one divide in lanes 0..3
       {
         double sn, cs;
         vsincos((lane & 1) ? x[1] : x[4], sn, cs);
@@ -572,12 +614,17 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
         const double sd = lane_bcast(sn, 1), cd = lane_bcast(cs, 1);
         const double kap = s.kap[k];
         const double rho = 1.0 - x[3] * kap;
-        const double q = rho / (x[0] * ce);
+        const int r4 = lane & 3;
+        const double num = r4 == 0 ? se : (r4 == 1 ? sd : rho);
+        const double den = r4 == 0 ? ce : (r4 == 1 ? cd * A.L : (r4 == 2 ? ce : x[0] * ce));
+        const double quo = num / den;
+        const double te = lane_bcast(quo, 0), tdl = lane_bcast(quo, 1);
+        const double rc = lane_bcast(quo, 2), q = lane_bcast(quo, 3);
         f[0] = q * u2[0];
         f[1] = q * u2[1];
         f[2] = 1.0;
-        f[3] = rho * (se / ce);
-        f[4] = ((sd / cd) / A.L) * (rho / ce) - kap;
+        f[3] = rho * te;
+        f[4] = tdl * rc - kap;
         f[5] = q;
       }
       double mine = 0.0;
@@ -672,82 +719,60 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
   VC_TACC(T_S3, t_s30)
   VC_TSTAMP(t_s40)
   double Hr[n];
-  {  // S4
+  double hjj;  // this lane's H[j][j]
+  {  // S4: H = E' diag(w) E on the matrix cores (gram_mfma over the ey rows and the terminal rows)
     const double vN = s.xb[N][0];
     const double cwv = (vN >= W.v_max) ? W.w_v : 0.0;
     gj += 2.0 * cwv * (vN - W.v_max) * cv;
     gj += 2.0 * W.w_epsi * s.xb[N][4] * cep;
     gj += W.w_time * ct;  // t_N (:149-151)
+    // weights of the terminal v_N (:144-148) and epsi_N (:155-157) rows, then two zero rows
+    if (lane < 4) s.vc[N + lane] = lane == 0 ? 2.0 * cwv : (lane == 1 ? 2.0 * W.w_epsi : 0.0);
+    for (int i = lane; i < 2 * LD; i += 64) E[(N + 2) * LD + i] = 0.0;
+    wave_sync();
+    // every tile: H is kept whole in LDS (the residual's H z reads full rows)
+    d4 acc[Tiles<N>::count(true)];
 #pragma unroll
-    for (int i = 0; i < n; ++i) Hr[i] = 0.0;
-    // runtime loop over the ey rows (a fully unrolled one lets the scheduler issue
-    // every row's loads at once and spill); inner loops are compile-time
-#pragma unroll 1
-    for (int k = 0; k < N; ++k) {
-      lds_cdouble* Ek = lds_opaque(E + k * LD);
-      double er[n];
-#pragma unroll
-      for (int i = 0; i < n; ++i) er[i] = Ek[i];
-      const double t = s.vc[k] * Ek[lane < n ? lane : n];
-      fence();
-#pragma unroll
-      for (int i = 0; i < n; ++i) Hr[i] += t * er[i];
-    }
-    {  // terminal v_N and epsi_N rows
-      lds_cdouble* Ev = lds_opaque(E + N * LD);
-      lds_cdouble* Ee = lds_opaque(E + (N + 1) * LD);
-      double ev[n], ee[n];
-#pragma unroll
-      for (int i = 0; i < n; ++i) {
-        ev[i] = Ev[i];
-        ee[i] = Ee[i];
-      }
-      const double tv = 2.0 * cwv * cv, te = 2.0 * W.w_epsi * cep;
-      fence();
-#pragma unroll
-      for (int i = 0; i < n; ++i) Hr[i] += tv * ev[i] + te * ee[i];
-    }
+    for (int t = 0; t < Tiles<N>::count(true); ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+    gram_mfma<N, ROWS_E, true>(acc, E, &s.vc[0], lane);
+    tiles_to_rows<N, true>(Hr, acc, s, lane);
   }
   // input costs: w_w w^2 (kinematic_mpc.py:124), slew w_a (a_{n+1}-a_n)^2 (:126-128), prox
-  {
-    const int kq = lane >> 1;
-    double dself = 2.0 * A.qp.prox, dm2 = 0.0, dp2 = 0.0;
-    if (lane < n) {
-      if (lane & 1) {
-        dself += 2.0 * W.w_w;
-        gj += 2.0 * W.w_w * s.ub[lane];
-      } else {
-        if (kq >= 1) {
-          dself += 2.0 * W.w_a; dm2 = -2.0 * W.w_a;
-          gj += 2.0 * W.w_a * (s.ub[lane] - s.ub[lane - 2]);
-        }
-        if (kq <= N - 2) {
-          dself += 2.0 * W.w_a; dp2 = -2.0 * W.w_a;
-          gj -= 2.0 * W.w_a * (s.ub[lane + 2] - s.ub[lane]);
-        }
+  const int kq = lane >> 1;
+  double dself = 2.0 * A.qp.prox, dm2 = 0.0, dp2 = 0.0;
+  if (lane < n) {
+    if (lane & 1) {
+      dself += 2.0 * W.w_w;
+      gj += 2.0 * W.w_w * s.ub[lane];
+    } else {
+      if (kq >= 1) {
+        dself += 2.0 * W.w_a; dm2 = -2.0 * W.w_a;
+        gj += 2.0 * W.w_a * (s.ub[lane] - s.ub[lane - 2]);
       }
-    }
-#pragma unroll
-    for (int i = 0; i < n; ++i) {
-      if (i == lane) Hr[i] += dself;
-      if (i == lane - 2) Hr[i] += dm2;
-      if (i == lane + 2) Hr[i] += dp2;
+      if (kq <= N - 2) {
+        dself += 2.0 * W.w_a; dp2 = -2.0 * W.w_a;
+        gj -= 2.0 * W.w_a * (s.ub[lane + 2] - s.ub[lane]);
+      }
     }
   }
   gj = (lane < n) ? gj : 0.0;
-#pragma unroll
-  for (int i = 0; i < n; ++i) Hr[i] = (lane < n) ? Hr[i] : 0.0;
-  wave_sync();
   {
     const int j = lane < n ? lane : n;  // lanes >= n write the dummy row
 #pragma unroll
     for (int i = 0; i < n; ++i) s.H[j][i] = Hr[i];
     s.H[j][n] = 0.0;  // zero column (normal-matrix padding)
+    // the input-cost band through this lane's own row in LDS (in issue order after the row
+    // store; a register add would need a lane-index select on all n entries); 0 where absent
+    s.H[j][j] += dself;
+    s.H[j][j >= 2 ? j - 2 : j] += dm2;
+    s.H[j][j + 2 < n ? j + 2 : j] += dp2;
+    hjj = lane < n ? s.H[j][j] : 0.0;
   }
+  wave_sync();
   if (A.mode == 1) {  // vc_condense: expose the QP data of the fused kernel
     if (lane < n) {
 #pragma unroll
-      for (int i = 0; i < n; ++i) A.H_out[((size_t)b * n + lane) * n + i] = Hr[i];
+      for (int i = 0; i < n; ++i) A.H_out[((size_t)b * n + lane) * n + i] = s.H[lane][i];
       A.g_out[(size_t)b * n + lane] = gj;
     }
     return;
@@ -783,7 +808,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
     }
   }
   const double mtot = double(4 * N + 3 * (N - 1));
-  double scale, hdiag_max, hjj = 0.0;  // hjj: this lane's H[j][j]
+  double scale, hdiag_max;
   {
     double m = fabs(gj);
     if (bx.hasLo) m = fmax(m, fabs(bx.lo));
@@ -791,9 +816,6 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
     if (cs.hasLo) m = fmax(m, fabs(cs.lo));
     if (cs.hasHi) m = fmax(m, fabs(cs.hi));
     scale = 1.0 + wave_max(m);
-#pragma unroll
-    for (int i = 0; i < n; ++i)
-      if (i == lane) hjj = Hr[i];
     hdiag_max = fmax(wave_max(hjj), 1.0);
   }
   // start point dz = 0, slacks max(d, 1), multipliers 1 (oracle/qp.py uses the same rule)
