@@ -35,6 +35,9 @@
 #include "vc_models.hpp"
 #include "vcmpc.h"
 
+#ifndef KIN_DOT_CH
+#define KIN_DOT_CH 8  // terms per chunk of the residual dot products
+#endif
 #ifndef KIN_CHOL_CH
 #define KIN_CHOL_CH 8  // rows per trailing-update chunk, loaded one chunk ahead (4: +5 % factorisation time)
 #endif
@@ -180,11 +183,11 @@ __host__ __device__ constexpr int crow_stage(int r) {
   return r < N - 1 ? r + 1 : r - (N - 1) + 1;
 }
 
-// sum_{i<LEN} a[i*SA] b[i*SB] over LDS operands, loaded one CH-chunk ahead of
-// their FMAs so the LDS latency is paid about once per call
-template <int LEN, int SA, int SB>
+// sum_{i<LEN} a[i*SA] b[i*SB] over LDS operands, loaded one CH-chunk ahead of their FMAs
+// (one scheduling fence per chunk) so the LDS latency is paid about once per call
+template <int LEN, int SA, int SB, int CH = KIN_DOT_CH>
 __device__ __forceinline__ double lds_dot(lds_cdouble* a, lds_cdouble* b) {
-  constexpr int CH = 4, NCH = (LEN + CH - 1) / CH;
+  constexpr int NCH = (LEN + CH - 1) / CH;
   double ca[2][CH], cb[2][CH];
   auto fetch = [&](int c, int buf) {
 #pragma unroll
@@ -205,8 +208,8 @@ __device__ __forceinline__ double lds_dot(lds_cdouble* a, lds_cdouble* b) {
       a0 += ca[c & 1][q] * cb[c & 1][q];
       a1 += ca[c & 1][q + 1] * cb[c & 1][q + 1];
     }
-    fence();
   }
+  fence();
   return a0 + a1;
 }
 
@@ -215,32 +218,17 @@ template <int N>
 __device__ double grow_dot(const Smem<N>& s, int lane) {
   constexpr int NC = Dims<N>::NC;
   const int r = lane < NC ? lane : 0;
-  lds_cdouble* g = lds_opaque(&s.G[r][0]);
-  lds_cdouble* v = lds_opaque(&s.vz[0]);
-  double a0 = 0.0, a1 = 0.0;
-#pragma unroll 4
-  for (int i = 0; i < 2 * (N - 1); i += 2) {
-    a0 += g[i] * v[i];
-    a1 += g[i + 1] * v[i + 1];
-  }
-  return lane < NC ? a0 + a1 : 0.0;
+  const double a = lds_dot<2 * (N - 1), 1, 1>(lds_opaque(&s.G[r][0]), lds_opaque(&s.vz[0]));
+  return lane < NC ? a : 0.0;
 }
 
 // (G' v)_j for lane j (v broadcast in s.vc)
 template <int N>
 __device__ double gt_dot(const Smem<N>& s, int lane) {
-  constexpr int n = Dims<N>::n, NC = Dims<N>::NC;
-  constexpr int LD = Dims<N>::LD;
+  constexpr int n = Dims<N>::n, NC = Dims<N>::NC, LD = Dims<N>::LD;
   const int j = lane < n ? lane : 0;
-  lds_cdouble* g = lds_opaque(&s.G[0][j]);
-  lds_cdouble* v = lds_opaque(&s.vc[0]);
-  double a0 = 0.0, a1 = 0.0;
-#pragma unroll 4
-  for (int r = 0; r < NC; r += 2) {
-    a0 += g[r * LD] * v[r];
-    a1 += g[(r + 1) * LD] * v[r + 1];
-  }
-  return lane < n ? a0 + a1 : 0.0;
+  const double a = lds_dot<NC, LD, 1>(lds_opaque(&s.G[0][j]), lds_opaque(&s.vc[0]));
+  return lane < n ? a : 0.0;
 }
 
 // (H v)_j for lane j (v broadcast in s.vz)
@@ -429,9 +417,12 @@ __host__ __device__ constexpr bool kstep_hits(int ks, int I) {
 }
 
 using d4 = __attribute__((ext_vector_type(4))) double;
+using d2 = __attribute__((ext_vector_type(2))) double;
 template <int N>
 struct Tiles {
-  static constexpr int n = Dims<N>::n, NB = (n + 15) / 16, NT = NB * (NB + 1) / 2, BLD = 16 * NB + 1;
+  // BLD even: the buffer rows are 16-byte aligned, so the row reads of tiles_to_rows pair up as
+  // ds_read_b128 (conflict-free: row starts 100 dwords apart spread over the 64 banks)
+  static constexpr int n = Dims<N>::n, NB = (n + 15) / 16, NT = NB * (NB + 1) / 2, BLD = 16 * NB + 2;
   static constexpr int count(bool full) { return full ? NB * NB : NT; }
 };
 
@@ -475,7 +466,7 @@ __device__ __forceinline__ void gram_mfma(d4 (&acc)[Tiles<N>::count(FULL)], cons
 
 // Accumulator tiles (lane l, element q of tile (I, J): row 16 I + (l >> 4) + 4 q, column
 // 16 J + (l & 15)) to row `lane` in Mr -- its lower block triangle, or the whole row (FULL) --
-// one 16-row block at a time through a 16 x 49 LDS buffer aliasing the (not yet written)
+// one 16-row block at a time through a 16 x 50 LDS buffer aliasing the (not yet written)
 // factor storage.  Select-free: lanes outside the block row being moved read the zero row.
 template <int N, bool FULL>
 __device__ __forceinline__ void tiles_to_rows(double (&Mr)[Dims<N>::n], const d4 (&acc)[Tiles<N>::count(FULL)],
@@ -495,14 +486,20 @@ __device__ __forceinline__ void tiles_to_rows(double (&Mr)[Dims<N>::n], const d4
       for (int q = 0; q < 4; ++q) buf[(lr + 4 * q) * BLD + 16 * J + lc] = acc[t0 + J][q];
     }
     wave_sync();
-    lds_cdouble* brow = lds_opaque(myI == I ? &buf[lc * BLD] : &s.zrow[0]);
-    constexpr int dummy = 0;
-    (void)dummy;
+    // 16-byte pair reads (BLD even; the laundered pointer hides the alignment from the compiler)
+    using lds_cd2 = const __attribute__((address_space(3))) d2;
+    lds_cd2* brow = (lds_cd2*)lds_opaque(myI == I ? &buf[lc * BLD] : &s.zrow[0]);
 #pragma unroll
-    for (int i = 0; i < n; ++i) {
+    for (int i = 0; i < n; i += 2) {
       const int iend = FULL ? n : 16 * (I + 1);
-      if (I == 0) Mr[i] = i < iend ? brow[i] : 0.0;
-      else if (i < iend) Mr[i] += brow[i];
+      if (i < iend) {
+        const d2 p = brow[i / 2];
+        if (I == 0) { Mr[i] = p.x; Mr[i + 1] = p.y; }
+        else { Mr[i] += p.x; Mr[i + 1] += p.y; }
+      } else if (I == 0) {
+        Mr[i] = 0.0;
+        Mr[i + 1] = 0.0;
+      }
     }
   }
   wave_sync();  // buffer reads done before the factorisation overwrites it
