@@ -35,6 +35,12 @@
 #include "vc_models.hpp"
 #include "vcmpc.h"
 
+#ifndef KIN_BLOCKED
+#define KIN_BLOCKED 1  // interior-point factorisation: panels + matrix-core trailing updates (0: row-per-lane `cholesky`)
+#endif
+#ifndef KIN_G_DOTS_CHUNKED
+#define KIN_G_DOTS_CHUNKED 1  // G-row / G-column dots as chunked lds_dot (0: rolled loops, no scratch)
+#endif
 #ifndef KIN_DOT_CH
 #define KIN_DOT_CH 8  // terms per chunk of the residual dot products
 #endif
@@ -96,6 +102,12 @@ __device__ __forceinline__ void wave_sync() {
   asm volatile("" ::: "memory");
 }
 __device__ __forceinline__ void fence() { __builtin_amdgcn_sched_barrier(0); }
+// the lane index through an opaque register: LDS addresses derived from it are recomputed
+// where they are used instead of being hoisted out of the solver loop (and spilled)
+__device__ __forceinline__ int lane_opaque(int lane) {
+  asm volatile("" : "+v"(lane));
+  return lane;
+}
 // compiler-only memory barrier: stops LICM from hoisting the (loop-invariant) LDS
 // reads of G / the factor out of the solver loops into thousands of live registers
 __device__ __forceinline__ void no_hoist() { asm volatile("" ::: "memory"); }
@@ -172,8 +184,13 @@ struct Smem {
   double jac[N + 1][9];     // Jacobian data per stage (KinJac); row N: dummy
   double ub[D::n];          // warm-start inputs, interleaved (a_0, w_0, a_1, ...)
   double kap[N], ds[N];
-  double vz[64];            // broadcast: a length-n vector (z, dz, ...)
-  double vc[64];            // broadcast: a length-NC vector (weights, residual terms)
+  union {
+    struct {
+      double vz[64];        // broadcast: a length-n vector (z, dz, ...)
+      double vc[64];        // broadcast: a length-NC vector (weights, residual terms)
+    };
+    alignas(16) double tb2[128];  // factor_blocked: last panel's transpose buffer (vz, vc are scratch then)
+  };
   double dinv[64];          // inverse pivots 1/L_kk of the current factor (uniform reads)
 };
 
@@ -213,6 +230,7 @@ __device__ __forceinline__ double lds_dot(lds_cdouble* a, lds_cdouble* b) {
   return a0 + a1;
 }
 
+#if KIN_G_DOTS_CHUNKED
 // y_r = G_r . v for lane r (v broadcast in s.vz); rows have <= 2(N-1) nonzeros
 template <int N>
 __device__ double grow_dot(const Smem<N>& s, int lane) {
@@ -230,6 +248,42 @@ __device__ double gt_dot(const Smem<N>& s, int lane) {
   const double a = lds_dot<NC, LD, 1>(lds_opaque(&s.G[0][j]), lds_opaque(&s.vc[0]));
   return lane < n ? a : 0.0;
 }
+
+#else
+// y_r = G_r . v for lane r (v broadcast in s.vz); rows have <= 2(N-1) nonzeros
+template <int N>
+__device__ double grow_dot(const Smem<N>& s, int lane) {
+  constexpr int NC = Dims<N>::NC;
+  const int r = lane < NC ? lane : 0;
+  lds_cdouble* g = lds_opaque(&s.G[r][0]);
+  lds_cdouble* v = lds_opaque(&s.vz[0]);
+  double a0 = 0.0, a1 = 0.0;
+#pragma unroll 4
+  for (int i = 0; i < 2 * (N - 1); i += 2) {
+    a0 += g[i] * v[i];
+    a1 += g[i + 1] * v[i + 1];
+  }
+  return lane < NC ? a0 + a1 : 0.0;
+}
+
+// (G' v)_j for lane j (v broadcast in s.vc)
+template <int N>
+__device__ double gt_dot(const Smem<N>& s, int lane) {
+  constexpr int n = Dims<N>::n, NC = Dims<N>::NC;
+  constexpr int LD = Dims<N>::LD;
+  const int j = lane < n ? lane : 0;
+  lds_cdouble* g = lds_opaque(&s.G[0][j]);
+  lds_cdouble* v = lds_opaque(&s.vc[0]);
+  double a0 = 0.0, a1 = 0.0;
+#pragma unroll 4
+  for (int r = 0; r < NC; r += 2) {
+    a0 += g[r * LD] * v[r];
+    a1 += g[(r + 1) * LD] * v[r + 1];
+  }
+  return lane < n ? a0 + a1 : 0.0;
+}
+
+#endif
 
 // (H v)_j for lane j (v broadcast in s.vz)
 template <int N>
@@ -270,6 +324,7 @@ __device__ bool cholesky(double (&Mr)[Dims<N>::n], Smem<N>& s, int lane) {
   constexpr int n = Dims<N>::n;
   static_assert(n % 2 == 0, "two-column blocks");
   constexpr int DUMMY = Smem<N>::LC_DUMMY;
+  lane = lane_opaque(lane);
   bool ok = true;
   double pa, pb, pc, pi1, pl21, pi2;  // chain state of the pending pivot block
   auto part = [&](int p, int k) {
@@ -369,9 +424,13 @@ __device__ double chol_solve(const double (&Lr)[Dims<N>::n], const Smem<N>& s, d
   acc *= dj;                                                           // y
   double x = 0.0;
   double lk[2][CH];
+  lds_cdouble* zero = lds_opaque(&s.zrow[0]);
   auto fetch = [&](int c, int buf) {  // L[k][row] for k = n-1-c*CH ... n-CH-c*CH
+    // a lane whose row is at or below every k of the chunk reads zeros at one shared address
+    // (broadcast) instead of the previous columns' storage (distinct addresses: bank conflicts)
+    lds_cdouble* src = row < n - 1 - c * CH ? col : zero;
 #pragma unroll
-    for (int q = 0; q < CH; ++q) lk[buf][q] = col[n - 1 - c * CH - q];
+    for (int q = 0; q < CH; ++q) lk[buf][q] = src[n - 1 - c * CH - q];
   };
   fetch(0, 0);
 #pragma unroll
@@ -436,6 +495,7 @@ __device__ __forceinline__ void gram_mfma(d4 (&acc)[Tiles<N>::count(FULL)], cons
                                           int lane) {
   constexpr int n = Dims<N>::n, LD = Dims<N>::LD, NB = Tiles<N>::NB;
   constexpr int KS = (gram_rows<N, KIND>() + 3) / 4;
+  lane = lane_opaque(lane);
   const int lr = lane >> 4, lc = lane & 15;
   lds_cdouble* R = lds_opaque(rows);
   lds_cdouble* W = lds_opaque(w);
@@ -474,6 +534,7 @@ __device__ __forceinline__ void tiles_to_rows(double (&Mr)[Dims<N>::n], const d4
   constexpr int n = Dims<N>::n, NB = Tiles<N>::NB, BLD = Tiles<N>::BLD;
   static_assert(16 * BLD <= Smem<N>::LC_DUMMY, "transpose buffer must fit the factor storage");
   static_assert(16 * NB <= 48, "zero row length");
+  lane = lane_opaque(lane);
   const int lr = lane >> 4, lc = lane & 15;
   double* buf = &s.Lc[0];
   const int myI = lane >> 4;
@@ -512,15 +573,14 @@ __device__ __forceinline__ void tiles_to_rows(double (&Mr)[Dims<N>::n], const d4
 // lane j's own H[j][j] slot (written before the tile loads, restored after), padding comes
 // from zero rows / columns in LDS (G rows NC, NC+1, H column n).  hjj: this lane's H[j][j].
 template <int N>
-__device__ __forceinline__ void build_normal_mfma(double (&Mr)[Dims<N>::n], Smem<N>& s, double wb, double hjj,
-                                                  int lane) {
-  constexpr int n = Dims<N>::n, LD = Dims<N>::LD, NB = Tiles<N>::NB, NT = Tiles<N>::NT;
+__device__ __forceinline__ void build_normal_acc(d4 (&acc)[Tiles<N>::NT], Smem<N>& s, double wb, double hjj, int lane) {
+  constexpr int n = Dims<N>::n, LD = Dims<N>::LD, NB = Tiles<N>::NB;
   static_assert(4 * ((Dims<N>::NC + 3) / 4) <= Dims<N>::NC + 2, "G zero rows cover the last k-step");
+  lane = lane_opaque(lane);
   const int lr = lane >> 4, lc = lane & 15;
   const int jd = lane < n ? lane : n;  // lanes >= n: the dummy row's padding slot
   s.H[jd][jd] = hjj + wb;
   wave_sync();
-  d4 acc[NT];
   {
     lds_cdouble* H = lds_opaque(&s.H[0][0]);
 #pragma unroll
@@ -538,7 +598,163 @@ __device__ __forceinline__ void build_normal_mfma(double (&Mr)[Dims<N>::n], Smem
   }
   s.H[jd][jd] = hjj;  // LDS executes in issue order: the loads above saw hjj + wb
   gram_mfma<N, ROWS_G, false>(acc, &s.G[0][0], &s.vc[0], lane);
+}
+
+template <int N>
+__device__ __forceinline__ void build_normal_mfma(double (&Mr)[Dims<N>::n], Smem<N>& s, double wb, double hjj,
+                                                  int lane) {
+  d4 acc[Tiles<N>::NT];
+  build_normal_acc<N>(acc, s, wb, hjj, lane);
   tiles_to_rows<N, false>(Mr, acc, s, lane);
+}
+
+// Blocked factorisation of the normal matrix straight from the build's accumulator tiles:
+// panels of 16 columns (the last one 8); for each, the panel's tiles (I, p), I >= p, are moved
+// to this lane's row registers (tile by tile through a 16 x 18 LDS buffer, select-free: lanes
+// outside block row I read the zero row), the panel is factored by the two-column pivot steps
+// of `cholesky` with the trailing update kept inside the panel, and the tiles to the right,
+// (I, J) with p < J <= I, take the panel's rank-16 update on the matrix cores
+// (v_mfma_f64_16x16x4_f64, operands = the just-stored factor columns from LDS): the trailing
+// update, 880 VALU FMAs + 380 broadcast reads in the row-per-lane factorisation, becomes
+// 16 MFMAs.  Output as `cholesky`'s: s.Lc columns, s.dinv, Mr = row `lane` of L strictly
+// below the diagonal.  Buffers: panels 0, 1 use the factor storage of columns >= 16 (written
+// only by panel 1's own steps, after its transposes), panel 2 the broadcast vectors (tb2).
+// Returns false (uniform) if a pivot is not positive.
+template <int N>
+__device__ bool factor_blocked(double (&Mr)[Dims<N>::n], d4 (&acc)[Tiles<N>::NT], Smem<N>& s, int lane) {
+  constexpr int n = Dims<N>::n, NB = Tiles<N>::NB;
+  constexpr int DUMMY = Smem<N>::LC_DUMMY;
+  static_assert(NB == 3 && n > 32 && n <= 40, "three panels, the last one at most 8 wide");
+  static_assert(lc_start<n>(16) + 16 * 18 <= DUMMY, "panel 0/1 transpose buffer inside the factor storage");
+  static_assert((lc_start<n>(16) & 1) == 0, "16-byte aligned transpose buffer");
+  lane = lane_opaque(lane);
+  const int lr = lane >> 4, lc = lane & 15, myI = lane >> 4;
+  bool ok = true;
+  double pa, pb, pc, pi1, pl21, pi2;  // chain state of the pending pivot block
+  auto part = [&](int p, int k) {
+    if (p == 0) {
+      pa = lane_bcast(Mr[k], k);
+      pb = lane_bcast(Mr[k], k + 1);
+      pc = lane_bcast(Mr[k + 1], k + 1);
+      pi1 = rsq_nr(pa);
+    } else if (p == 1) {
+      pl21 = pb * pi1;
+      const double d2 = fma(-pl21, pl21, pc);
+      pi2 = rsq_nr(d2);
+      ok = ok && (pa > 0.0) && (d2 > 0.0);
+    } else {
+      const double x = Mr[k] * pi1;
+      const double y = fma(-x, pl21, Mr[k + 1]) * pi2;
+      Mr[k] = x;
+      Mr[k + 1] = y;
+      s.Lc[lane >= k && lane < n ? lc_base<n>(k) + lane : DUMMY] = x;
+      s.Lc[lane >= k + 1 && lane < n ? lc_base<n>(k + 1) + lane : DUMMY] = y;
+      s.dinv[k] = pi1;
+      s.dinv[k + 1] = pi2;
+    }
+  };
+  using lds_cd2 = const __attribute__((address_space(3))) d2;
+#pragma unroll
+  for (int p = 0; p < NB; ++p) {
+    const int c0 = 16 * p, c1 = (16 * p + 16 < n) ? 16 * p + 16 : n, W = c1 - c0;
+    // ---- panel columns of this lane's row from tiles (I, p), I >= p
+    double* tb = p < 2 ? &s.Lc[lc_start<n>(16)] : &s.tb2[0];
+    const int TS = p < 2 ? 18 : 10;  // even stride: 16-byte rows, conflict-free row reads
+#pragma unroll
+    for (int i = c0; i < c1; ++i) Mr[i] = 0.0;
+#pragma unroll
+    for (int I = p; I < NB; ++I) {
+      const int t = I * (I + 1) / 2 + p;
+      wave_sync();  // previous tile consumed
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = lr + 4 * q;
+        if (4 * q < W)  // panel 2: rows 8..15 of its tile are padding
+          tb[(lc < W ? r * TS + lc : 8 * TS + lc)] = acc[t][q];  // lc >= W: dummy slots past the rows
+      }
+      wave_sync();
+      lds_cd2* src = (lds_cd2*)lds_opaque(myI == I && lc < W ? &tb[lc * TS] : &s.zrow[0]);
+#pragma unroll
+      for (int i = 0; i < W; i += 2) {
+        const d2 v = src[i / 2];
+        Mr[c0 + i] += v.x;
+        Mr[c0 + i + 1] += v.y;
+      }
+    }
+    wave_sync();  // buffer reads done before the panel's factor stores
+    // ---- the panel: two-column pivot steps, trailing update inside the panel
+    part(0, c0);
+    part(1, c0);
+    part(2, c0);
+#pragma unroll
+    for (int k = c0; k + 2 < c1; k += 2) {
+      wave_sync();  // columns k, k+1 visible
+      fence();
+      const double x = Mr[k], y = Mr[k + 1];
+      Mr[k] = lane > k ? x : 0.0;
+      Mr[k + 1] = lane > k + 1 ? y : 0.0;
+      const double* cA = &s.Lc[lc_base<n>(k)];
+      const double* cB = &s.Lc[lc_base<n>(k + 1)];
+      constexpr int CH = 4;
+      const int J0 = k + 2, NCH = (c1 - J0 + CH - 1) / CH;
+      double u0[2][CH], u1[2][CH];
+      auto load = [&](int ch, int buf) {
+#pragma unroll
+        for (int q = 0; q < CH; ++q) {
+          const int j = J0 + ch * CH + q;
+          u0[buf][q] = j < c1 ? cA[j] : 0.0;
+          u1[buf][q] = j < c1 ? cB[j] : 0.0;
+        }
+      };
+      load(0, 0);
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch) {
+        if (ch + 1 < NCH) load(ch + 1, (ch + 1) & 1);
+        fence();
+#pragma unroll
+        for (int q = 0; q < CH; ++q) {
+          const int j = J0 + ch * CH + q;
+          if (j < c1) Mr[j] = fma(-y, u1[ch & 1][q], fma(-x, u0[ch & 1][q], Mr[j]));
+        }
+        if (ch >= 1 && ch <= 3) part(ch - 1, k + 2);
+        fence();
+      }
+#pragma unroll
+      for (int pp = NCH - 1; pp < 3; ++pp) {
+        part(pp < 0 ? 0 : pp, k + 2);
+        fence();
+      }
+    }
+    Mr[c1 - 2] = lane > c1 - 2 ? Mr[c1 - 2] : 0.0;
+    Mr[c1 - 1] = lane > c1 - 1 ? Mr[c1 - 1] : 0.0;
+    wave_sync();  // the panel's factor columns visible
+    // ---- rank-W update of the tiles right of the panel on the matrix cores
+    if (p + 1 < NB) {
+      lds_cdouble* Lc = lds_opaque(&s.Lc[0]);
+      lds_cdouble* Z = lds_opaque(&s.zrow[0]);
+#pragma unroll
+      for (int ks = 0; ks < W / 4; ++ks) {
+        // operand of block row I: lane l holds L[16 I + (l & 15)][c0 + 4 ks + (l >> 4)]
+        const int kk = c0 + 4 * ks + lr;
+        double op[NB];
+#pragma unroll
+        for (int I = p + 1; I < NB; ++I) {
+          const int jj = 16 * I + lc;
+          op[I] = jj < n ? Lc[lc_base<n>(kk) + jj] : Z[0];
+        }
+#pragma unroll
+        for (int I = p + 1; I < NB; ++I) {
+#pragma unroll
+          for (int J = p + 1; J <= I; ++J) {
+            const int t = I * (I + 1) / 2 + J;
+            acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(-op[I], op[J], acc[t], 0, 0, 0);
+          }
+        }
+      }
+    }
+  }
+  wave_sync();  // factor and inverse pivots visible to the solves
+  return ok;
 }
 
 // inequality data of one lane role (box or state row): bounds lo <= y <= hi,
@@ -868,10 +1084,18 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
       wave_sync();
       VC_TACC(T_RESID, t_res0)
       VC_TSTAMP(t_build0)
+#if KIN_BLOCKED
+      d4 nacc[Tiles<N>::NT];
+      build_normal_acc<N>(nacc, s, wlo_b + whi_b, hjj, lane);
+      VC_TACC(T_BUILD, t_build0)
+      VC_TSTAMP(t_chol0)
+      const bool chol_ok = factor_blocked<N>(Mr, nacc, s, lane);
+#else
       build_normal_mfma<N>(Mr, s, wlo_b + whi_b, hjj, lane);
       VC_TACC(T_BUILD, t_build0)
       VC_TSTAMP(t_chol0)
       const bool chol_ok = cholesky<N>(Mr, s, lane);
+#endif
       VC_TACC(T_CHOL, t_chol0)
       if (!chol_ok) {
         // The barrier weights lambda/s of the active set (~1/mu) have made the
