@@ -827,9 +827,9 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": ("synthetic (seeded C2 sampler, vcmpc/workload.py: SURVEY 8(d)'s x0 / kappa / ubar "
-                     "distributions; ds = 0.03 v0 + 0.5, one constant per problem (the SURVEY's per-stage "
-                     "0.03 vbar_n + 0.5 with a constant speed prediction); problems whose warm-start rollout "
-                     "leaves v > 1 m/s or |epsi| < 1.2 rad are re-drawn)"),
+                     "distributions; per-stage ds_n = 0.03 vbar_n + 0.5 from the warm start's speed "
+                     "prediction, kinematic_mpc.py:178-182; problems whose warm-start rollout drops to "
+                     "v <= 1 m/s or reaches |epsi| >= 1.2 rad are re-drawn)"),
             "config": {"workload": f"C2 kinematic-bicycle LTV-MPC, B={B} per GPU, N={N_HORIZON}, fp64",
                        "batch_per_gpu": B, "global_batch": B * world, "horizon": N_HORIZON,
                        "parallelism": f"dp{world} (independent shards)"},
@@ -844,6 +844,9 @@ def main():
                          "traffic_unit": f"HBM bytes/launch (rocprofv3 FETCH_SIZE+WRITE_SIZE, {os.path.relpath(PMC_SUMMARY, ROOT)})",
                          "kernel": "kin_ltv_kernel<20>", "kernel_ms": kern_ms, "flops_per_solve": flops_F,
                          "flops_note": "SURVEY 8(d) F: 0.42 MFLOP sweep + (IPM iterations + 1 polish) x 0.28 MFLOP",
+                         "count": "dense-equivalent: F prices the dense condensing GEMM and dense C'DC the "
+                                  "kernel does not execute; the executed (structure-exploiting) count is "
+                                  "`structured`",
                          "structured": {"flops_per_solve": flops,
                                         "achieved": flops * B / (kern_ms / 1e3) / 1e12,
                                         "frac": flops * B / (kern_ms / 1e3) / 1e12 / FP64_VALU_PEAK,

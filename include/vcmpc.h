@@ -19,6 +19,8 @@
  *   vc_plant_step    RacingCar.drive / Robot.transition  vehicle_control/models/racing_car.py:34-46,
  *                    kinematic_car.py:34-45,66-68 (Euler), dynamic_car.py:144-167,193-195 (RK4)
  *   vc_spatial_step  <Model>.spatial_transition       kinematic_car.py:70-72, dynamic_car.py:169-199
+ *   vc_ode           the vector field f(x, u, curvature) the integrators wrap (utils/integrators.py:18,29):
+ *                    temporal kinematic_car.py:34-40, dynamic_car.py:153-167; spatial :47-60, :169-191
  *   vc_set_obstacles Track._construct_obstacles       environment/track.py:131-138 (the obstacle list the
  *                                                     barrier terms kinematic_mpc.py:130-133 read)
  *   vc_track_set     Track._precompute_curvatures     environment/track.py:156-167 (the bspline k(s) table)
@@ -58,7 +60,7 @@
 extern "C" {
 #endif
 
-#define VCMPC_ABI_VERSION 9
+#define VCMPC_ABI_VERSION 10
 #define VC_MAX_OBSTACLES 16
 
 typedef struct vc_ctx vc_ctx;
@@ -143,7 +145,8 @@ typedef struct vc_qp {
                        (oracle/ltv_qp.py elastic_qp).  -rho < 0 (kin_sqp > 0): elastic on failure
                        -- every QP is solved with hard rows and only the ones that solve leaves
                        non-solved are solved again with elastic rows at rho (SNOPT's elastic mode).
-                       0 = hard rows */
+                       0 = hard rows.  rho > 0 on a one-step context routes to the stagewise kernel;
+                       rho < 0 needs kin_sqp > 0 (vc_solve returns VC_E_ARG otherwise) */
 } vc_qp;
 
 /* Cascaded controller: single-track stages followed by a point-mass tail
@@ -283,6 +286,11 @@ int vc_plant_step(vc_ctx* ctx, int B, const void* x, const void* u, const void* 
 /* Spatial step x_next = spatial_transition(x, u, kappa, ds): ds[B]. */
 int vc_spatial_step(vc_ctx* ctx, int B, const void* x, const void* u, const void* kappa,
                     const void* ds, void* x_next, int flags);
+
+/* The continuous model f[b] = f(x[b], u[b], kappa[b]): space = 0 the temporal ODE (dx/dt, the
+ * `f` of the plant's integrator), space = 1 the spatial ODE (dx/ds of the MPC's integrator).
+ * x[B][nx], u[B][nu], kappa[B], f[B][nx] in the context dtype. */
+int vc_ode(vc_ctx* ctx, int B, const void* x, const void* u, const void* kappa, int space, void* f, int flags);
 
 /* ---- Track curvature and the batched closed loop ---------------
  *

@@ -5,7 +5,8 @@ Parity status: the reference holds no kinematic trace and no QP (its MPC is a
 CasADi/IPOPT NLP that cannot be imported here), so these vectors are
 the oracle's -- every solution carries a KKT optimality certificate (stat, pfeas,
 dfeas, comp < 1e-9) that the tests re-check.  Inputs: the C2 sampler
-(vcmpc/workload.py) plus hand-built edge cases (saturated inputs, boundary
+(vcmpc/workload.py: per-stage ds_n = 0.03 vbar_n + 0.5 from the warm start's speed
+prediction, kinematic_mpc.py:178-182) plus hand-built constant-ds edge cases (saturated inputs, boundary
 violation, terminal over-speed, a straight track).
 
 Run from the repo root:  python tests/golden/make_kin_golden.py
@@ -61,10 +62,11 @@ def main():
     print("B", len(inp["x0"]), "iters", sol["iters"].max(), {n: float(v.max()) for n, v in k.items()},
           "polished", sol["polished"].all())
     assert sol["polished"].all() and max(v.max() for v in k.values()) < 1e-9
+    Wk = sorted(k for k in W if np.isscalar(W[k]))       # the scalar weights / bounds (no obstacle list)
     nh = 16
     out = dict(inp, xbar=sol["xbar"], A=sol["A"][:nh], Bm=sol["Bm"][:nh], H=sol["H"][:nh], g=sol["g"][:nh],
                u_star=sol["u_star"], x_star=sol["x_star"], u0=sol["u0"], lam=sol["lam"],
-               L=np.float64(L), W=np.array([W[k] for k in sorted(W)]), W_keys=np.array(sorted(W)))
+               L=np.float64(L), W=np.array([W[k] for k in Wk]), W_keys=np.array(Wk))
     np.savez_compressed(os.path.join(HERE, "kin_ltv_golden.npz"), **out)
 
 

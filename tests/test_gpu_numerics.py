@@ -64,6 +64,9 @@ def test_reciprocal_classes(probe):
                               ref[:nspec][~normal_safe[:nspec]])))
         # inside the normal range both forms are within 1 ulp of IEEE
         assert np.nanmax(np.where(normal_safe, rel, 0)) <= 2.3e-16, x[bad][:5]
+    # rcp_nr (kin_ltv, and the Riccati kernels' 2x2 pivot inverses) is IEEE 1/x bit for bit on every
+    # input here, special classes included (r03c measured 1.00000; the kernels' comments rely on it)
+    np.testing.assert_array_equal(_bits(out[:, 1]), _bits(ref))
     # the classes the kernels see: kin_ltv's slacks / multipliers are positive normals; the
     # Riccati kernels' 2x2 determinants are finite positives of the normal range
     sl = np.exp(np.random.default_rng(1).uniform(np.log(1e-290), np.log(1e290), 4000))

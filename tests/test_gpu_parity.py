@@ -65,6 +65,49 @@ def test_kin_plant_and_spatial_step(ctx):
                                rtol=1e-13, atol=1e-13)
 
 
+def test_model_vector_field_f(ctx, dyn_ctx, dyn_kat, dyn_params):
+    """vc_ode / VehicleModel.f(x, u, curvature): the continuous vector field the reference's
+    integrators wrap (utils/integrators.py:18,29) -- temporal and spatial, kinematic and dynamic
+    -- against the oracle's ODEs (same fp64 formulas: 1e-13 relative), and the Euler identity
+    spatial_transition = x + ds f_spatial."""
+    rng = np.random.default_rng(1)
+    B = 500
+    x = np.column_stack([rng.uniform(2, 10, B), rng.uniform(-.3, .3, B), rng.uniform(0, 300, B),
+                         rng.uniform(-2, 2, B), rng.uniform(-.3, .3, B), rng.uniform(0, 5, B)])
+    u = np.column_stack([rng.uniform(-3, 3, B), rng.uniform(-.4, .4, B)])
+    k = rng.uniform(0, .05, B)
+    np.testing.assert_allclose(ctx.ode(x, u, k), M.kin_temporal_ode(x, u, k, L), rtol=1e-13, atol=1e-13)
+    fs = ctx.ode(x, u, k, space=True)
+    np.testing.assert_allclose(fs, M.kin_spatial_ode(x, u, k, L), rtol=1e-13, atol=1e-13)
+    ds = rng.uniform(.3, .9, B)
+    np.testing.assert_allclose(ctx.spatial_step(x, u, k, ds), x + ds[:, None] * fs, rtol=1e-14, atol=1e-14)
+    d = dyn_kat
+    xd, ud, kd = (np.ascontiguousarray(d[key]) for key in ("x", "u", "kappa"))
+    np.testing.assert_allclose(dyn_ctx.ode(xd, ud, kd), M.dyn_temporal_ode(xd, ud, kd, dyn_params),
+                               rtol=1e-12, atol=1e-9)
+    np.testing.assert_allclose(dyn_ctx.ode(xd, ud, kd, space=True), M.dyn_spatial_ode(xd, ud, kd, dyn_params),
+                               rtol=1e-12, atol=1e-9)
+
+
+def test_drop_in_f_alias():
+    """KinematicCar.f(x, u, curvature) (the north star's VehicleModel.f) is the temporal ODE:
+    transition(x, u, k, dt) = x + dt f(x, u, k) for the Euler kinematic car (kinematic_car.py:34-45)."""
+    from vcmpc.config import load_config
+    from vcmpc.models import KinematicCar
+
+    class _T:
+        def k(self, s):
+            return 0.02
+
+    car = KinematicCar(load_config("kinematic_car"), _T())
+    x = np.array([6.0, 0.1, 10.0, 0.5, 0.05, 1.0]); u = np.array([1.0, -0.2])
+    f = car.f(x, u, 0.02)
+    np.testing.assert_allclose(f, M.kin_temporal_ode(x[None], u[None], np.array([0.02]), L)[0], rtol=1e-13)
+    np.testing.assert_allclose(car.transition(x, u, 0.02, 0.05), x + 0.05 * f, rtol=1e-14)
+    np.testing.assert_allclose(car.f_spatial(x, u, 0.02), M.kin_spatial_ode(x[None], u[None], np.array([0.02]), L)[0],
+                               rtol=1e-13)
+
+
 def test_rollout_and_linearize_vs_golden(ctx, kin_golden):
     g = kin_golden
     xbar = ctx.rollout(g["x0"], g["ubar"], g["kappa"], g["ds"])

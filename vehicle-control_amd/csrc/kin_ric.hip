@@ -405,7 +405,7 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
     WSYNC();
     const double h00 = s.Hm[5][5], h01 = s.Hm[5][6], h11 = s.Hm[6][6];
     const double det = h00 * h11 - h01 * h01;
-    // IEEE-exact reciprocal (tests/test_gpu_numerics.py): the plain v_rcp_f64 + Newton form turns
+    // reciprocal bit-identical to IEEE 1/x on every class (asserted: tests/test_gpu_numerics.py): the plain v_rcp_f64 + Newton form turns
     // det = +inf (h00 h11 overflowing at barrier weights ~1e154) into NaN where 1/det = 0
 #ifdef VC_KIN_RIC_RAW_RCP  // diagnostic build only (scripts/: the round-2 inverse)
     double id = __builtin_amdgcn_rcp(det);
@@ -932,7 +932,8 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
     else if (solved) st = VC_SOLVED;
     else st = VC_MAX_ITER;
     A.status[b] = st;
-    A.iters[b] = it;
+    // the elastic-on-failure pass adds its iterations to the hard-row pass's (read before overwriting)
+    A.iters[b] = it + (A.qp.elastic < 0.0 ? A.iters[b] : 0);
     if (A.diag) {
       A.diag[(size_t)b * DS + 0] = last_res;
       A.diag[(size_t)b * DS + 1] = last_mu;

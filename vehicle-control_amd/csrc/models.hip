@@ -34,6 +34,29 @@ __device__ inline void spatial_step(const ModelArgs& m, const T* x, const T* u, 
   }
 }
 
+// the continuous vector field f(x, u, kappa): temporal (kinematic_car.py:34-40, dynamic_car.py:153-167)
+// or spatial (kinematic_car.py:47-60, dynamic_car.py:169-191) -- the `f` CasADi Function the
+// reference's integrators wrap (utils/integrators.py:18,29)
+template <typename T, int NX>
+__global__ void ode_kernel(ModelArgs m, const T* x, const T* u, const T* kappa, int space, T* fo) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= m.B) return;
+  T xl[NX], ul[2], f[NX];
+#pragma unroll
+  for (int i = 0; i < NX; ++i) xl[i] = x[(size_t)b * NX + i];
+  ul[0] = u[(size_t)b * 2];
+  ul[1] = u[(size_t)b * 2 + 1];
+  if (m.model == VC_MODEL_KINEMATIC) {
+    if (space) kin_spatial_ode(xl, ul, kappa[b], T(m.L), f);
+    else kin_temporal_ode(xl, ul, kappa[b], T(m.L), f);
+  } else {
+    if (space) dyn_spatial_ode(xl, ul, kappa[b], dyn_coef<T>(m), f);
+    else dyn_temporal_ode(xl, ul, kappa[b], dyn_coef<T>(m), f);
+  }
+#pragma unroll
+  for (int i = 0; i < NX; ++i) fo[(size_t)b * NX + i] = f[i];
+}
+
 template <typename T, int NX>
 __global__ void plant_step_kernel(ModelArgs m, const T* x, const T* u, const T* kappa, T dt, T* xn) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -157,6 +180,24 @@ hipError_t launch_rollout_t(const ModelArgs& m, const void* x0, const void* ubar
   return hipGetLastError();
 }
 
+template <typename T>
+hipError_t launch_ode_t(const ModelArgs& m, const void* x, const void* u, const void* kappa, int space, void* f,
+                        hipStream_t st) {
+  if (m.model == VC_MODEL_KINEMATIC)
+    hipLaunchKernelGGL((ode_kernel<T, KIN_NX>), grid1(m.B, 128), dim3(128), 0, st, m, (const T*)x, (const T*)u,
+                       (const T*)kappa, space, (T*)f);
+  else
+    hipLaunchKernelGGL((ode_kernel<T, DYN_NX>), grid1(m.B, 128), dim3(128), 0, st, m, (const T*)x, (const T*)u,
+                       (const T*)kappa, space, (T*)f);
+  return hipGetLastError();
+}
+
+hipError_t launch_ode(const ModelArgs& m, int dtype, const void* x, const void* u, const void* kappa, int space,
+                      void* f, hipStream_t st) {
+  if (m.B <= 0) return hipSuccess;
+  return dtype == VC_F32 ? launch_ode_t<float>(m, x, u, kappa, space, f, st)
+                         : launch_ode_t<double>(m, x, u, kappa, space, f, st);
+}
 hipError_t launch_plant_step(const ModelArgs& m, int dtype, const void* x, const void* u, const void* kappa, double dt,
                              void* xn, hipStream_t st) {
   if (m.B <= 0) return hipSuccess;

@@ -558,7 +558,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       const double h00 = s.u.q.f.Hm[7][7], h01 = s.u.q.f.Hm[7][8], h11 = s.u.q.f.Hm[8][8];
       const double det = h00 * h11 - h01 * h01;
       // 1 / det: v_rcp_f64 + two Newton steps (full fp64 accuracy, no IEEE divide sequence)
-      // IEEE-exact reciprocal (tests/test_gpu_numerics.py): the plain v_rcp_f64 + Newton form turns
+      // reciprocal bit-identical to IEEE 1/x on every class (asserted: tests/test_gpu_numerics.py): the plain v_rcp_f64 + Newton form turns
       // det = +inf (h00 h11 overflowing at barrier weights ~1e154) into NaN where 1/det = 0
       const double id = rcp_nr(det);
       const double i00 = h11 * id, i01 = -h01 * id, i11 = h00 * id;

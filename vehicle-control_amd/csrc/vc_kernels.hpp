@@ -273,6 +273,8 @@ bool casc_sqp_built(int N, int M);
 size_t dyn_sqp_smem_bytes(int N);
 int dyn_sqp_debug_stride();
 size_t kin_ltv_smem_bytes(int N);
+hipError_t launch_ode(const ModelArgs& m, int dtype, const void* x, const void* u, const void* kappa, int space,
+                      void* f, hipStream_t st);
 hipError_t launch_plant_step(const ModelArgs& m, int dtype, const void* x, const void* u, const void* kappa, double dt,
                              void* xn, hipStream_t st);
 hipError_t launch_spatial_step(const ModelArgs& m, int dtype, const void* x, const void* u, const void* kappa,

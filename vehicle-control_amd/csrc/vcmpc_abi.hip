@@ -133,7 +133,9 @@ vc::TrackTable track_table(const vc_ctx* c) {
 // barriers, condition numbers ~1e6) need the stagewise factorisation's accuracy (kin_ric.hip
 // matches the oracle to 1e-8 there, the condensed normal equations to 8e-5; scripts/kin_sqp_debug.py)
 bool kin_condensed(const vc_ctx* c) {
-  return vc::kin_ltv_smem_bytes(c->N) > 0 && c->p.qp.solver == 0 && c->p.qp.kin_sqp <= 0 && !c->p.qp.ms;
+  // elastic rows (qp.elastic) and multiple shooting are built in the stagewise kernel only
+  return vc::kin_ltv_smem_bytes(c->N) > 0 && c->p.qp.solver == 0 && c->p.qp.kin_sqp <= 0 && !c->p.qp.ms &&
+         c->p.qp.elastic == 0.0;
 }
 bool kin_solve_built(const vc_ctx* c) {
   return c->model == VC_MODEL_KINEMATIC && c->dtype == VC_F64 && (kin_condensed(c) || vc::kin_ric_built(c->N));
@@ -463,6 +465,8 @@ int vc_solve_diag(vc_ctx* c, int B, const void* x0, const void* kappa, const voi
   if (B == 0) return 0;
   if (c->model == VC_MODEL_DYNAMIC) return dyn_solve(c, B, x0, kappa, ds, xbar, ubar, u0, status, iters, diag, flags);
   if (c->model == VC_MODEL_CASCADED) return casc_solve(c, B, x0, kappa, ds, xbar, ubar, u0, status, iters, diag, flags);
+  if (c->p.qp.elastic < 0.0 && c->p.qp.kin_sqp <= 0)
+    return fail(c, VC_E_ARG, "vc_qp.elastic < 0 (elastic on failure) needs kin_sqp > 0; rho > 0 for one QP step");
   const int N = c->N, nx = 6, nu = 2;
   vc::KinLtvArgs a{};
   a.mode = 0;
@@ -508,7 +512,6 @@ int vc_solve_diag(vc_ctx* c, int B, const void* x0, const void* kappa, const voi
   a.x_in = a.x_out;  // multiple shooting (qp.ms): the warm-start states arrive in xbar
   const int S = c->p.qp.kin_sqp;
   if (S <= 0) {  // the LTV-QP contract: one QP step
-    if (a.qp.elastic < 0.0) a.qp.elastic = 0.0;  // elastic on failure is an SQP-step option
     if (kin_condensed(c)) VC_HIP(c, vc::launch_kin_ltv(a, N, c->stream));
     else VC_HIP(c, vc::launch_kin_ric(a, N, c->stream));
   } else {
@@ -726,6 +729,27 @@ int vc_plant_step(vc_ctx* c, int B, const void* x, const void* u, const void* ka
     return unstage(c, slots);
   }
   VC_HIP(c, vc::launch_plant_step(m, c->dtype, x, u, kappa, dt, x_next, c->stream));
+  return 0;
+}
+
+int vc_ode(vc_ctx* c, int B, const void* x, const void* u, const void* kappa, int space, void* f, int flags) {
+  if (int r = check_common(c, B, flags)) return r;
+  if (!x || !u || !kappa || !f) return fail(c, VC_E_ARG, "null pointer");
+  if (space != 0 && space != 1) return fail(c, VC_E_ARG, "vc_ode: space must be 0 (temporal) or 1 (spatial)");
+  if (B == 0) return 0;
+  const int nx = nx_of(c);
+  const size_t es = esize(c);
+  vc::ModelArgs m = model_args(c, B);
+  if (flags == VC_HOST_PTRS) {
+    std::vector<Slot> slots = {{x, nullptr, (size_t)B * nx * es, nullptr},
+                               {u, nullptr, (size_t)B * 2 * es, nullptr},
+                               {kappa, nullptr, (size_t)B * es, nullptr},
+                               {nullptr, f, (size_t)B * nx * es, nullptr}};
+    if (int r = stage(c, slots)) return r;
+    VC_HIP(c, vc::launch_ode(m, c->dtype, slots[0].dev, slots[1].dev, slots[2].dev, space, slots[3].dev, c->stream));
+    return unstage(c, slots);
+  }
+  VC_HIP(c, vc::launch_ode(m, c->dtype, x, u, kappa, space, f, c->stream));
   return 0;
 }
 

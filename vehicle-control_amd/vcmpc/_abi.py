@@ -12,7 +12,7 @@ import os
 
 LIB_NAME = "libvcmpc.so"
 LIB_PATH = os.environ.get("VCMPC_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME))
-ABI_VERSION = 9
+ABI_VERSION = 10
 VC_MAX_OBSTACLES = 16
 OBS_MARGIN_MIN = 0.05  # VC_OBS_MARGIN_MIN (csrc/vc_kernels.hpp)
 
@@ -105,6 +105,7 @@ PROTOTYPES = {
     "vc_condense": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int]),
     "vc_plant_step": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, C.c_double, _vp, C.c_int]),
     "vc_spatial_step": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, C.c_int]),
+    "vc_ode": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, C.c_int, _vp, C.c_int]),
     "vc_track_set": (C.c_int, [_vp, C.c_int, C.c_double, C.c_double, _vp]),
     "vc_track_k": (C.c_int, [_vp, C.c_int, _vp, _vp, C.c_int]),
     "vc_horizon": (C.c_int, [_vp, C.c_int, _vp, _vp, C.c_double, _vp, _vp, C.c_int]),

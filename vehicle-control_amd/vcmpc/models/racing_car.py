@@ -4,7 +4,12 @@
 the reference's CasADi-Function call signature but evaluate on the GPU through
 ``vc_plant_step`` / ``vc_spatial_step``; they accept one problem (``x[nx]``) or a
 batch (``x[B, nx]``, ``kappa[B]``) and return numpy arrays of the same shape.
-``f`` is the north star's ``VehicleModel.f(x, u)`` alias of ``transition``.
+``f(x, u, curvature)`` is the north star's ``VehicleModel.f(x, u)``: the continuous temporal
+vector field the reference's integrators wrap (``f = ca.Function("f", [state, action,
+curvature], [f])``, utils/integrators.py:18,29; kinematic_car.py:34-40, dynamic_car.py:153-167),
+evaluated by ``vc_ode``; ``f_spatial`` is the spatial one (kinematic_car.py:47-60,
+dynamic_car.py:169-191), so ``spatial_transition(x, u, k, ds) == x + ds * f_spatial(x, u, k)``
+for the (Euler) kinematic car.
 """
 from __future__ import annotations
 
@@ -73,9 +78,19 @@ class RacingCar(Robot):
     def spatial_transition(self):
         return self._spatial_transition
 
-    @property
-    def f(self):
-        return self._transition
+    def _ode(self, x, u, curvature, space=False):
+        nx = len(self.state)
+        single, xb, ub, kb, _ = self._batchify(x, u, curvature, 0.0, nx)
+        out = self._context().ode(xb, ub, kb, space=space)
+        return out[0] if single else out
+
+    def f(self, x, u, curvature=0.0):
+        """dx/dt = f(x, u, curvature) (utils/integrators.py:18; one problem or a batch)."""
+        return self._ode(x, u, curvature)
+
+    def f_spatial(self, x, u, curvature=0.0):
+        """dx/ds = f'(x, u, curvature), the MPC's spatial vector field (kinematic_car.py:47-60)."""
+        return self._ode(x, u, curvature, space=True)
 
     def drive(self, input):
         """Plant step at the track curvature -- racing_car.py:34-46."""

@@ -204,6 +204,16 @@ class Context:
         self._check(self.lib.vc_plant_step(self._h, B, px, pu, pk, float(dt), pxn, flags))
         return xn
 
+    def ode(self, x, u, kappa, space=False):
+        """``vc_ode``: the model's vector field f(x, u, kappa) (temporal, or spatial with
+        ``space=True``) for B points."""
+        B, nx, f = self._batch(x), self.nx, _NP_DT[self.dtype]
+        fo = self._like(x, (B, nx))
+        ptrs, flags = self._marshal([x, u, kappa, fo], [(B, nx), (B, NU), (B,), (B, nx)], [f] * 4)
+        p = ptrs
+        self._check(self.lib.vc_ode(self._h, B, p[0], p[1], p[2], int(bool(space)), p[3], flags))
+        return fo
+
     def spatial_step(self, x, u, kappa, ds):
         B, nx, f = self._batch(x), self.nx, _NP_DT[self.dtype]
         xn = self._like(x, (B, nx))

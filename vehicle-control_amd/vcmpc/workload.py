@@ -5,11 +5,12 @@ C2/C4 (kinematic LTV-MPC, N = 20, fp64), seeded ``numpy.random.default_rng``:
          epsi ~ U(-0.2, 0.2), t = 0
   kappa: piecewise constant over 4 segments, each ~ U(0, 0.047) (ippodromo's
          range of back-solved curvature)
-  ds:    mpc_dt * v0 + 0.5 for every stage (kinematic_mpc.py:178-182 with a
-         constant speed prediction)
   ubar:  U(-1, 1) * (3, 0.4) (the input boxes of kinematic.yaml)
-Problems whose warm-start rollout would leave the model's domain (v below 1 m/s,
-|epsi| above 1.2 rad, where v cos(epsi) -> 0 makes the spatial ODE singular) are
+  ds:    per stage, ds_n = mpc_dt * vbar_n + 0.5 (kinematic_mpc.py:178-182) with
+         vbar the speed prediction of the warm start: the rollout of ubar from x0 on the
+         provisional grid mpc_dt * v0 + 0.5
+Problems whose warm-start rollout (on the final grid) would leave the model's domain (v below
+1 m/s, |epsi| above 1.2 rad, where v cos(epsi) -> 0 makes the spatial ODE singular) are
 re-drawn, so every generated problem is well posed.
 """
 from __future__ import annotations
@@ -20,10 +21,12 @@ V_LO = 1.0
 EPSI_HI = 1.2
 
 
-def _kin_rollout(x0, ubar, kappa, ds, L):
-    """Host-side Euler rollout used only to screen samples (kinematic_car.py:47-64)."""
+def _kin_rollout(x0, ubar, kappa, ds, L, speeds=False):
+    """Host-side Euler rollout used only to screen samples (kinematic_car.py:47-64); with
+    ``speeds`` also the predicted speeds v[B, N+1]."""
     B, N = kappa.shape
     x = x0.copy()
+    v_traj = [x[:, 0].copy()]
     vmin = x[:, 0].copy()
     emax = np.abs(x[:, 4])
     for k in range(N):
@@ -34,10 +37,11 @@ def _kin_rollout(x0, ubar, kappa, ds, L):
         f = np.stack([q * ubar[:, k, 0], q * ubar[:, k, 1], np.ones(B), rho * np.tan(ep),
                       np.tan(d) / L * rho / c - kappa[:, k], q], 1)
         x = x + ds[:, k:k + 1] * f
+        v_traj.append(x[:, 0].copy())
         vmin = np.minimum(vmin, x[:, 0])
         emax = np.maximum(emax, np.abs(x[:, 4]))
     ok = np.isfinite(x).all(1) & (vmin > V_LO) & (emax < EPSI_HI)
-    return ok
+    return (ok, np.stack(v_traj, 1)) if speeds else ok
 
 
 def kinematic_batch(B: int, N: int = 20, seed: int = 31, mpc_dt: float = 0.03, L: float = 2.5,
@@ -56,9 +60,12 @@ def kinematic_batch(B: int, N: int = 20, seed: int = 31, mpc_dt: float = 0.03, L
         x0[:, 4] = rng.uniform(-0.2, 0.2, m)
         seg = rng.uniform(0, 0.047, (m, 4))
         kappa = np.repeat(seg, -(-N // 4), axis=1)[:, :N]
-        ds = np.repeat(mpc_dt * x0[:, :1] + 0.5, N, axis=1)
         ubar = rng.uniform(-1, 1, (m, N, 2)) * np.array([a_max, w_max])
-        ok = _kin_rollout(x0, ubar, kappa, ds, L)
+        ds_c = np.repeat(mpc_dt * x0[:, :1] + 0.5, N, axis=1)
+        with np.errstate(all="ignore"):
+            _, v_pred = _kin_rollout(x0, ubar, kappa, ds_c, L, speeds=True)
+            ds = mpc_dt * v_pred[:, :N] + 0.5             # kinematic_mpc.py:178-182
+            ok = _kin_rollout(x0, ubar, kappa, ds, L) & np.isfinite(ds).all(1)
         for k, v in (("x0", x0), ("kappa", kappa), ("ds", ds), ("ubar", ubar)):
             out[k].append(v[ok])
         have += int(ok.sum())
