@@ -13,7 +13,9 @@ because IPOPT solves the NLP with the exact barrier.  The build's globalised ste
         alpha = the first of 1, 1/2, ..., 2^-(LS_STEPS-1) with
                 phi(ubar + alpha dz) <= phi(ubar) + ARMIJO * alpha * D,
                 D = (phi(ubar + EPS_FD dz) - phi(ubar)) / EPS_FD  (one-sided derivative),
-                and no step at all (alpha = 0) if none qualifies or D >= 0
+                and no step at all (alpha = 0) if none qualifies or D >= 0 -- unless |D| is at
+                its own rounding level and the full step does not raise phi (noise_step: the
+                flat directions near a KKT point)
         ubar += alpha dz
 
 phi is the exact NLP cost of the QP contract (the same terms, each `if_else` evaluated on
@@ -51,11 +53,13 @@ import numpy as np
 from . import ltv_qp as Q
 from . import models as M
 
-LS_STEPS = 8        # alpha = 1 .. 2^-7
+LS_STEPS = 24       # alpha = 1 .. 2^-23 (one lane each in kin_merit.hip)
 ARMIJO = 1e-4
 EPS_FD = 1e-7
 RHO = 1e3           # L1 penalty on the state rows (above every multiplier seen in the contract's QPs)
 RHO_DEF = 1e3       # L1 penalty on the multiple-shooting defects
+NOISE_D = 8.0 * 2.220446049250313e-16 / 1e-7   # rounding level of the one-sided difference D (x max(1, |phi|))
+NOISE_PHI = 1e-13   # a noise-level step may not raise phi by more than this (x max(1, |phi|))
 TIE = 1e-9          # the rollout is preferred unless the state iterate's merit is lower by more
 IV, ID, IS, IEY, IEP, IT = Q.IV, Q.ID, Q.IS, Q.IEY, Q.IEP, Q.IT
 IA, IW = Q.IA, Q.IW
@@ -129,14 +133,29 @@ def line_search(x0, ubar, dz, kappa, ds, L, W):
     phia = phi0.copy()
     done = D >= 0.0
     a = 1.0
+    p1 = None
     for _ in range(LS_STEPS):
         pa = merit(x0, ubar + a * dz, kappa, ds, L, W)
         ok = ~done & (pa <= phi0 + ARMIJO * a * D)
+        p1 = pa if p1 is None else p1
         alpha[ok] = a
         phia[ok] = pa[ok]
         done |= ok
         a *= 0.5
+    nz = noise_step(alpha, phi0, p1, D)
+    alpha[nz] = 1.0
+    phia[nz] = p1[nz]
     return alpha, phi0, phia, D
+
+
+def noise_step(alpha, phi0, p1, D):
+    """Where no step size passed the Armijo test and |D| is at the rounding level of its own
+    one-sided difference, the full step is taken if it does not raise phi beyond rounding:
+    near a solution the decrease a QP step promises (~|dz|^2 times the curvature of flat
+    directions such as the last acceleration, whose only cost is the 1e-4 slew) is below what
+    the merit can resolve, and the SQP would otherwise stop short of the KKT point."""
+    sc = np.maximum(1.0, np.abs(phi0))
+    return (alpha == 0.0) & (np.abs(D) <= NOISE_D * sc) & (p1 <= phi0 + NOISE_PHI * sc)
 
 
 def line_search_ms(x0, ubar, dz, x, dx, kappa, ds, L, W):
@@ -159,15 +178,21 @@ def line_search_ms(x0, ubar, dz, x, dx, kappa, ds, L, W):
     pr, pa_m = ps0.copy(), pm0.copy()
     done = D >= 0.0
     a = 1.0
+    first = None
     for _ in range(LS_STEPS):
         vs, vm = ps(a), pm(a)
         pa = sel(vs, vm)
+        first = (pa, vs, vm) if first is None else first
         ok = ~done & (pa <= phi0 + ARMIJO * a * D)
         alpha[ok] = a
         phia[ok] = pa[ok]
         pr[ok], pa_m[ok] = vs[ok], vm[ok]
         done |= ok
         a *= 0.5
+    nz = noise_step(alpha, phi0, first[0], D)
+    alpha[nz] = 1.0
+    phia[nz] = first[0][nz]
+    pr[nz], pa_m[nz] = first[1][nz], first[2][nz]
     reset = np.isfinite(pr) & (pr <= pa_m + TIE * np.abs(pa_m))
     return alpha, phi0, phia, D, reset
 

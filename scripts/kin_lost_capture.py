@@ -78,6 +78,9 @@ def main():
             prev = nf
             X[k + 1] = sim.states
             UOUT[k] = np.array(sim.ubar, copy=True)
+            if k % 50 == 49:
+                print(f"  seed {seed} step {k + 1}: non-solved so far {int(FAIL.sum())} ({time.time() - t0:.1f} s)",
+                      flush=True)
         ey = np.abs(X[:, :, 3])
         keep = np.nonzero(FAIL.any(axis=0) | (ey.max(axis=0) > tr.width / 2 + 0.5))[0]
         print(f"seed {seed}: non-solved {int(FAIL.sum())} of {B * K}, max |ey| {ey.max():.2f}, "

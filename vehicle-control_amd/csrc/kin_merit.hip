@@ -7,10 +7,12 @@
 // Contract and operation order: oracle/kin_sqp.py (merit, line_search).
 //
 // Lanes 0..LS-1 evaluate phi(u_prev + 2^-j dz), lane LS phi(u_prev + EPS dz) (the one-sided
-// directional derivative), lane LS+1 phi(u_prev); each lane rolls its candidate out with the
+// directional derivative), lane LS+1 phi(u_prev) -- 26 of the wave's 64 lanes, so the 24 step
+// sizes cost one evaluation's latency; each lane rolls its candidate out with the
 // spatial Euler model (kinematic_car.py:47-64) and sums the cost terms stage by stage -- a few
 // thousand flops per lane, negligible next to the QP.  Lane 0 picks the first candidate with
-// sufficient decrease (none, or a failed QP: alpha = 0), then the wavefront writes the
+// sufficient decrease (none, or a failed QP: alpha = 0; the full step when the decrease is at the
+// merit's rounding level and phi does not rise, noise_step), then the wavefront writes the
 // accepted inputs, lane 0 their rollout x* and u0, and the solve status / iteration count
 // accumulate over the SQP iterations (status: the first QP's -- a later QP's failure only
 // refuses its step; iterations: summed).  A first QP without a solution restarts the iterate
@@ -29,11 +31,15 @@
 namespace vc {
 namespace {
 
-constexpr int LS = 8;            // alpha = 1 .. 2^-7  (oracle/kin_sqp.py LS_STEPS)
+constexpr int LS = 24;           // alpha = 1 .. 2^-23  (oracle/kin_sqp.py LS_STEPS)
 constexpr double ARMIJO = 1e-4;  // sufficient-decrease constant
 constexpr double EPS_FD = 1e-7;  // directional-derivative step
 constexpr double RHO = 1e3;      // L1 penalty on the state rows
 constexpr double RHO_DEF = 1e3;  // L1 penalty on the multiple-shooting defects
+// noise-level steps (oracle/kin_sqp.py noise_step): |D| at its own rounding level, full step
+// taken when it raises phi by no more than NOISE_PHI (both x max(1, |phi0|))
+constexpr double NOISE_D = 8.0 * 2.220446049250313e-16 / 1e-7;
+constexpr double NOISE_PHI = 1e-13;
 constexpr double TIE = 1e-9;     // the rollout wins unless the state iterate's merit is lower by more
 constexpr int32_t RESTART_PENDING = -1;  // st_acc: the iterate restarted, the next QP's status is the step's
 
@@ -141,7 +147,11 @@ __global__ __launch_bounds__(64) void kin_merit_kernel(KinMeritArgs A) {
   // lane 0..LS-1: sufficient decrease?  the first such lane (largest alpha) wins
   const bool good = l < LS && qp_ok && D < 0.0 && isfinite(phi) && phi <= phi0 + ARMIJO * alpha * D;
   const uint64_t mask = __ballot(good);
-  const int pick = mask ? __builtin_ctzll(mask) : -1;
+  const double sc = fmax(1.0, fabs(phi0));
+  const double p1 = bcast(phi, 0);
+  // no Armijo step: near a KKT point the promised decrease is below the merit's resolution
+  const bool noise = !mask && qp_ok && fabs(D) <= NOISE_D * sc && p1 <= phi0 + NOISE_PHI * sc;
+  const int pick = mask ? __builtin_ctzll(mask) : (noise ? 0 : -1);
   const double al = pick >= 0 ? ldexp(1.0, -pick) : 0.0;
   const double phia = pick >= 0 ? bcast(phi, pick) : phi0;
   const double* up = A.u_prev + (size_t)b * N * 2;
