@@ -22,11 +22,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "vehicle-control_amd")]
 
 
+def track_of(run):
+    """The recorded run's track: the experiment directory's suffix (<name>_<track>[:<ctl>])."""
+    return run.split(":")[0].rsplit("_", 1)[1]
+
+
 def config_for(run, rec):
-    """The build's config (its `qp` block) with the recorded run's horizons, weights and bounds."""
+    """The build's config (its `qp` block) with the recorded run's horizons, weights, bounds and
+    obstacle switch (the barrier then uses the run's track's obstacle_data, cascaded_mpc.py:173-176)."""
     from vcmpc.config import load_config
     cfg = copy.deepcopy(load_config("cascaded_mpc" if rec.get("horizon_pm", 0) else "singletrack_mpc"))
-    for k in ("horizon", "mpc_dt", "horizon_pm", "ds_pm"):
+    for k in ("horizon", "mpc_dt", "horizon_pm", "ds_pm", "obstacles"):
         if k in rec:
             cfg[k] = rec[k]
     for k in ("cost_weights", "input_constraints", "state_constraints", "state_pm_constraints"):
@@ -35,47 +41,59 @@ def config_for(run, rec):
     return cfg
 
 
-def replay(run, g, rec, sqp, skip=5, qp=None, dump=None):
+def replay(run, g, rec, sqp, skip=5, qp=None, dump=None, segments=1):
+    """segments > 1: the run's T steps are cut into that many contiguous windows, replayed side
+    by side as one batch (each window starts from the controller's own initial guess, so its
+    first `skip` steps are the warm-up and are not compared) -- the same per-step comparison
+    in T / segments sequential solves."""
     from vcmpc.config import load_config
     from vcmpc.controllers.cascaded_mpc import BatchedCascadedMPC, BatchedSingleTrackMPC
     from vcmpc.environment import Track
     from vcmpc.models import DynamicCar
-    track = Track.load("ippodromo")
+    track = Track.load(track_of(run))
     car = DynamicCar(load_config("dynamic_car"), track, tyre="fiala")
     cfg = config_for(run, rec)
     cfg["qp"] = dict(cfg["qp"], sqp_iters=sqp, **(qp or {}))
     X, U, P = g[f"{run}/state_traj"], g[f"{run}/action_traj"], g[f"{run}/preds"]
-    ctl = (BatchedCascadedMPC if cfg.get("horizon_pm", 0) else BatchedSingleTrackMPC)(car, cfg, batch=1)
-    N = int(cfg["horizon"])
     T = min(len(X), len(U))
-    du, dplan, nfail, us, dbg = [], [], 0, [], None
+    K = max(1, min(int(segments), T // (4 * skip + 1)))
+    bounds = np.linspace(0, T, K + 1).astype(int)
+    ctl = (BatchedCascadedMPC if cfg.get("horizon_pm", 0) else BatchedSingleTrackMPC)(car, cfg, batch=K)
+    N = int(cfg["horizon"])
+    du, dplan, rel_u, nfail, dbg = [], [], [], 0, None
+    us = np.full((T, 2), np.nan)
     rec_nan = own_nan = 0
-    for n in range(T):
-        u = ctl.command(X[n][None])[0]
-        us.append(u)
-        nfail += int(ctl.status[0] != 0)
-        if n < skip:
-            continue
-        if n + 1 < len(U):   # racing.py:230-241: action_traj[n + 1] is the command at state_traj[n]
-            du.append(u - U[n + 1])
-        if n < len(P):
-            sp = ctl.state_prediction[0]
-            xy = np.array([track.rel2glob(sp[4, i], sp[5, i], sp[6, i])[:2] for i in range(min(N, 20))])
-            # the recorded plans hold NaN past the reference track's spline range (its k / x / y
-            # do not wrap; e.g. cascaded7 step 406, stages >= 17): compare on the recorded stages
-            # that exist, and count our own non-finite plans separately
-            rec_ok = np.isfinite(P[n, :len(xy)]).all(axis=1)
-            rec_nan += int(not rec_ok.all())
-            own_nan += int(not np.isfinite(xy).all())
-            dplan.append(np.hypot(*(xy[rec_ok] - P[n, :len(xy)][rec_ok]).T).max())
-            if dbg is None and n == 50:
-                dbg = dict(ours=xy[:3].tolist(), recorded=P[n, :3].tolist())
+    for j in range(int(np.max(np.diff(bounds)))):
+        idx = np.minimum(bounds[:-1] + j, bounds[1:] - 1)          # a finished window repeats its last row
+        live = bounds[:-1] + j < bounds[1:]
+        u = ctl.command(X[idx])
+        for k in np.nonzero(live)[0]:
+            n = int(idx[k])
+            us[n] = u[k]
+            nfail += int(ctl.status[k] != 0)
+            if j < skip:
+                continue
+            if n + 1 < len(U):   # racing.py:230-241: action_traj[n + 1] is the command at state_traj[n]
+                du.append(u[k] - U[n + 1])
+                rel_u.append(U[n + 1])
+            if n < len(P):
+                sp = ctl.state_prediction[k]
+                xy = np.array([track.rel2glob(sp[4, i], sp[5, i], sp[6, i])[:2] for i in range(min(N, 20))])
+                # the recorded plans hold NaN past the reference track's spline range (its k / x / y
+                # do not wrap; e.g. cascaded7 step 406, stages >= 17): compare on the recorded stages
+                # that exist, and count our own non-finite plans separately
+                rec_ok = np.isfinite(P[n, :len(xy)]).all(axis=1)
+                rec_nan += int(not rec_ok.all())
+                own_nan += int(not np.isfinite(xy).all())
+                dplan.append(np.hypot(*(xy[rec_ok] - P[n, :len(xy)][rec_ok]).T).max())
+                if dbg is None and n >= 50:
+                    dbg = dict(step=n, ours=xy[:3].tolist(), recorded=P[n, :3].tolist())
     du, dplan = np.abs(np.array(du)), np.array(dplan)
-    us = np.array(us)
     if dump:   # per-step arrays for a closer look (our u0, the recorded command, the state)
-        np.savez(dump, u=us, U=U, X=X, du=du, dplan=dplan, skip=skip)
-    rel = du / np.maximum(np.abs(U[skip + 1:skip + 1 + len(du)]), [100.0, 0.01])
-    return dict(run=run, sqp=sqp, qp=cfg["qp"], steps=T - skip, nonsolved=nfail,
+        np.savez(dump, u=us, U=U, X=X, du=du, dplan=dplan, skip=skip, bounds=bounds)
+    rel = du / np.maximum(np.abs(np.array(rel_u)), [100.0, 0.01])
+    return dict(run=run, sqp=sqp, qp=cfg["qp"], steps=len(du), segments=K, nonsolved=nfail,
+                obstacles=bool(cfg.get("obstacles")), track=track_of(run),
                 dFx_median=float(np.median(du[:, 0])), dFx_p90=float(np.percentile(du[:, 0], 90)),
                 dFx_max=float(du[:, 0].max()), dw_median=float(np.median(du[:, 1])),
                 dw_p90=float(np.percentile(du[:, 1], 90)), dw_max=float(du[:, 1].max()),
@@ -88,19 +106,22 @@ def replay(run, g, rec, sqp, skip=5, qp=None, dump=None):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sqp", type=int, nargs="+", default=[3, 5, 10, 20])
-    ap.add_argument("--runs", nargs="+", default=["cascaded7_ippodromo", "singletrack_ippodromo"])
+    ap.add_argument("--runs", nargs="+", default=["cascaded7_ippodromo", "singletrack_ippodromo"],
+                    help="fixture keys (tests/golden/make_replay_kat.py), or 'all'")
     ap.add_argument("--out", default=None)
     ap.add_argument("--prox", type=float, nargs="+", default=[None], help="override qp.prox (sweep)")
     ap.add_argument("--dump", default=None, help="npz prefix for per-step arrays")
+    ap.add_argument("--segments", type=int, default=1, help="replay windows side by side (see replay())")
     args = ap.parse_args()
     g = dict(np.load(os.path.join(ROOT, "tests", "golden", "replay_kat.npz"), allow_pickle=False))
     recs = json.loads(str(g["configs"]))
     res = []
-    for run in args.runs:
+    for run in (sorted(recs) if args.runs == ["all"] else args.runs):
         for prox in args.prox:
             for sqp in args.sqp:
                 r = replay(run, g, recs[run], sqp, qp=None if prox is None else {"prox": prox},
-                           dump=None if args.dump is None else f"{args.dump}_{run}_p{prox}_s{sqp}.npz")
+                           dump=None if args.dump is None else f"{args.dump}_{run}_p{prox}_s{sqp}.npz",
+                           segments=args.segments)
                 res.append(r)
                 print(json.dumps({k: v for k, v in r.items() if k != "example_plan"}), flush=True)
     if args.out:
