@@ -70,3 +70,37 @@ def test_cascaded_replay_converges_to_ipopt(data):
     assert r40["dw_median"] < 1e-4          # measured 4.3e-5
     assert r40["frac_within_1pct"] > 0.5    # measured 0.53
     assert r40["plan_dev_median_m"] < 1e-3  # measured 2.7e-4 m
+
+
+# Round 4: every recorded run with the obstacle barrier on, and the shoe-track runs (fixture keys
+# "<dir>:<controller>", tests/golden/make_replay_kat.py; the three giant-obstacle runs are not
+# replayable: their obstacle set was never recorded).  Converged setting (prox 0.01, 40 SQP
+# iterations), the run cut into windows replayed side by side (scripts/replay_recorded.py
+# replay(segments=)): each window starts from the controller's own initial guess and its first 5
+# steps are not compared.  Bars, stated before the first measurement (from the two ippodromo
+# runs above): single-track -- at most 1 % of the steps non-solved, median |dFx| < 1 N, median
+# |dw| < 1e-4 rad/s, > 60 % of the steps within 1 %, median plan deviation < 0.01 m; cascaded
+# (the slower-converging tail) -- at most 1 % non-solved, median |dFx| < 20 N, median |dw| < 1e-3,
+# > 25 % within 1 %, median plan deviation < 0.05 m.  Every plan finite.
+REPLAY_R4 = ["singletrack_obstacles_shoe:singletrack", "race_obstacles_shoe:singletrack", "singletrack_shoe:singletrack",
+             "race1_shoe:singletrack", "race2_shoe:singletrack",
+             "cascaded_obstacles1_ippodromo:cascaded", "cascaded_obstacles2_ippodromo:cascaded",
+             "cascaded_obstacles_shoe:cascaded", "race_obstacles_shoe:cascaded", "race1_shoe:cascaded",
+             "race2_shoe:cascaded"]
+
+
+@pytest.mark.parametrize("run", REPLAY_R4)
+def test_replay_obstacle_and_shoe_runs(data, run):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(GOLDEN), "..", "scripts"))
+    from replay_recorded import replay
+    recs = json.loads(str(data["configs"]))
+    r = replay(run, data, recs[run], 40, qp={"prox": 0.01}, segments=24)
+    print(json.dumps({k: v for k, v in r.items() if k != "example_plan"}))
+    casc = run.endswith(":cascaded")
+    assert r["plan_nan_steps"] == 0
+    assert r["nonsolved"] <= 0.01 * r["steps"]
+    assert r["dFx_median"] < (20.0 if casc else 1.0)
+    assert r["dw_median"] < (1e-3 if casc else 1e-4)
+    assert r["frac_within_1pct"] > (0.25 if casc else 0.6)
+    assert r["plan_dev_median_m"] < (0.05 if casc else 0.01)
