@@ -118,3 +118,63 @@ def test_cascaded_lap_within_recorded_bands(M, vmax):
     assert np.abs(Ul[:, 1]).max() <= 0.4 + 1e-9
     assert stats["ey_absmax"] < max(track.width / 2, 1.1 * rec["ey_absmax"])
     assert stats["nfail"] <= 1
+
+
+# Round 4: the recorded obstacle runs and shoe-track runs (closed_loop_bands.json "runs_r4",
+# make_st_bands.py), each driven from its recorded x0 with its own controller config on its own
+# track, obstacles as recorded.  Bars, stated before the first measurement: a completed recorded
+# lap -> our lap within 4 % of its steps (3 % above was measured on ippodromo only); a race car
+# the simulator stopped early (the other car finished) -> s after the same number of steps within
+# 3 %; median Ux within 0.5 m/s; |ey| inside the track or within 10 % of the recorded max; at most
+# max(1, 0.5 % of the steps) non-solved; and wherever the recorded run kept clear of every obstacle
+# (clearance > 0), so does ours.  (race_obstacles_shoe's two recorded cars pass 1.48 m inside an
+# obstacle -- the reference's barrier w ds / (dist - r - 0.1) turns negative inside and rewards
+# staying there -- so no clearance bar applies to that run.)
+def _runs_r4():
+    with open(os.path.join(GOLDEN, "closed_loop_bands.json")) as f:
+        return {r["key"]: r for r in json.load(f)["runs_r4"]}
+
+
+RUNS_R4 = _runs_r4()
+
+
+@pytest.mark.parametrize("key", sorted(RUNS_R4))
+def test_recorded_obstacle_and_shoe_runs_within_bands(key):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(GOLDEN), "..", "scripts"))
+    from replay_recorded import config_for
+    from vcmpc.config import load_config
+    from vcmpc.environment import Track
+    from vcmpc.models import DynamicCar
+    from vcmpc.simulation import BatchedRacingSimulator
+    rec = RUNS_R4[key]
+    track = Track.load(rec["track"])
+    cfg = config_for(key, rec["config"])
+    if cfg.get("horizon_pm", 0):
+        cfg["qp"] = dict(cfg["qp"], sqp_iters=5)
+    car = DynamicCar(load_config("dynamic_car"), track, tyre="fiala")
+    sim = BatchedRacingSimulator(car, cfg, track, batch=1)
+    K = int(rec["steps"] * 1.08) if rec["complete"] else rec["steps"]
+    out = sim.reset(np.array([rec["x0"]])).run(K)
+    X, U = out["state_traj"][:, 0], out["action_traj"][:, 0]
+    assert np.isfinite(X).all()
+    done = np.nonzero(X[:, 4] > track.length - 0.1)[0]
+    n = int(done[0]) if len(done) else K
+    Xl = X[:n]
+    clear = None
+    if rec["obstacles"]:
+        clear = float(min(np.hypot(Xl[:, 4] - o.s, Xl[:, 5] - o.ey).min() - o.radius for o in track.obstacles))
+    stats = dict(steps=n, s_end=float(X[min(rec["steps"], len(X) - 1), 4]), Ux_median=float(np.median(Xl[:, 0])),
+                 ey_absmax=float(np.abs(Xl[:, 5]).max()), nfail=int(out["nfail"].sum()), clearance=clear)
+    print(f"{key}: build {stats} | recorded steps={rec['steps']} complete={rec['complete']} s_end={rec['s_end']:.1f} "
+          f"Ux_median={rec['Ux_median']:.2f} |ey|max={rec['ey_absmax']:.2f} clearance={rec['clearance_min']}")
+    if rec["complete"]:
+        assert len(done), f"no lap in {K} steps: s = {X[-1, 4]:.1f} of {track.length:.1f}"
+        assert abs(n - rec["lap_steps"]) <= 0.04 * rec["lap_steps"], (n, rec["lap_steps"])
+    else:
+        assert abs(stats["s_end"] - rec["s_end"]) <= 0.03 * rec["s_end"], (stats["s_end"], rec["s_end"])
+    assert abs(stats["Ux_median"] - rec["Ux_median"]) <= 0.5
+    assert stats["ey_absmax"] < max(track.width / 2, 1.1 * rec["ey_absmax"])
+    assert stats["nfail"] <= max(1, 0.005 * n)
+    if rec["obstacles"] and rec["clearance_min"] > 0:
+        assert clear > 0
