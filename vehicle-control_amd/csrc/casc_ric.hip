@@ -57,16 +57,36 @@ __host__ __device__ constexpr int qslot(int i, int j) {
   if (i == 3 && j == 8) return Q38;
   return -1;
 }
+// Swizzled lane-per-stage arrays (round 4): lane k reads row k of trow[.][8] and st[.][42] at a
+// fixed column, and those even strides put lanes k and k + 4 (trow: 8-way over a 32-lane
+// ds_read_b64 group) or k and k + 16 (st: 2-way) on the same banks.  Instead of padding (no LDS to
+// spare at N = 60) each row is permuted: trow column a of row k sits in slot (a + k / 4) mod 8,
+// st element e = 6 r + j of row k in slot e ^ (k / 16 mod 2) -- every lane of a group then reads
+// a distinct bank pair, and the layout stays a permutation within each row.
+__device__ __forceinline__ int tsw(int k, int a) { return (a + (k >> 2)) & 7; }
+__device__ __forceinline__ int stx(int k, int r, int j) { return (6 * r + j) ^ ((k >> 4) & 1); }
 // stage vector index -> column of [A6 | B6] (-1 for p: no dynamics enters through it)
 __host__ __device__ constexpr int vcol(int i) { return i < 6 ? i : (i == 6 ? -1 : i - 1); }
 
+// Strides (round 4): a lane-per-stage phase reads row k of xs / ub / J in lane k; an even stride
+// of 8 doubles put lanes k and k + 4 on the same banks (ds_read_b64: bank (a/4) mod 64 over 32
+// lanes -> 8-way on xs, 16-way on J's 48-double stages, 2-way on ub), so every such array has an
+// odd stride (9, 3, 49): the 32 lanes of a ds_read_b64 group then hit 32 distinct bank pairs and
+// the 16 of a ds_write_b64 / ds_read2_b64 group 16 ((a/4) mod 32).  +180 doubles: M = 40 stays at
+// three one-wave workgroups per CU.
+struct CrJ {  // [A6 | B6 diag(S, 1 or S)] of one transition + 1 pad (49 doubles)
+  double m[6][8];
+  double pad;
+  __device__ __forceinline__ double* operator[](int r) { return m[r]; }
+  __device__ __forceinline__ const double* operator[](int r) const { return m[r]; }
+};
 template <int N, int M>
 struct CrSmem {
   static constexpr int H = N + M;
-  double xs[H][8];    // prediction: single-track states k < N, point-mass (V, s, ey, epsi, t) k >= N
-  double ub[H][2];    // current ubar
+  double xs[H][9];    // prediction: single-track states k < N, point-mass (V, s, ey, epsi, t) k >= N; [8] pad
+  double ub[H][3];    // current ubar; [2] pad
   double kap[H], dsv[H];
-  double J[H][6][8];  // [A6 | B6 diag(S, 1 or S)] of the transition out of stage k
+  CrJ J[H];           // J[k][row][col]: [A6 | B6 diag(S, 1 or S)] of the transition out of stage k
   union {
     struct {
       double Qt[H][NQ];  // stage Hessian + barrier, this iteration
@@ -92,7 +112,7 @@ struct CrSmem {
     } q;
     struct {
       double trow[H][8];     // t-row of the transition out of stage k over (y | u)
-      double st[N][7][6];    // single-track stage functions: value + gradient over (Ux, Uy, r, delta, Fx)
+      double st[N][42];    // single-track stage functions: value + gradient over (Ux, Uy, r, delta, Fx)
       double gfy[6];         // Fy_f + Fy_r at stage N-1: value + gradient over (Ux, Uy, r, delta, Fx)
     } l;
   } u;
@@ -335,7 +355,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
           const int yr[6] = {0, 1, 2, 3, 5, 6};
 #pragma unroll
           for (int r = 0; r < 6; ++r) s.J[kk][r][col] = xn[yr[r]].d[0] * s0;
-          s.u.l.trow[kk][col] = xn[7].d[0] * s0;
+          s.u.l.trow[kk][tsw(kk, col)] = xn[7].d[0] * s0;
         }
       }
 #pragma unroll 1
@@ -351,8 +371,8 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
           dyn_stage_terms_alg<D1, double>(X5, c, o);
 #pragma unroll
           for (int r = 0; r < 7; ++r) {
-            s.u.l.st[kk][r][1 + j] = o[r].d[0];
-            if (j == 0) s.u.l.st[kk][r][0] = o[r].v;
+            s.u.l.st[kk][stx(kk, r, 1 + j)] = o[r].d[0];
+            if (j == 0) s.u.l.st[kk][stx(kk, r, 0)] = o[r].v;
           }
         }
       }
@@ -383,16 +403,16 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
               s.J[j][r][0] = (r == 0 ? 1.0 : 0.0) + h * f[yi[r]].d[0];
               s.J[j][r][1] = (r == 1 ? 1.0 : 0.0) + h * f[yi[r]].d[1];
             }
-            s.u.l.trow[j][0] = h * f[4].d[0];
-            s.u.l.trow[j][1] = h * f[4].d[1];
+            s.u.l.trow[j][tsw(j, 0)] = h * f[4].d[0];
+            s.u.l.trow[j][tsw(j, 1)] = h * f[4].d[1];
           } else if (pr == 1) {
 #pragma unroll
             for (int r = 0; r < 3; ++r) s.J[j][r][2] = (r == 2 ? 1.0 : 0.0) + h * f[yi[r]].d[0];
-            s.u.l.trow[j][2] = h * f[4].d[0];
+            s.u.l.trow[j][tsw(j, 2)] = h * f[4].d[0];
 #pragma unroll
             for (int cc = 3; cc < 6; ++cc) {
               s.J[j][0][cc] = s.J[j][1][cc] = s.J[j][2][cc] = 0.0;
-              s.u.l.trow[j][cc] = 0.0;
+              s.u.l.trow[j][tsw(j, cc)] = 0.0;
             }
 #pragma unroll
             for (int r = 3; r < 6; ++r)
@@ -404,8 +424,8 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
               s.J[j][r][6] = h * f[yi[r]].d[0] * S;
               s.J[j][r][7] = h * f[yi[r]].d[1] * S;
             }
-            s.u.l.trow[j][6] = h * f[4].d[0] * S;
-            s.u.l.trow[j][7] = h * f[4].d[1] * S;
+            s.u.l.trow[j][tsw(j, 6)] = h * f[4].d[0] * S;
+            s.u.l.trow[j][tsw(j, 7)] = h * f[4].d[1] * S;
           }
         }
       }
@@ -441,7 +461,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       s.J[N - 1][2][1] = Ux / q2;
       s.J[N - 1][2][5] = 1.0;
 #pragma unroll
-      for (int cc = 0; cc < 8; ++cc) s.u.l.trow[N - 1][cc] = 0.0;
+      for (int cc = 0; cc < 8; ++cc) s.u.l.trow[N - 1][tsw(N - 1, cc)] = 0.0;
     }
     WSYNC();
     // the switch's c row: the lateral-force gradient over (Ux, Uy, r, delta | dFx / S)
@@ -489,10 +509,10 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
         // slip-angle penalties when active at the prediction (:155-165)
 #pragma unroll
         for (int sr = 0; sr < 2; ++sr) {
-          const double fv = s.u.l.st[k][sr][0];
+          const double fv = s.u.l.st[k][stx(k, sr, 0)];
           const double wsl = fv >= 0.0 ? 2.0 * W.w_slip : 0.0;
-          const double a5[5] = {s.u.l.st[k][sr][1], s.u.l.st[k][sr][2], s.u.l.st[k][sr][3], s.u.l.st[k][sr][4],
-                                s.u.l.st[k][sr][5] * S};
+          const double a5[5] = {s.u.l.st[k][stx(k, sr, 1)], s.u.l.st[k][stx(k, sr, 2)], s.u.l.st[k][stx(k, sr, 3)], s.u.l.st[k][stx(k, sr, 4)],
+                                s.u.l.st[k][stx(k, sr, 5)] * S};
           constexpr int ix[5] = {0, 1, 2, 3, 7};
 #pragma unroll
           for (int a = 0; a < 5; ++a) {
@@ -535,7 +555,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       if (k < H - 1) {
         constexpr int iy[8] = {0, 1, 2, 3, 4, 5, 7, 8};
 #pragma unroll
-        for (int a = 0; a < 8; ++a) qc[iy[a]] += W.w_time * s.u.l.trow[k][a];
+        for (int a = 0; a < 8; ++a) qc[iy[a]] += W.w_time * s.u.l.trow[k][tsw(k, a)];
       }
       // terminal on the last point-mass state (:279-304)
       if (k == H - 1) {
@@ -565,9 +585,9 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
         for (int r = 0; r < 5; ++r) {
           const int fn = 2 + r;
 #pragma unroll
-          for (int a = 0; a < 4; ++a) R.c[r][a] = s.u.l.st[k][fn][1 + a] / S;
-          R.c[r][4] = s.u.l.st[k][fn][5];
-          R.d[3 + r] = -s.u.l.st[k][fn][0] / S;
+          for (int a = 0; a < 4; ++a) R.c[r][a] = s.u.l.st[k][stx(k, fn, 1 + a)] / S;
+          R.c[r][4] = s.u.l.st[k][stx(k, fn, 5)];
+          R.d[3 + r] = -s.u.l.st[k][stx(k, fn, 0)] / S;
           R.set(3 + r, on > 0.0);
         }
         const double wv = s.ub[k][1];

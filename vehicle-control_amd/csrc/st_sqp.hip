@@ -53,6 +53,14 @@ __host__ __device__ constexpr int qslot(int i, int j) {
   if (i == 8 && j == 8) return Q88;
   return -1;
 }
+// Swizzled lane-per-stage arrays (round 4): lane k reads row k of trow[.][8] and st[.][42] at a
+// fixed column, and those even strides put lanes k and k + 4 (trow: 8-way over a 32-lane
+// ds_read_b64 group) or k and k + 16 (st: 2-way) on the same banks.  Instead of padding (no LDS to
+// spare at N = 60) each row is permuted: trow column a of row k sits in slot (a + k / 4) mod 8,
+// st element e = 6 r + j of row k in slot e ^ (k / 16 mod 2) -- every lane of a group then reads
+// a distinct bank pair, and the layout stays a permutation within each row.
+__device__ __forceinline__ int tsw(int k, int a) { return (a + (k >> 2)) & 7; }
+__device__ __forceinline__ int stx(int k, int r, int j) { return (6 * r + j) ^ ((k >> 4) & 1); }
 // stage vector index -> column of [A6 | B6] (-1 for p: no dynamics enters through it)
 __host__ __device__ constexpr int vcol(int i) { return i < 6 ? i : (i == 6 ? -1 : i - 1); }
 
@@ -64,18 +72,25 @@ __host__ __device__ constexpr int vcol(int i) { return i < 6 ? i : (i == 6 ? -1 
 // Newton direction and the SQP cut-back's data in turn, and the Riccati scratch between them
 // (disjoint live ranges, below); the QP iterate stays in registers.  N = 40 then fits 4 one-wave
 // workgroups per CU (one per SIMD; 48.5 KB before left one SIMD idle), N = 60 fits 3 (was 2).
-struct StJ {  // [A6 | B6 diag(S, 1)] of one step, rows Ux, Uy, r, delta, ey, epsi; + 1 pad
-  double m[6][8];
+// [A6 | B6 diag(S, 1)] of one step, rows Ux, Uy, r, delta, ey, epsi; + 1 pad.  The forward LQ pass
+// reads rows 0..5 of one stage in lanes 0..5: a row stride of 8 doubles puts rows r and r + 4 on
+// the same banks, 9 does not -- used where the extra 6 doubles per stage keep the workgroups per
+// CU (N = 20, 40, 50; N = 30 / 60 would lose one)
+template <int JW>
+struct StJT {
+  double m[6][JW];
   double pad;
   __device__ __forceinline__ double* operator[](int r) { return m[r]; }
   __device__ __forceinline__ const double* operator[](int r) const { return m[r]; }
 };
 template <int N>
+using StJ = StJT<(N == 30 || N == 60) ? 8 : 9>;
+template <int N>
 struct StSmem {
   double xs[N][9];    // prediction (N columns, dynamics for k < N-1); [8] pad
   double ub[N][3];    // current ubar; [2] pad
   double kap[N], dsv[N];
-  StJ J[N];            // J[k][row][col], cols Ux, Uy, r, delta, ey, epsi | dFx, dw
+  StJ<N> J[N];         // J[k][row][col], cols Ux, Uy, r, delta, ey, epsi | dFx, dw
   union {
     struct {
       double Qt[N][NQ + 1];  // stage Hessian + barrier, this iteration; [NQ] pad
@@ -101,7 +116,7 @@ struct StSmem {
     struct {
       // (unpadded: this member sets the union's size; its reads are once per SQP iteration)
       double trow[N][8];     // t-row of step k over (y | dFx, dw)
-      double st[N][7][6];    // stage functions: value + gradient over (Ux, Uy, r, delta, Fx)
+      double st[N][42];    // stage functions: value + gradient over (Ux, Uy, r, delta, Fx)
     } l;
   } u;
   int flag[4];
@@ -365,8 +380,8 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
             s.J[kk][r][c0] = xn[yr[r]].d[0] * s0;
             s.J[kk][r][c1] = xn[yr[r]].d[1];
           }
-          s.u.l.trow[kk][c0] = xn[7].d[0] * s0;
-          s.u.l.trow[kk][c1] = xn[7].d[1];
+          s.u.l.trow[kk][tsw(kk, c0)] = xn[7].d[0] * s0;
+          s.u.l.trow[kk][tsw(kk, c1)] = xn[7].d[1];
         } else {
           const int q = task - NLIN, kk = q / 5, j = q % 5;
           D1 X5[5], o[7];
@@ -378,8 +393,8 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
           dyn_stage_terms_alg<D1, double>(X5, c, o);
 #pragma unroll
           for (int r = 0; r < 7; ++r) {
-            s.u.l.st[kk][r][1 + j] = o[r].d[0];
-            if (j == 0) s.u.l.st[kk][r][0] = o[r].v;
+            s.u.l.st[kk][stx(kk, r, 1 + j)] = o[r].d[0];
+            if (j == 0) s.u.l.st[kk][stx(kk, r, 0)] = o[r].v;
           }
         }
       }
@@ -416,10 +431,10 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       // slip-angle penalties when active at the prediction (:155-165)
 #pragma unroll
       for (int sr = 0; sr < 2; ++sr) {
-        const double fv = s.u.l.st[k][sr][0];
+        const double fv = s.u.l.st[k][stx(k, sr, 0)];
         const double wsl = fv >= 0.0 ? 2.0 * W.w_slip : 0.0;
-        const double a5[5] = {s.u.l.st[k][sr][1], s.u.l.st[k][sr][2], s.u.l.st[k][sr][3], s.u.l.st[k][sr][4],
-                              s.u.l.st[k][sr][5] * S};
+        const double a5[5] = {s.u.l.st[k][stx(k, sr, 1)], s.u.l.st[k][stx(k, sr, 2)], s.u.l.st[k][stx(k, sr, 3)], s.u.l.st[k][stx(k, sr, 4)],
+                              s.u.l.st[k][stx(k, sr, 5)] * S};
         constexpr int ix[5] = {0, 1, 2, 3, 7};
 #pragma unroll
         for (int a = 0; a < 5; ++a) {
@@ -442,7 +457,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       if (k < N - 1) {
         constexpr int iy[8] = {0, 1, 2, 3, 4, 5, 7, 8};
 #pragma unroll
-        for (int a = 0; a < 8; ++a) qc[iy[a]] += W.w_time * s.u.l.trow[k][a];
+        for (int a = 0; a < 8; ++a) qc[iy[a]] += W.w_time * s.u.l.trow[k][tsw(k, a)];
       }
       // terminal (:290-303)
       if (k == N - 1) {
@@ -466,9 +481,9 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       for (int r = 0; r < 5; ++r) {
         const int fn = 2 + r;
 #pragma unroll
-        for (int a = 0; a < 4; ++a) R.c[r][a] = s.u.l.st[k][fn][1 + a] / S;
-        R.c[r][4] = s.u.l.st[k][fn][5];
-        R.d[3 + r] = -s.u.l.st[k][fn][0] / S;
+        for (int a = 0; a < 4; ++a) R.c[r][a] = s.u.l.st[k][stx(k, fn, 1 + a)] / S;
+        R.c[r][4] = s.u.l.st[k][stx(k, fn, 5)];
+        R.d[3 + r] = -s.u.l.st[k][stx(k, fn, 0)] / S;
         R.m[3 + r] = stl ? 1.0 : 0.0;
       }
       const double wv = s.ub[k][1];
