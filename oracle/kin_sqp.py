@@ -60,6 +60,8 @@ RHO = 1e3           # L1 penalty on the state rows (above every multiplier seen 
 RHO_DEF = 1e3       # L1 penalty on the multiple-shooting defects
 NOISE_D = 8.0 * 2.220446049250313e-16 / 1e-7   # rounding level of the one-sided difference D (x max(1, |phi|))
 NOISE_PHI = 1e-13   # a noise-level step may not raise phi by more than this (x max(1, |phi|))
+V_DOM = 0.5        # merit domain: v > V_DOM, |epsi| < EPSI_DOM, rho > 0 on stages 0..N-1
+EPSI_DOM = 1.2
 TIE = 1e-9          # the rollout is preferred unless the state iterate's merit is lower by more
 IV, ID, IS, IEY, IEP, IT = Q.IV, Q.ID, Q.IS, Q.IEY, Q.IEP, Q.IT
 IA, IW = Q.IA, Q.IW
@@ -120,23 +122,33 @@ def merit(x0, u, kappa, ds, L, W, x=None):
     viol = (np.maximum(W["v_min"] - v, 0.0) + np.maximum(dl - W["delta_max"], 0.0)
             + np.maximum(W["delta_min"] - dl, 0.0))
     phi += RHO * np.sum(viol, axis=1)
-    return phi + pdef
+    # the spatial model's domain (kinematic_car.py:47-60 divides by v cos(epsi) and rho = 1 - ey kappa):
+    # a trajectory whose stages 0..N-1 leave it (v <= V_DOM, |epsi| >= EPSI_DOM, rho <= 0) is no
+    # candidate -- e.g. a plan spinning to |epsi| >> pi/2, which the defect rollout of the next
+    # control step turns into delta ~ 1e10 and an infeasible QP
+    xs = x[:, :N]
+    rho_ = 1.0 - xs[:, :, IEY] * np.asarray(kappa, np.float64)
+    inside = ((xs[:, :, IV] > V_DOM) & (np.abs(xs[:, :, IEP]) < EPSI_DOM) & (rho_ > 0.0)).all(axis=1)
+    return np.where(inside, phi + pdef, np.inf)
 
 
 def line_search(x0, ubar, dz, kappa, ds, L, W):
     """(alpha[B], phi0[B], phi_alpha[B], D[B]) of the rule in the module docstring."""
     ubar = np.asarray(ubar, np.float64)
     phi0 = merit(x0, ubar, kappa, ds, L, W)
-    D = (merit(x0, ubar + EPS_FD * dz, kappa, ds, L, W) - phi0) / EPS_FD
+    with np.errstate(invalid="ignore"):
+        D = (merit(x0, ubar + EPS_FD * dz, kappa, ds, L, W) - phi0) / EPS_FD
     B = len(phi0)
     alpha = np.zeros(B)
     phia = phi0.copy()
-    done = D >= 0.0
+    restore = ~np.isfinite(phi0)   # outside the domain: the largest step back inside it
+    done = (D >= 0.0) & ~restore
     a = 1.0
     p1 = None
     for _ in range(LS_STEPS):
         pa = merit(x0, ubar + a * dz, kappa, ds, L, W)
-        ok = ~done & (pa <= phi0 + ARMIJO * a * D)
+        with np.errstate(invalid="ignore"):
+            ok = ~done & np.isfinite(pa) & (restore | (pa <= phi0 + ARMIJO * a * D))
         p1 = pa if p1 is None else p1
         alpha[ok] = a
         phia[ok] = pa[ok]
@@ -171,19 +183,22 @@ def line_search_ms(x0, ubar, dz, x, dx, kappa, ds, L, W):
     roll = np.isfinite(ps0) & (ps0 <= pm0 + TIE * np.abs(pm0))
     sel = lambda vs, vm: np.where(roll, vs, vm)
     phi0 = sel(ps0, pm0)
-    D = (sel(ps(EPS_FD), pm(EPS_FD)) - phi0) / EPS_FD
+    with np.errstate(invalid="ignore"):
+        D = (sel(ps(EPS_FD), pm(EPS_FD)) - phi0) / EPS_FD
     B = len(phi0)
     alpha = np.zeros(B)
     phia = phi0.copy()
     pr, pa_m = ps0.copy(), pm0.copy()
-    done = D >= 0.0
+    restore = ~np.isfinite(phi0)   # both merits outside the domain: the largest step back inside
+    done = (D >= 0.0) & ~restore
     a = 1.0
     first = None
     for _ in range(LS_STEPS):
         vs, vm = ps(a), pm(a)
         pa = sel(vs, vm)
         first = (pa, vs, vm) if first is None else first
-        ok = ~done & (pa <= phi0 + ARMIJO * a * D)
+        with np.errstate(invalid="ignore"):
+            ok = ~done & np.isfinite(pa) & (restore | (pa <= phi0 + ARMIJO * a * D))
         alpha[ok] = a
         phia[ok] = pa[ok]
         pr[ok], pa_m[ok] = vs[ok], vm[ok]
@@ -194,6 +209,7 @@ def line_search_ms(x0, ubar, dz, x, dx, kappa, ds, L, W):
     phia[nz] = first[0][nz]
     pr[nz], pa_m[nz] = first[1][nz], first[2][nz]
     reset = np.isfinite(pr) & (pr <= pa_m + TIE * np.abs(pa_m))
+    line_search_ms.reset_gap = (pr - pa_m) / np.abs(pa_m)   # for tests: how close the reset decision was
     return alpha, phi0, phia, D, reset
 
 
@@ -252,6 +268,7 @@ def kin_sqp_solve(x0, ubar, kappa, ds, L, W, sqp_iters, x_ws=None, elastic=0.0, 
             x[reset] = Q.kin_predict(np.asarray(x0, np.float64)[reset], u[reset], np.asarray(kappa)[reset],
                                      np.asarray(ds)[reset], L)
             hist[-1]["reset"] = reset
+            hist[-1]["reset_gap"] = line_search_ms.reset_gap
         # a first QP without a solution restarts the iterate from the neutral guess (u = 0, the
         # state iterate x0 at every stage); the next QP's status is then the step's (kin_merit.hip)
         if it == 0 and sqp_iters > 1 and not ok.all():

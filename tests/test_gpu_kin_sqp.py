@@ -135,7 +135,16 @@ def test_kin_sqp_multiple_shooting_vs_oracle(golden):
           f"status {np.bincount(st)}")
     assert (st == 0).all(), st
     assert err.max() < U_TOL, np.argsort(err)[-5:]
-    assert ex < 1e-6
+    # x*: the state iterate, or its rollout where the last step reset it -- a discrete choice
+    # between two merits; where the oracle's two merits were within 1e-6 (relative) of each
+    # other, u* differences of ~1e-8 can flip it, so there x* may equal either candidate
+    tie = np.abs(ref["hist"][-1]["reset_gap"]) < 1e-6
+    exb = np.abs(xs - ref["x_star"]).max(axis=(1, 2))
+    x_roll = Q.kin_predict(x0, us, kap, ds, 2.5)
+    exb = np.where(tie, np.minimum(exb, np.abs(xs - x_roll).max(axis=(1, 2))), exb)
+    print(f"reset near-ties: {np.nonzero(tie)[0].tolist()}; |x* - x*_oracle| max outside them "
+          f"{exb.max():.2e}")
+    assert exb.max() < 1e-6
     np.testing.assert_array_equal(u0, us[:, 0])
     phi_end = np.minimum(KS.merit(x0, us, kap, ds, 2.5, W), KS.merit(x0, us, kap, ds, 2.5, W, x=xs))
     assert (phi_end <= np.minimum(ps0, pm0) * (1 + 1e-9)).all()

@@ -153,27 +153,14 @@ def test_kinematic_closed_loop_with_obstacles():
     assert nfail_on.sum() <= 0.02 * B * K, nfail_on.sum()
 
 
-@pytest.mark.parametrize("N", [30, 50])
-def test_kinematic_closed_loop_with_obstacles_long_horizon(N):
-    """The same obstacle loop at longer kinematic horizons (the reference's kinematic.yaml has
-    N = 50), where the multiple-shooting SQP (vc_qp.ms) keeps the swerving plans' states as the
-    iterate instead of re-rolling them through eps = +-pi/2, and a first QP without a solution
-    restarts the step's iterate from the neutral guess (kin_merit.hip).  N = 30: every vehicle
-    clear and on track.  N = 50: every vehicle clear of the obstacles, <= 1 % non-solved steps,
-    >= 3/4 on track -- NOT every vehicle: vehicles whose plans cross the *soft* track boundary
-    (a cost term, kinematic_mpc.py:110-122; the plans cross with every QP solved, so that is the
-    NLP's own trade-off) count as off track, and over four seeds of this loop (scripts/
-    kin_obs_n50_diag.py) one or two vehicles per 64 are lost after runs of
-    non-solved steps in two of them -- a known limitation at this horizon, reported, not asserted
-    away."""
+def _kin_obstacle_loop(N, seed, B=64, K=400):
     from vcmpc.config import load_config
     from vcmpc.environment import Track
     from vcmpc.models import KinematicCar
     from vcmpc.simulation import BatchedRacingSimulator
     tr = Track.load("ippodromo")
     obs = [(o.s, o.ey, o.radius) for o in tr.obstacles]
-    B, K = 64, 400
-    rng = np.random.default_rng(3)
+    rng = np.random.default_rng(seed)
     x0 = np.zeros((B, 6))
     x0[:, 0] = rng.uniform(5, 8, B)
     x0[:, 2] = rng.uniform(0, 15, B)
@@ -187,15 +174,39 @@ def test_kinematic_closed_loop_with_obstacles_long_horizon(N):
     X = out["state_traj"]
     clear = _min_clearance(X, obs, 2, 3)
     on = (np.abs(X[:, :, 3]) < tr.width / 2).all(axis=0)
-    print(f"N={N}: {int((clear > 0).sum())}/{B} clear, {int(on.sum())}/{B} on track, non-solved "
-          f"{int(out['nfail'].sum())} of {B * K}, max |ey| {np.abs(X[:, :, 3]).max():.2f}")
+    print(f"N={N} seed={seed}: {int((clear > 0).sum())}/{B} clear, {int(on.sum())}/{B} on track, non-solved "
+          f"{int(out['nfail'].sum())} of {B * K}, max |ey| {np.abs(X[:, :, 3]).max():.2f}, median s_end "
+          f"{np.median(X[-1, :, 2]):.1f}")
+    return X, clear, on, out["nfail"], tr
+
+
+def test_kinematic_closed_loop_with_obstacles_n30():
+    """The same obstacle loop at N = 30: every vehicle clear and on track, <= 0.2 % non-solved."""
+    X, clear, on, nfail, tr = _kin_obstacle_loop(30, 3)
     assert (clear > 0).all()
-    if N <= 30:
-        assert on.all()
-        assert out["nfail"].sum() <= 0.002 * B * K
-    else:
-        assert on.sum() >= int(0.75 * B)
-        assert out["nfail"].sum() <= 0.01 * B * K
+    assert on.all()
+    assert nfail.sum() <= 0.002 * nfail.size * 400
+
+
+@pytest.mark.parametrize("seed", [3, 5, 7, 11])
+def test_kinematic_closed_loop_with_obstacles_reference_horizon(seed):
+    """The reference's default kinematic controller (config/controllers/kinematic.yaml: N = 50,
+    obstacles True; kinematic_mpc.py:110-133) on the obstacle loop, four seeds.  Round 3 lost
+    vehicles here (seed 5: |ey| 35.5 m and 32.5 m, seed 11: 58 m, after runs of non-solved steps;
+    0.9-1.7 % non-solved).  Round 4 found three causes on the captured failing steps
+    (scripts/kin_lost_capture.py + kin_lost_replay.py, kin_loop_cpu.py): the merit line
+    search stopped short (8 step sizes, no steps below the merit's rounding level: the SQP stalled
+    on a stale plan), an accepted multiple-shooting iterate could leave the model's domain (plans
+    spinning to |epsi| >> pi/2, whose defect rollout made the next QP infeasible), and the QPs
+    through an obstacle needed more than the 40 interior-point iterations of the C2 cap.  Bars
+    (VERDICT r03 item 1): nobody lost (|ey| < width / 2 + 2.5 m for every vehicle at every step),
+    every vehicle clear of every obstacle, <= 0.5 % non-solved steps."""
+    X, clear, on, nfail, tr = _kin_obstacle_loop(50, seed)
+    assert np.isfinite(X).all()
+    assert np.abs(X[:, :, 3]).max() < tr.width / 2 + 2.5
+    assert (clear > 0).all()
+    assert nfail.sum() <= 0.005 * nfail.size * 400
+    assert np.median(X[-1, :, 2]) > 200.0         # through the field (obstacles up to s = 185)
 
 
 def test_dynamic_closed_loop_avoids_obstacles():

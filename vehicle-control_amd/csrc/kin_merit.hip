@@ -40,6 +40,8 @@ constexpr double RHO_DEF = 1e3;  // L1 penalty on the multiple-shooting defects
 // taken when it raises phi by no more than NOISE_PHI (both x max(1, |phi0|))
 constexpr double NOISE_D = 8.0 * 2.220446049250313e-16 / 1e-7;
 constexpr double NOISE_PHI = 1e-13;
+constexpr double V_DOM = 0.5;      // merit domain: v > V_DOM, |epsi| < EPSI_DOM, rho > 0 (oracle V_DOM)
+constexpr double EPSI_DOM = 1.2;
 constexpr double TIE = 1e-9;     // the rollout wins unless the state iterate's merit is lower by more
 constexpr int32_t RESTART_PENDING = -1;  // st_acc: the iterate restarted, the next QP's status is the step's
 
@@ -77,6 +79,7 @@ __device__ double merit(const KinMeritArgs& A, int b, double alpha, bool msm) {
 #pragma unroll
   for (int i = 0; i < KIN_NX; ++i) x[i] = x0[i];
   double blo = 0.0, bhi = 0.0, dev = 0.0, obs = 0.0, ww = 0.0, wa = 0.0, pen = 0.0, a_prev = 0.0, pdef = 0.0;
+  bool inside = true;  // the spatial model's domain on stages 0..N-1 (oracle/kin_sqp.py merit)
   const double m0 = A.obs.margin_min;
   for (int n = 0; n < N; ++n) {
     const double u[2] = {step_to(up[2 * n], uq[2 * n], alpha), step_to(up[2 * n + 1], uq[2 * n + 1], alpha)};
@@ -96,6 +99,7 @@ __device__ double merit(const KinMeritArgs& A, int b, double alpha, bool msm) {
     }
     ww += W.w_w * u[1] * u[1];
     a_prev = u[0];
+    inside = inside && x[0] > V_DOM && fabs(x[4]) < EPSI_DOM && 1.0 - x[3] * kap[n] > 0.0;
     double f[KIN_NX];
     kin_spatial_ode<double>(x, u, kap[n], A.L, f);
     if (msm) {
@@ -114,7 +118,7 @@ __device__ double merit(const KinMeritArgs& A, int b, double alpha, bool msm) {
   double phi = blo + bhi + dev + obs + ww + wa + RHO_DEF * pdef;
   if (x[0] >= W.v_max) phi += W.w_v * (x[0] - W.v_max) * (x[0] - W.v_max);
   phi += W.w_time * x[5] + W.w_ey * x[3] * x[3] + W.w_epsi * x[4] * x[4];
-  return phi + RHO * pen;
+  return inside ? phi + RHO * pen : __builtin_huge_val();
 }
 
 __global__ __launch_bounds__(64) void kin_merit_kernel(KinMeritArgs A) {
@@ -144,8 +148,10 @@ __global__ __launch_bounds__(64) void kin_merit_kernel(KinMeritArgs A) {
   // the neutral guess (u = 0, the state iterate the current state at every stage, the plan
   // vc_simulate's failure restart would give) and the remaining iterations solve from there
   const bool restart = A.restart && A.first && !qp_ok;
-  // lane 0..LS-1: sufficient decrease?  the first such lane (largest alpha) wins
-  const bool good = l < LS && qp_ok && D < 0.0 && isfinite(phi) && phi <= phi0 + ARMIJO * alpha * D;
+  // lane 0..LS-1: sufficient decrease?  the first such lane (largest alpha) wins.  From an iterate
+  // outside the model's domain (phi0 = inf): the largest step back inside it
+  const bool restore = !isfinite(phi0);
+  const bool good = l < LS && qp_ok && isfinite(phi) && (restore || (D < 0.0 && phi <= phi0 + ARMIJO * alpha * D));
   const uint64_t mask = __ballot(good);
   const double sc = fmax(1.0, fabs(phi0));
   const double p1 = bcast(phi, 0);

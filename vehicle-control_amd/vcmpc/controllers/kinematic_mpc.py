@@ -60,8 +60,12 @@ KIN_OBS_MS = 1
 # max |ey| 3.6 / 43 m; N = 50 36 / 40 off, 813 / 763 non-solved, 0 / 5 obstacle hits; DESIGN.md
 # 2c), so the controller keeps hard rows; elastic stays available through the qp block.
 KIN_OBS_ELASTIC = 0.0
-# The elastic rows' interior point needs about twice the plain one's iterations (the multipliers
-# start on rho = la + le): with elastic rows the cap is raised.
+# The obstacle QPs need more interior-point iterations than the C2 cap of 40: a plan that runs
+# through an obstacle (e.g. the neutral restart's constant-ey plan) meets the barrier's floored
+# margin, curvatures ~1e6 and condition numbers ~4e10 (44 iterations for the oracle on
+# gpurun_out/kin_lost seed 3 vehicle 1, where the 40-iteration kernel reported max-iter), and elastic
+# rows about twice the plain count (the multipliers start on rho = la + le): with obstacles on the
+# cap is raised to 80 (the easy QPs stop at their own tolerance long before).
 KIN_OBS_MAX_ITER = 80
 
 
@@ -78,7 +82,7 @@ def kin_qp_block(config) -> dict:
     if int(config["horizon"]) >= KIN_SHIFT_FROM_N:
         qp["shift"] = 1
     qp.update(config.get("qp") or {})
-    if qp.get("elastic", 0.0) != 0.0:
+    if config.get("obstacles") or qp.get("elastic", 0.0) != 0.0:
         qp["max_iter"] = max(int(qp.get("max_iter", 0)), KIN_OBS_MAX_ITER)
     return qp
 
