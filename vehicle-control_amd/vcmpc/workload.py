@@ -63,9 +63,10 @@ def kinematic_batch(B: int, N: int = 20, seed: int = 31, mpc_dt: float = 0.03, L
         ubar = rng.uniform(-1, 1, (m, N, 2)) * np.array([a_max, w_max])
         ds_c = np.repeat(mpc_dt * x0[:, :1] + 0.5, N, axis=1)
         with np.errstate(all="ignore"):
-            _, v_pred = _kin_rollout(x0, ubar, kappa, ds_c, L, speeds=True)
+            ok_pred, v_pred = _kin_rollout(x0, ubar, kappa, ds_c, L, speeds=True)
             ds = mpc_dt * v_pred[:, :N] + 0.5             # kinematic_mpc.py:178-182
-            ok = _kin_rollout(x0, ubar, kappa, ds, L) & np.isfinite(ds).all(1)
+            # both the speed prediction and the rollout on the final grid inside the domain
+            ok = ok_pred & _kin_rollout(x0, ubar, kappa, ds, L) & np.isfinite(ds).all(1)
         for k, v in (("x0", x0), ("kappa", kappa), ("ds", ds), ("ubar", ubar)):
             out[k].append(v[ok])
         have += int(ok.sum())
