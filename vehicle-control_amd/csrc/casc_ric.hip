@@ -71,9 +71,10 @@ __host__ __device__ constexpr int vcol(int i) { return i < 6 ? i : (i == 6 ? -1 
 // Strides (round 4): a lane-per-stage phase reads row k of xs / ub / J in lane k; an even stride
 // of 8 doubles put lanes k and k + 4 on the same banks (ds_read_b64: bank (a/4) mod 64 over 32
 // lanes -> 8-way on xs, 16-way on J's 48-double stages, 2-way on ub), so every such array has an
-// odd stride (9, 3, 49): the 32 lanes of a ds_read_b64 group then hit 32 distinct bank pairs and
-// the 16 of a ds_write_b64 / ds_read2_b64 group 16 ((a/4) mod 32).  +180 doubles: M = 40 stays at
-// three one-wave workgroups per CU.
+// odd stride (xs 9, J 49): the 32 lanes of a ds_read_b64 group then hit 32 distinct bank pairs and
+// the 16 of a ds_write_b64 / ds_read2_b64 group 16 ((a/4) mod 32).  ub keeps stride 2 (2-way
+// only): with it at 3 too, M = 40 needed 54,312 B and dropped to two workgroups per CU (C3
+// cascaded 201 K -> 143 K solves/s, r04c); at 53,832 B three fit (<= 54,272 B).
 struct CrJ {  // [A6 | B6 diag(S, 1 or S)] of one transition + 1 pad (49 doubles)
   double m[6][8];
   double pad;
@@ -84,7 +85,7 @@ template <int N, int M>
 struct CrSmem {
   static constexpr int H = N + M;
   double xs[H][9];    // prediction: single-track states k < N, point-mass (V, s, ey, epsi, t) k >= N; [8] pad
-  double ub[H][3];    // current ubar; [2] pad
+  double ub[H][2];    // current ubar (stride 2: the odd stride 3 cost M = 40 its third workgroup per CU)
   double kap[H], dsv[H];
   CrJ J[H];           // J[k][row][col]: [A6 | B6 diag(S, 1 or S)] of the transition out of stage k
   union {
@@ -211,6 +212,9 @@ template <int N, int M, int TYRE>
 __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
   constexpr int H = N + M;
   static_assert(N >= 2 && M >= 2 && H <= WTH, "one lane per stage");
+  // occupancy guard: one-wave workgroups per CU = floor(160 KB / LDS), LDS allocated in 1 KB
+  // granules (measured: 54,312 B ran two per CU at M = 40, r04c); M = 40 must keep three
+  static_assert(M != 40 || sizeof(CrSmem<N, M>) <= 54272, "casc_ric<20, 40> must fit three workgroups per CU");
   __shared__ CrSmem<N, M> s;
   const int l = threadIdx.x;
   const int b = xcd_problem(blockIdx.x, A.B);

@@ -226,6 +226,8 @@ __device__ __forceinline__ void qmul(const double* Q, const double* v, double* o
 template <int N, int TYRE>
 __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
   static_assert(N >= 2 && N <= WTH, "one lane per stage");
+  // occupancy guard (1 KB LDS granules, 160 KB per CU): N = 60 keeps three workgroups per CU
+  static_assert(N != 60 || sizeof(StSmem<N>) <= 54272, "st_sqp<60> must fit three workgroups per CU");
   __shared__ StSmem<N> s;
   const int l = threadIdx.x;
   const int b = xcd_problem(blockIdx.x, A.B);
