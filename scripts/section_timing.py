@@ -50,3 +50,14 @@ with Context(N=20, max_batch=B, params=p) as c:
         per_it = cyc[:, i].sum() / max(its.sum(), 1) if nm in ("resid", "build", "chol", "solve") else float("nan")
         print(f"  {nm:10s} mean {cyc[:, i].mean():10.0f}  ({100 * cyc[:, i].mean() / tot.mean():5.1f} %)  per IPM iter {per_it:9.0f}"
               f"   slowest problem {cyc[tot.argmax(), i]:10.0f}")
+    # the launch ends with its slowest problem (one wave per SIMD at B = 1024): where the tail comes from
+    order = np.argsort(tot)[::-1]
+    print(f"  total cycles percentiles p50 {np.percentile(tot, 50):.0f} p90 {np.percentile(tot, 90):.0f} "
+          f"p99 {np.percentile(tot, 99):.0f} max {tot.max():.0f}")
+    for b in order[:6]:
+        print(f"  slow problem {b}: total {tot[b]:.0f} iters {its[b]:.0f} polish rounds {dg[b, 3]:.0f} "
+              + " ".join(f"{nm}={cyc[b, i]:.0f}" for i, nm in enumerate(names) if cyc[b, i] > 0))
+    for k in range(int(its.min()), int(its.max()) + 1):
+        sel = its == k
+        if sel.any():
+            print(f"  iters {k:2d}: {sel.sum():4d} problems, total cycles mean {tot[sel].mean():.0f} max {tot[sel].max():.0f}")

@@ -70,11 +70,13 @@ __host__ __device__ constexpr int vcol(int i) { return i < 6 ? i : (i == 6 ? -1 
 
 // Strides (round 4): a lane-per-stage phase reads row k of xs / ub / J in lane k; an even stride
 // of 8 doubles put lanes k and k + 4 on the same banks (ds_read_b64: bank (a/4) mod 64 over 32
-// lanes -> 8-way on xs, 16-way on J's 48-double stages, 2-way on ub), so every such array has an
-// odd stride (xs 9, J 49): the 32 lanes of a ds_read_b64 group then hit 32 distinct bank pairs and
-// the 16 of a ds_write_b64 / ds_read2_b64 group 16 ((a/4) mod 32).  ub keeps stride 2 (2-way
-// only): with it at 3 too, M = 40 needed 54,312 B and dropped to two workgroups per CU (C3
-// cascaded 201 K -> 143 K solves/s, r04c); at 53,832 B three fit (<= 54,272 B).
+// lanes -> 8-way on xs, 16-way on J's 48-double stages, 2-way on ub).  J, the array every
+// Riccati sweep reads, gets the odd stride 49: the 32 lanes of a ds_read_b64 group then hit 32
+// distinct bank pairs and the 16 of a ds_write_b64 / ds_read2_b64 group 16 ((a/4) mod 32).  xs
+// and ub keep 8 / 2, and the model coefficients are read from the kernel arguments instead of
+// LDS: with odd xs / ub strides too the M = 40 block reached 54,312 B, which rocprofv3 allocates
+// as 54,272 B -- two workgroups per CU instead of three (cascaded 201 K -> 143 K solves/s,
+// r04c/d); three need <= 53,248 B.
 struct CrJ {  // [A6 | B6 diag(S, 1 or S)] of one transition + 1 pad (49 doubles)
   double m[6][8];
   double pad;
@@ -84,7 +86,7 @@ struct CrJ {  // [A6 | B6 diag(S, 1 or S)] of one transition + 1 pad (49 doubles
 template <int N, int M>
 struct CrSmem {
   static constexpr int H = N + M;
-  double xs[H][9];    // prediction: single-track states k < N, point-mass (V, s, ey, epsi, t) k >= N; [8] pad
+  double xs[H][8];    // prediction: single-track states k < N, point-mass (V, s, ey, epsi, t) k >= N
   double ub[H][2];    // current ubar (stride 2: the odd stride 3 cost M = 40 its third workgroup per CU)
   double kap[H], dsv[H];
   CrJ J[H];           // J[k][row][col]: [A6 | B6 diag(S, 1 or S)] of the transition out of stage k
@@ -117,14 +119,18 @@ struct CrSmem {
       double gfy[6];         // Fy_f + Fy_r at stage N-1: value + gradient over (Ux, Uy, r, delta, Fx)
     } l;
   } u;
-  // model coefficients and weights: each phase loads its own register copy from here (held in
-  // registers across the SQP loop they were spilled to scratch)
-  DynCoef<double> car;
+  // weights and QP options: each phase loads its own register copy from here (held in registers
+  // across the SQP loop they were spilled to scratch); the model coefficients are re-read from
+  // the kernel arguments (kargs), which keeps the M = 40 block at three workgroups per CU
   vc_dyn_mpc w;
   vc_casc_mpc cw;
   vc_qp qp;
   int flag[4];
 };
+
+#ifndef CR_RES_RECUR
+#define CR_RES_RECUR 1  // dual residual carried by the steps (0: adjoint sweep every iteration)
+#endif
 
 #define WSYNC()                          \
   do {                                   \
@@ -133,6 +139,14 @@ struct CrSmem {
     asm volatile("" ::: "memory");       \
   } while (0)
 
+// the kernel-argument block through an opaque scalar pointer: every read is a fresh scalar load
+// at its point of use (K$ hit), so nothing derived from it is held -- spilled -- across a phase
+template <typename T>
+__device__ __forceinline__ const T* kargs() {
+  const T* p = (const T*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
 __device__ __forceinline__ double bcast(double v, int l) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
   const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
@@ -212,9 +226,9 @@ template <int N, int M, int TYRE>
 __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
   constexpr int H = N + M;
   static_assert(N >= 2 && M >= 2 && H <= WTH, "one lane per stage");
-  // occupancy guard: one-wave workgroups per CU = floor(160 KB / LDS), LDS allocated in 1 KB
-  // granules (measured: 54,312 B ran two per CU at M = 40, r04c); M = 40 must keep three
-  static_assert(M != 40 || sizeof(CrSmem<N, M>) <= 54272, "casc_ric<20, 40> must fit three workgroups per CU");
+  // occupancy guard (rocprofv3 LDS_Block_Size: 53,248 B ran three one-wave workgroups per CU --
+  // r03, 201 K solves/s at M = 40 --, 54,272 B two -- r04c/d, 143-147 K); M = 40 must keep three
+  static_assert(M != 40 || sizeof(CrSmem<N, M>) <= 53248, "casc_ric<20, 40> must fit three workgroups per CU");
   __shared__ CrSmem<N, M> s;
   const int l = threadIdx.x;
   const int b = xcd_problem(blockIdx.x, A.B);
@@ -235,7 +249,6 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
   }
   if (l == 0) {
     s.flag[0] = VC_SOLVED;
-    s.car = A.car;
     s.w = A.w;
     s.cw = A.cw;
     s.qp = A.qp;
@@ -263,7 +276,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     // ---------------- predict (lane 0: RK4, switch, point-mass Euler) ----------------
     // the only rollout site; flag[2]: finite and inside both models' domain (casc_in_domain)
     if (l == 0) {
-      DynCoef<double> c = s.car;
+      DynCoef<double> c = kargs<CascSqpArgs>()->car;
       c.tyre = TYRE;
       double x[8];
 #pragma unroll
@@ -328,7 +341,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
 
     // ---------------- linearize + stage functions ----------------
     {
-      DynCoef<double> c = s.car;
+      DynCoef<double> c = kargs<CascSqpArgs>()->car;
       c.tyre = TYRE;
       constexpr int NLIN = 8 * (N - 1), NSTF = 5 * N, NPM = 3 * (M - 1);
       using D2 = Dual<2, double>;
@@ -440,7 +453,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     // (V, ey, epsi); t passes through unchanged
     if (l < 5) {
       using D1 = Dual<1, double>;
-      DynCoef<double> c = s.car;
+      DynCoef<double> c = kargs<CascSqpArgs>()->car;
       c.tyre = TYRE;
       D1 X5[5];
 #pragma unroll
@@ -485,7 +498,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       const vc_dyn_mpc W = s.w;
       const vc_casc_mpc CW = s.cw;
       const vc_qp QP = s.qp;
-      const double Peng = s.car.Peng;
+      const double Peng = kargs<CascSqpArgs>()->car.Peng;
       const double ds = s.dsv[k];
       // ey / s slots of this stage's state
       const double ey = pm ? s.xs[k][2] : s.xs[k][5], sa = pm ? s.xs[k][1] : s.xs[k][4];
@@ -866,6 +879,12 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     // ---------------- interior point (Mehrotra predictor-corrector) ----------------
     int it = 0;
     bool conv = false, fail = false;
+    // dual residual carried by the steps (CR_RES_RECUR): the LQ direction solves the linearised
+    // stationarity exactly, so a step of length alpha scales the condensed gradient by
+    // (1 - alpha); the adjoint sweep runs at the first iteration and wherever the carried value
+    // would end the loop (convergence, or acceptance at a factorisation failure)
+    double rd_carry = 0.0;
+    bool have_rd = false;
 #pragma unroll 1
     for (; it < s.qp.max_iter; ++it) {
       double rp[NR], wg[NR], grk[9], val[NR];
@@ -913,10 +932,17 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       WSYNC();
       rpm = wmax(rpm);
       const double mu = wsum(mus) / mcount;
-      const double rdm = dual_residual();
+      double rdm = (CR_RES_RECUR && have_rd) ? rd_carry : dual_residual();
       last_res = fmax(rdm, rpm);
       last_mu = mu;
       if (!(last_res == last_res) || !(mu == mu) || last_res > 1e300) { fail = true; break; }
+      if (CR_RES_RECUR && have_rd && mu <= 1e2 * tol_mu && fmax(rdm, rpm) <= 1e3 * rtol) {
+        // the carried value would end the loop here or below: take the sweep's
+        rdm = dual_residual();
+        have_rd = false;
+        last_res = fmax(rdm, rpm);
+        if (!(last_res == last_res) || last_res > 1e300) { fail = true; break; }
+      }
       if (last_res <= rtol && mu <= tol_mu) { conv = true; break; }
 
       const bool fok = factor();
@@ -980,6 +1006,8 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
         if (stl && R.m(i) > 0.0) amin = fmin(amin, fmin(step_to_bound(sl[i], dsa[i]), step_to_bound(la[i], dla[i])));
       }
       const double alpha = fmin(1.0, 0.99 * wmin(amin));
+      rd_carry = (1.0 - alpha) * rdm;
+      have_rd = true;
       if (stl) {
 #pragma unroll
         for (int i = 0; i < NR; ++i) {

@@ -56,7 +56,6 @@ __host__ __device__ constexpr int fcol(int j) { return j < 4 ? j : (j == 4 ? -1 
 template <int N>
 struct KrSmem {
   double xs[N + 1][6];  // prediction (becomes x* at the end)
-  double cdef[N][6];    // multiple shooting: defects F(xs_k, ub_k) - xs_{k+1}
   double ew[N + 1][5];  // multiple shooting: their linear rollout e over (v, delta, ey, epsi | t)
   double ub[N][2];
   double kap[N], dsv[N];
@@ -64,7 +63,13 @@ struct KrSmem {
   double tr[N][4];      // t-row of step k over (v, delta, ey, epsi)
   double Qt[N + 1][NQK];
   double gr[N + 1][NV];
-  double h[N + 1][NV];
+  // the LQ right-hand side h lives in the interior point / polish only; before it, in the
+  // multiple-shooting setup, the same space holds the defects -- at N = 50 this keeps the block
+  // at <= 39,936 B, four workgroups per CU instead of three (rocprofv3 LDS_Block_Size)
+  union {
+    double cdef[N][6];  // multiple shooting: defects F(xs_k, ub_k) - xs_{k+1} (setup only)
+    double h[N + 1][NV];
+  };
   double v[N + 1][NV];
   double dv[N + 1][NV];
   double K[N][2][NXT];
@@ -75,6 +80,10 @@ struct KrSmem {
   double Hm[NV][NV];
   int flag;
 };
+
+#ifndef KR_RES_RECUR
+#define KR_RES_RECUR 1  // dual residual carried by the steps (0: adjoint sweep every iteration)
+#endif
 
 #define WSYNC()                          \
   do {                                   \
@@ -696,6 +705,11 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
   bool conv = false, fail = false, polished = false, tried_polish = false;
   double mu_next_polish = MU_POLISH;
   double last_res = 0.0, last_mu = 0.0;
+  // dual residual carried by the steps (KR_RES_RECUR): the LQ direction solves the linearised
+  // stationarity exactly, so a step of length alpha scales the condensed gradient by (1 - alpha);
+  // the adjoint sweep runs at the first iteration and wherever the carried value would end the loop
+  double rd_carry = 0.0;
+  bool have_rd = false;
 #pragma unroll 1
   for (; finite_pred && it < A.qp.max_iter; ++it) {
     // (a) residuals, stage gradients, barrier-augmented stage Hessians
@@ -745,10 +759,17 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
     WSYNC();
     rpm = wmax(rpm);
     const double mu = wsum(mus) / mcount;
-    const double rdm = dual_residual();
+    double rdm = (KR_RES_RECUR && have_rd) ? rd_carry : dual_residual();
     last_res = fmax(rdm, rpm);
     last_mu = mu;
     if (!(last_res == last_res) || !(mu == mu) || last_res > 1e300) { fail = true; break; }
+    if (KR_RES_RECUR && have_rd && mu <= 1e2 * tol_mu && fmax(rdm, rpm) <= 1e3 * tol_r) {
+      // the carried value would end the loop here: take the sweep's
+      rdm = dual_residual();
+      have_rd = false;
+      last_res = fmax(rdm, rpm);
+      if (!(last_res == last_res) || last_res > 1e300) { fail = true; break; }
+    }
     if (last_res <= tol_r && mu <= tol_mu) { conv = true; break; }
     // polish attempts at mu <= 1e-7 and, if that active set does not certify, at 1e-10
     if (A.qp.polish > 0 && mu <= mu_next_polish) {
@@ -860,6 +881,8 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
       if (stl && m[i] > 0.0) amin = fmin(amin, fmin(step_to_bound(sl[i], dsa[i]), step_to_bound(la[i], dla[i])));
     }
     const double alpha = fmin(1.0, 0.99 * wmin(amin));
+    rd_carry = (1.0 - alpha) * rdm;
+    have_rd = true;
     if (stl) {
 #pragma unroll
       for (int i = 0; i < NRW; ++i) {

@@ -85,10 +85,17 @@ struct StJT {
 };
 template <int N>
 using StJ = StJT<(N == 30 || N == 60) ? 8 : 9>;
+// Row strides of xs / ub: odd (9, 3; conflict-free lane-per-stage reads) where the LDS allows;
+// N = 60 takes 8 / 2 -- a block above 53,248 B leaves two workgroups per CU instead of three
+// (measured: rocprofv3 LDS_Block_Size 53,248 ran three per CU, 54,272 two; r04)
+template <int N>
+constexpr int st_xs_w() { return N == 60 ? 8 : 9; }
+template <int N>
+constexpr int st_ub_w() { return N == 60 ? 2 : 3; }
 template <int N>
 struct StSmem {
-  double xs[N][9];    // prediction (N columns, dynamics for k < N-1); [8] pad
-  double ub[N][3];    // current ubar; [2] pad
+  double xs[N][st_xs_w<N>()];  // prediction (N columns, dynamics for k < N-1); [8] pad where 9
+  double ub[N][st_ub_w<N>()];  // current ubar; [2] pad where 3
   double kap[N], dsv[N];
   StJ<N> J[N];         // J[k][row][col], cols Ux, Uy, r, delta, ey, epsi | dFx, dw
   union {
@@ -115,7 +122,7 @@ struct StSmem {
     } q;
     struct {
       // (unpadded: this member sets the union's size; its reads are once per SQP iteration)
-      double trow[N][8];     // t-row of step k over (y | dFx, dw)
+      double trow[N - 1][8];  // t-row of step k < N-1 over (y | dFx, dw)
       double st[N][42];    // stage functions: value + gradient over (Ux, Uy, r, delta, Fx)
     } l;
   } u;
@@ -125,6 +132,10 @@ struct StSmem {
 // Workgroup = one wavefront: LDS operations of a wave execute in order, so a sync only has to
 // stop the compiler from moving memory operations across it (no s_barrier, and no wait for
 // outstanding loads other than the ones actually used).
+#ifndef ST_RES_RECUR
+#define ST_RES_RECUR 1  // dual residual carried by the steps (0: adjoint sweep every iteration)
+#endif
+
 #define WSYNC()                          \
   do {                                   \
     asm volatile("" ::: "memory");       \
@@ -226,8 +237,9 @@ __device__ __forceinline__ void qmul(const double* Q, const double* v, double* o
 template <int N, int TYRE>
 __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
   static_assert(N >= 2 && N <= WTH, "one lane per stage");
-  // occupancy guard (1 KB LDS granules, 160 KB per CU): N = 60 keeps three workgroups per CU
-  static_assert(N != 60 || sizeof(StSmem<N>) <= 54272, "st_sqp<60> must fit three workgroups per CU");
+  // occupancy guard (rocprofv3 LDS_Block_Size: 53,248 B ran three one-wave workgroups per CU,
+  // 54,272 B two): N = 60 keeps three
+  static_assert(N != 60 || sizeof(StSmem<N>) <= 53248, "st_sqp<60> must fit three workgroups per CU");
   __shared__ StSmem<N> s;
   const int l = threadIdx.x;
   const int b = xcd_problem(blockIdx.x, A.B);
@@ -753,6 +765,12 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     // ---------------- interior point (Mehrotra predictor-corrector) ----------------
     int it = 0;
     bool conv = false, fail = false;
+    // dual residual carried by the steps (ST_RES_RECUR): the LQ direction solves the linearised
+    // stationarity exactly, so a step of length alpha scales the condensed gradient by
+    // (1 - alpha); the adjoint sweep runs at the first iteration and wherever the carried value
+    // would end the loop (convergence, or acceptance at a factorisation failure)
+    double rd_carry = 0.0;
+    bool have_rd = false;
 #pragma unroll 1
     for (; it < A.qp.max_iter; ++it) {
       // (a) residuals, stage gradients, barrier-augmented stage Hessians
@@ -804,11 +822,18 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       const double mu = wsum(mus) / mcount;
       ST_ACC(ST_RESID, t_r0)
       ST_STAMP(t_d0)
-      const double rdm = dual_residual();
+      double rdm = (ST_RES_RECUR && have_rd) ? rd_carry : dual_residual();
       ST_ACC(ST_DUAL, t_d0)
       last_res = fmax(rdm, rpm);
       last_mu = mu;
       if (!(last_res == last_res) || !(mu == mu) || last_res > 1e300) { fail = true; break; }
+      if (ST_RES_RECUR && have_rd && mu <= 1e2 * tol_mu && fmax(rdm, rpm) <= 1e3 * rtol) {
+        // the carried value would end the loop here or below: take the sweep's
+        rdm = dual_residual();
+        have_rd = false;
+        last_res = fmax(rdm, rpm);
+        if (!(last_res == last_res) || last_res > 1e300) { fail = true; break; }
+      }
       if (last_res <= rtol && mu <= tol_mu) { conv = true; break; }
 
       // (b) Riccati factorisation of H + C'WC
@@ -886,6 +911,8 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
         if (stl && R.m[i] > 0.0) amin = fmin(amin, fmin(step_to_bound(sl[i], dsa[i]), step_to_bound(la[i], dla[i])));
       }
       const double alpha = fmin(1.0, 0.99 * wmin(amin));
+      rd_carry = (1.0 - alpha) * rdm;
+      have_rd = true;
       if (stl) {
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
