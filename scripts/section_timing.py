@@ -17,7 +17,8 @@ from vcmpc.workload import kinematic_batch  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 tol = float(sys.argv[2]) if len(sys.argv) > 2 else 1e-10
-names = ["S1 rollout", "setup", "resid", "build", "chol", "solve", "update", "polish", "out", "S2 jac", "S3 sens", "S4 hess"]
+names = ["S1 rollout", "setup", "resid", "build", "chol", "solve", "pol fact", "polish", "out", "S2 jac", "S3 sens", "S4 hess",
+         "pol AL", "AL passes"]
 dev = torch.device("cuda:0")
 d = kinematic_batch(B, seed=31)
 t = {k: torch.from_numpy(v).to(dev) for k, v in d.items()}
@@ -29,7 +30,7 @@ with Context(N=20, max_batch=B, params=p) as c:
     u0 = torch.empty((B, 2), dtype=torch.float64, device=dev)
     st = torch.empty((B,), dtype=torch.int32, device=dev)
     it = torch.empty((B,), dtype=torch.int32, device=dev)
-    diag = torch.zeros((B, 16), dtype=torch.float64, device=dev)
+    diag = torch.zeros((B, 4 + len(names)), dtype=torch.float64, device=dev)
     ptrs = [C for C in (t["x0"], t["kappa"], t["ds"], xbar, t["ubar"].clone(), u0, st, it, diag)]
     import ctypes as C
     for _ in range(2):
@@ -42,7 +43,8 @@ with Context(N=20, max_batch=B, params=p) as c:
     dg = diag.cpu().numpy()
     its = it.cpu().numpy().astype(float)
     cyc = dg[:, 4:]
-    tot = cyc.sum(1)
+    # pol fact (slot 6) and pol AL (12) are parts of polish (7); slot 13 counts AL passes
+    tot = cyc[:, :12].sum(1) - cyc[:, 6]
     print(f"B={B} tol={tol:g}: solved {(st.cpu().numpy() == 0).mean():.4f} iters mean {its.mean():.2f} max {its.max():.0f} "
           f"polish rounds mean {dg[:, 3].mean():.2f}")
     print(f"  total stamped cycles/problem: mean {tot.mean():.0f}  max {tot.max():.0f}")

@@ -854,14 +854,17 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       }
       WSYNC();
     };
-    auto dual_residual = [&]() -> double {
+    // condensed dual residual through the dynamics (adjoint sweep); cl: through the closed-loop
+    // A + B K of the last Riccati factorisation, as in st_sqp.hip (the open-loop sweep amplifies
+    // rounding through the RK4 step's unstable lateral mode at low speed)
+    auto dual_residual = [&](bool cl) -> double {
       BwdOps A3, B3;
       bwd_load(H - 1, s.u.q.g, A3);
       double rho = 0.0, rmax = 0.0;
       auto rstage = [&](int kk, const BwdOps& o) {
         const double g = bwd_g(kk, o, rho);
         rmax = fk ? fmax(rmax, fabs(g)) : rmax;
-        rho = g;
+        rho = cl ? g + o.a * bcast(g, 7) + o.b * bcast(g, 8) : g;  // lanes 0..6: + K' g_u
       };
 #pragma unroll 1
       for (int kk = H - 1; kk >= 0; kk -= 2) {
@@ -885,6 +888,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     // would end the loop (convergence, or acceptance at a factorisation failure)
     double rd_carry = 0.0;
     bool have_rd = false;
+    bool kvalid = false;  // s.u.q.K holds this IPM's factorisation (the linearisation aliases it)
 #pragma unroll 1
     for (; it < s.qp.max_iter; ++it) {
       double rp[NR], wg[NR], grk[9], val[NR];
@@ -932,13 +936,16 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       WSYNC();
       rpm = wmax(rpm);
       const double mu = wsum(mus) / mcount;
-      double rdm = (CR_RES_RECUR && have_rd) ? rd_carry : dual_residual();
+      const bool carried = CR_RES_RECUR && have_rd;
+      double rdm = carried ? rd_carry : dual_residual(kvalid);
+      bool rd_cl = carried || kvalid;
       last_res = fmax(rdm, rpm);
       last_mu = mu;
       if (!(last_res == last_res) || !(mu == mu) || last_res > 1e300) { fail = true; break; }
       if (CR_RES_RECUR && have_rd && mu <= 1e2 * tol_mu && fmax(rdm, rpm) <= 1e3 * rtol) {
         // the carried value would end the loop here or below: take the sweep's
-        rdm = dual_residual();
+        rdm = dual_residual(kvalid);
+        rd_cl = kvalid;
         have_rd = false;
         last_res = fmax(rdm, rpm);
         if (!(last_res == last_res) || last_res > 1e300) { fail = true; break; }
@@ -946,6 +953,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       if (last_res <= rtol && mu <= tol_mu) { conv = true; break; }
 
       const bool fok = factor();
+      kvalid = kvalid || fok;
       if (!fok) {
         // the barrier-augmented recursion lost definiteness at the numerical floor (weights
         // ~1e13, cancellation in P = Hxx - Hxu Huu^-1 Hux): a near-converged iterate stands
@@ -1007,7 +1015,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       }
       const double alpha = fmin(1.0, 0.99 * wmin(amin));
       rd_carry = (1.0 - alpha) * rdm;
-      have_rd = true;
+      have_rd = rd_cl;  // only closed-loop values are carried
       if (stl) {
 #pragma unroll
         for (int i = 0; i < NR; ++i) {

@@ -46,6 +46,9 @@
 // iteration (0: three matrix-vector products per iteration, the round-3 form)
 #define KIN_RES_RECUR 1
 #endif
+#ifndef KIN_POLISH_BLOCKED
+#define KIN_POLISH_BLOCKED 1  // polish factorisation: the interior point's blocked one (0: row-per-lane)
+#endif
 #ifndef KIN_POLISH_WARM
 #define KIN_POLISH_WARM 1  // polish multipliers start from the interior point's (0: from zero, round 3)
 #endif
@@ -149,7 +152,9 @@ __device__ __forceinline__ lds_cdouble* lds_opaque(const double* p) {
 #define VC_TACC(slot, t0)
 #endif
 // T_SWEEP = the serial rollout S1; T_S2 / T_S3 / T_S4 the sweep's other three parts
-enum { T_SWEEP = 0, T_SETUP, T_RESID, T_BUILD, T_CHOL, T_SOLVE, T_UPDATE, T_POLISH, T_OUT, T_S2, T_S3, T_S4, T_NSLOT };
+// T_UPDATE: the polish's matrix build + factorisation (part of T_POLISH); T_PAL its augmented-
+// Lagrangian passes (cycles), T_PPASS their count
+enum { T_SWEEP = 0, T_SETUP, T_RESID, T_BUILD, T_CHOL, T_SOLVE, T_UPDATE, T_POLISH, T_OUT, T_S2, T_S3, T_S4, T_PAL, T_PPASS, T_NSLOT };
 
 
 template <int N>
@@ -1234,6 +1239,37 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
       wave_sync();
       s.vc[lane] = rho_c;
       wave_sync();
+      VC_TSTAMP(t_pf0)
+#if KIN_POLISH_BLOCKED
+      {
+        // the interior point's path: H + G' diag(rho_c) G in the accumulator tiles (s.vc =
+        // rho_c; zero weights where no row is active), fixed rows / columns set to the identity
+        // in the tiles -- D (H + G'WG) D + (I - D) with D the free-variable mask equals the
+        // reduced matrix H_FF + G_F' W G_F -- and the blocked factorisation (matrix-core panel
+        // updates) instead of the row-per-lane one
+        d4 pacc[Tiles<N>::NT];
+        build_normal_acc<N>(pacc, s, 0.0, hjj, lane);
+        const int plr = lane >> 4, plc = lane & 15;
+#pragma unroll
+        for (int I = 0, t = 0; I < Tiles<N>::NB; ++I) {
+#pragma unroll
+          for (int J = 0; J <= I; ++J, ++t) {
+            const int c = 16 * J + plc;
+            const bool fc = (fmask >> c) & 1ull;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int r = 16 * I + plr + 4 * q;
+              const bool fr = (fmask >> r) & 1ull;
+              pacc[t][q] = (fr || fc) ? (r == c ? 1.0 : 0.0) : pacc[t][q];
+            }
+          }
+        }
+        if (!factor_blocked<N>(Mr, pacc, s, lane)) {
+          pchol_fail = true;
+          break;
+        }
+      }
+#else
       if (__ballot(rho_c > 0.0)) {
         build_normal_mfma<N>(Mr, s, 0.0, hjj, lane);
       } else {  // no active state row (most problems): the reduced Hessian only
@@ -1251,6 +1287,9 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
         pchol_fail = true;
         break;
       }
+#endif
+      VC_TACC(T_UPDATE, t_pf0)
+      VC_TSTAMP(t_pal0)
       // multiplier estimate: the interior point's own (lambda_hi - lambda_lo of an active row,
       // the sign convention of the check below), so the augmented-Lagrangian passes start next
       // to the fixed point instead of at 0 (KIN_POLISH_WARM; the fixed point does not depend on
@@ -1274,8 +1313,12 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
         const double e = al_act ? (yr - (alo_c ? cs.lo : cs.hi)) : 0.0;
         nu_c += rho_c * e;
         emax = wave_max(fabs(e));
+#ifdef VC_TIMING
+        tacc[T_PPASS] += 1;
+#endif
         if (emax <= 1e-14 * scale) break;
       }
+      VC_TACC(T_PAL, t_pal0)
       // KKT check of zp
       wave_sync();
       s.vz[lane] = (lane < n) ? zp : 0.0;
@@ -1379,7 +1422,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
   }
   VC_TACC(T_OUT, t_out0)
 #ifdef VC_TIMING
-  // timing builds: diag is [B][4 + T_NSLOT]; slot T_UPDATE = PDIP total - parts
+  // timing builds: diag is [B][4 + T_NSLOT]
   if (A.diag && lane < T_NSLOT) {
     double v = 0.0;
 #pragma unroll

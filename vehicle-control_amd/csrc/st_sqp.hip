@@ -739,15 +739,23 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       WSYNC();
     };
 
-    // condensed dual residual max |d/du (sum_k gr_k . v_k)| through the dynamics (adjoint sweep)
-    auto dual_residual = [&]() -> double {
+    // condensed dual residual max |d/du (sum_k gr_k . v_k)| through the dynamics (adjoint sweep).
+    // cl: through the closed-loop dynamics A + B K of the last Riccati factorisation, i.e. the
+    // gradient over v in u = K x + v -- zero exactly where the open-loop one is (an invertible
+    // change of the input variables), but without the open-loop sweep's growth: at low speed the
+    // reference's RK4 step (mpc_dt 0.03 s) is unstable in the lateral mode (|eig A_k| 3-5 at
+    // Ux = 4 m/s, Fx = 0), so over 60 stages the open-loop adjoint amplifies rounding by ~1e30 and
+    // the interior point never meets its tolerance once anything excites that mode (an obstacle's
+    // barrier gradient: scripts/st_obs_shoe_diag.py, the N = 60 obstacle runs of test_gpu_bands).
+    auto dual_residual = [&](bool cl) -> double {
       BwdOps A3, B3;
       bwd_load(N - 1, s.u.q.g, A3);
       double rho = 0.0, rmax = 0.0;
       auto rstage = [&](int kk, const BwdOps& o) {
         const double g = bwd_g(kk, o, rho);
         rmax = fk ? fmax(rmax, fabs(g)) : rmax;
-        rho = g;
+        // lanes 0..6: + K' g_u (the lq_solve backward pass's pv); lanes 7, 8 are not read on
+        rho = cl ? g + o.a * bcast(g, 7) + o.b * bcast(g, 8) : g;
       };
 #pragma unroll 1
       for (int kk = N - 1; kk >= 0; kk -= 2) {
@@ -771,6 +779,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     // would end the loop (convergence, or acceptance at a factorisation failure)
     double rd_carry = 0.0;
     bool have_rd = false;
+    bool kvalid = false;  // s.u.q.K holds this IPM's factorisation (the linearisation aliases it)
 #pragma unroll 1
     for (; it < A.qp.max_iter; ++it) {
       // (a) residuals, stage gradients, barrier-augmented stage Hessians
@@ -822,14 +831,17 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       const double mu = wsum(mus) / mcount;
       ST_ACC(ST_RESID, t_r0)
       ST_STAMP(t_d0)
-      double rdm = (ST_RES_RECUR && have_rd) ? rd_carry : dual_residual();
+      const bool carried = ST_RES_RECUR && have_rd;
+      double rdm = carried ? rd_carry : dual_residual(kvalid);
+      bool rd_cl = carried || kvalid;
       ST_ACC(ST_DUAL, t_d0)
       last_res = fmax(rdm, rpm);
       last_mu = mu;
       if (!(last_res == last_res) || !(mu == mu) || last_res > 1e300) { fail = true; break; }
       if (ST_RES_RECUR && have_rd && mu <= 1e2 * tol_mu && fmax(rdm, rpm) <= 1e3 * rtol) {
         // the carried value would end the loop here or below: take the sweep's
-        rdm = dual_residual();
+        rdm = dual_residual(kvalid);
+        rd_cl = kvalid;
         have_rd = false;
         last_res = fmax(rdm, rpm);
         if (!(last_res == last_res) || last_res > 1e300) { fail = true; break; }
@@ -839,6 +851,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       // (b) Riccati factorisation of H + C'WC
       ST_STAMP(t_f0)
       const bool fok = factor();
+      kvalid = kvalid || fok;
       ST_ACC(ST_FACT, t_f0)
       if (!fok) {
         // the barrier-augmented recursion lost definiteness at the numerical floor (weights
@@ -912,7 +925,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       }
       const double alpha = fmin(1.0, 0.99 * wmin(amin));
       rd_carry = (1.0 - alpha) * rdm;
-      have_rd = true;
+      have_rd = rd_cl;  // only closed-loop values are carried
       if (stl) {
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
