@@ -293,20 +293,27 @@ def casc_sqp_solve(x0, ubar, kappa, ds, p, W, tyre="fiala", keep_qps=False, **qp
     scale[:, 0] = S
     scale[N:, 1] = S
     hist = []
-    for _ in range(W["sqp_iters"]):
+    # a QP after the first without a solution ends the SQP at the current iterate (casc_ric.hip
+    # CR_KEEP_ITERATE; oracle/dyn_sqp.py)
+    stopped = np.zeros(B, bool)
+    for it_sqp in range(W["sqp_iters"]):
         Q = casc_qp(x0, u, kappa, ds, p, W, tyre)
         sol = solve_qp_batch(Q["H"], Q["g"], Q["C"], Q["d"], **qp_kw)
-        rec = dict(ubar=u.copy(), dz=sol["z"], kkt=sol["kkt"], polished=sol["polished"], iters=sol["iters"])
+        if it_sqp > 0:
+            stopped |= ~np.asarray(sol["converged"], bool)
+        z = np.where(stopped[:, None], 0.0, sol["z"])
+        rec = dict(ubar=u.copy(), dz=z, kkt=sol["kkt"], polished=sol["polished"], iters=sol["iters"])
         if keep_qps:
             rec.update({k: Q[k] for k in ("H", "g", "C", "d", "Gs", "Gp")})
-        du = sol["z"].reshape(B, H_, 2) * scale
+        du = z.reshape(B, H_, 2) * scale
         alpha = D.domain_step(np.asarray(x0, np.float64), u, du, np.asarray(kappa, np.float64),
                               np.asarray(ds, np.float64), p, tyre,
                               lambda x0_, u_, k_, ds_, p_, t_: casc_predict(x0_, u_, k_, ds_, p_, W, t_),
                               in_domain=casc_in_domain)
         rec["alpha"] = alpha
+        rec["stopped"] = stopped.copy()
         hist.append(rec)
-        u = np.where((alpha > 0)[:, None, None], u + alpha[:, None, None] * du, u)
+        u = np.where(((alpha > 0) & ~stopped)[:, None, None], u + alpha[:, None, None] * du, u)
     xs, xp = casc_predict(np.asarray(x0, np.float64), u, np.asarray(kappa, np.float64),
                           np.asarray(ds, np.float64), p, W, tyre)
     return dict(u_star=u, x_star=pack_states(xs, xp), u0=u[:, 0].copy(), hist=hist)

@@ -24,6 +24,8 @@ here once and implemented identically by ``csrc/dyn_sqp.hip``:
                   inside, 0 if none -- IPOPT cuts its step back the same way when the NLP
                   functions cannot be evaluated at a trial point; alpha = 1 from an iterate
                   outside the domain, and wherever the full step stays inside
+  A QP after the first without a solution (infeasible linearisation) refuses its step and ends
+  the SQP at the current iterate.
   output u* = ubar, x* = predict(u*), u0 = u*_0.
 
 QP cost = the reference NLP cost in Gauss-Newton form about (xbar, ubar), with every
@@ -289,10 +291,16 @@ def dyn_sqp_solve(x0, ubar, kappa, ds, p, W, tyre="linear", keep_qps=False, **qp
     B, N = u.shape[:2]
     S = W["fx_scale"]
     hist = []
-    for _ in range(W["sqp_iters"]):
+    # a QP after the first without a solution (converged False: the interior point diverged on an
+    # infeasible linearisation) refuses its step and ends the SQP at the current iterate
+    # (csrc/st_sqp.hip ST_KEEP_ITERATE, the kinematic SQP's rule)
+    stopped = np.zeros(B, bool)
+    for it_sqp in range(W["sqp_iters"]):
         Q = dyn_qp(x0, u, kappa, ds, p, W, tyre)
         sol = solve_qp_batch(Q["H"], Q["g"], Q["C"], Q["d"], **qp_kw)
-        dz = sol["z"]
+        if it_sqp > 0:
+            stopped |= ~np.asarray(sol["converged"], bool)
+        dz = np.where(stopped[:, None], 0.0, sol["z"])
         rec = dict(ubar=u.copy(), dz=dz, lam=sol["lam"], kkt=sol["kkt"], polished=sol["polished"],
                    iters=sol["iters"])
         if keep_qps:
@@ -301,8 +309,9 @@ def dyn_sqp_solve(x0, ubar, kappa, ds, p, W, tyre="linear", keep_qps=False, **qp
         alpha = domain_step(np.asarray(x0, np.float64), u, du, np.asarray(kappa, np.float64),
                             np.asarray(ds, np.float64), p, tyre, dyn_predict)
         rec["alpha"] = alpha
+        rec["stopped"] = stopped.copy()
         hist.append(rec)
-        u = np.where((alpha > 0)[:, None, None], u + alpha[:, None, None] * du, u)
+        u = np.where(((alpha > 0) & ~stopped)[:, None, None], u + alpha[:, None, None] * du, u)
     x_star = dyn_predict(np.asarray(x0, np.float64), u, np.asarray(kappa, np.float64),
                          np.asarray(ds, np.float64), p, tyre)
     return dict(u_star=u, x_star=x_star, u0=u[:, 0].copy(), hist=hist)

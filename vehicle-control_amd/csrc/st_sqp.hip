@@ -136,6 +136,10 @@ struct StSmem {
 #define ST_RES_RECUR 1  // dual residual carried by the steps (0: adjoint sweep every iteration)
 #endif
 
+#ifndef ST_KEEP_ITERATE
+#define ST_KEEP_ITERATE 1  // a later QP without a solution keeps the iterate (0: applies it, step non-solved)
+#endif
+
 #define WSYNC()                          \
   do {                                   \
     asm volatile("" ::: "memory");       \
@@ -942,6 +946,13 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     }
     it_total += it;
     it_max = max(it_max, it);
+    // a QP after the first without a solution (an infeasible linearisation: the interior point
+    // diverges) refuses its own step and ends the SQP at the current iterate, whose rollout is
+    // s.xs; the step's status is then that of the QPs before it -- the kinematic SQP's rule
+    // (kin_merit.hip) and oracle/dyn_sqp.py alike.  (Applying the unconverged iterate and
+    // reporting the whole step non-solved threw away a plan from converged QPs: the
+    // single-track N = 60 obstacle run on the shoe track lost the car, scripts/band_trace.py.)
+    if (ST_KEEP_ITERATE && sq > 0 && !conv) break;
     all_conv = all_conv && conv;
     any_fail = any_fail || fail;
 

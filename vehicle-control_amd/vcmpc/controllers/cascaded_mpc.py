@@ -33,6 +33,24 @@ IUX, IS = 0, 4
 IFX, IW = 0, 1
 
 
+# With the obstacle barrier on, one control step takes at least DYN_OBS_SQP SQP iterations (the
+# kinematic controller's KIN_OBS_SQP, kinematic_mpc.py here): the barrier's curvature changes
+# quickly along the plan, and at the configs' 3-5 iterations the recorded obstacle runs of the
+# reference were not driven like IPOPT drives them (r04, tests/test_gpu_bands.py: cascaded
+# obstacles2 no lap in 502 steps at 5, lap in 458 vs the recorded 464 at 10; single-track N = 60
+# on the shoe track 7 non-solved steps at 5, 3 at 10; scripts/band_settings.py).
+DYN_OBS_SQP = 10
+
+
+def dyn_qp_block(config) -> dict:
+    """The dynamic controllers' `qp` block: the config's own, with at least DYN_OBS_SQP SQP
+    iterations per step when obstacles are on."""
+    qp = dict(config.get("qp") or {})
+    if config.get("obstacles"):
+        qp["sqp_iters"] = max(int(qp.get("sqp_iters", 0)), DYN_OBS_SQP)
+    return qp
+
+
 def dyn_horizon_params(s0, ux_pred, mpc_dt, k_of_s):
     """``_init_horizon`` for horizon_pm = 0 (cascaded_mpc.py:323-330), batched.
 
@@ -66,7 +84,8 @@ class BatchedSingleTrackMPC(Controller):
         self.np_dtype = np.float64 if dtype == "f64" else np.float32
         vdt = _abi.VC_F64 if dtype == "f64" else _abi.VC_F32
         self.ctx = Context(model=_abi.VC_MODEL_DYNAMIC, N=self.N, max_batch=self.B, dtype=vdt, device=device,
-                           params=make_params(dyn_car=car.config, dyn_mpc=config, tyre=getattr(car, "tyre", "fiala"),
+                           params=make_params(dyn_car=car.config, dyn_mpc=dict(config, qp=dyn_qp_block(config)),
+                                              tyre=getattr(car, "tyre", "fiala"),
                                               obstacles=obstacle_list(car, config)))
         # warm starts: cascaded_mpc.py:72-76
         rng = np.random.RandomState(seed) if seed is not None else np.random
@@ -138,7 +157,8 @@ class BatchedCascadedMPC(Controller):
         self.B = int(batch)
         self.ctx = Context(model=_abi.VC_MODEL_CASCADED, N=self.N, max_batch=self.B, dtype=_abi.VC_F64,
                            device=device,
-                           params=make_params(dyn_car=car.config, dyn_mpc=config, tyre=getattr(car, "tyre", "fiala"),
+                           params=make_params(dyn_car=car.config, dyn_mpc=dict(config, qp=dyn_qp_block(config)),
+                                              tyre=getattr(car, "tyre", "fiala"),
                                               obstacles=obstacle_list(car, config)))
         # warm starts: cascaded_mpc.py:72-76 (ones over H columns, Ux + 3 on the single-track part)
         rng = np.random.RandomState(seed) if seed is not None else np.random

@@ -58,8 +58,9 @@ class BatchedRacingSimulator:
         self.mpc_dt = float(cfg["mpc_dt"])
         self.dt = float(car.dt)
         if self.dynamic:
-            params = make_params(dyn_car=car.config, dyn_mpc=cfg, tyre=getattr(car, "tyre", "fiala"),
-                                 obstacles=obstacle_list(track, cfg))
+            from .controllers.cascaded_mpc import dyn_qp_block  # obstacles: DYN_OBS_SQP iterations
+            params = make_params(dyn_car=car.config, dyn_mpc=dict(cfg, qp=dyn_qp_block(cfg)),
+                                 tyre=getattr(car, "tyre", "fiala"), obstacles=obstacle_list(track, cfg))
             if self.M > 0:  # cascaded SQP, fp64 (csrc/casc_ric.hip)
                 model, dtype = _abi.VC_MODEL_CASCADED, _abi.VC_F64
             else:
