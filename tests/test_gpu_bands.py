@@ -146,6 +146,9 @@ RUNS_R4 = _runs_r4()
 XFAIL_R4 = {
     "cascaded_obstacles1_ippodromo:cascaded": "median Ux 12.2-12.5 vs recorded 13.23 m/s (bar 0.5); lap 518 vs 517 steps",
     "cascaded_obstacles_shoe:cascaded": "median Ux 14.05-14.10 vs recorded 13.49 m/s (bar 0.5); lap 998-1001 vs 1026 steps",
+    # the recorded car drove through the obstacle (1.48 m inside it); ours goes round it (0.95 m clear)
+    "race_obstacles_shoe:singletrack": "s after 972 steps 663.4 vs recorded 687.4 m (3.5 %, bar 3 %); recorded car "
+                                       "1.48 m inside an obstacle, ours 0.95 m clear of it",
 }
 
 
