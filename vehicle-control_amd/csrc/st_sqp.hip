@@ -132,6 +132,15 @@ struct StSmem {
 // Workgroup = one wavefront: LDS operations of a wave execute in order, so a sync only has to
 // stop the compiler from moving memory operations across it (no s_barrier, and no wait for
 // outstanding loads other than the ones actually used).
+#ifndef ST_NEWTON_ROLLOUT
+#define ST_NEWTON_ROLLOUT 1  // after a QP step: chord-Newton rollout from the pre-step trajectory (0: serial)
+#endif
+#ifndef ST_NEWTON_FROM_SQ
+#define ST_NEWTON_FROM_SQ 1  // from the second QP step on (the first, from the warm start, is the largest)
+#endif
+#ifndef ST_NEWTON_MAX
+#define ST_NEWTON_MAX 12
+#endif
 #ifndef ST_RES_RECUR
 #define ST_RES_RECUR 1  // dual residual carried by the steps (0: adjoint sweep every iteration)
 #endif
@@ -311,32 +320,125 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     const vc_dyn_mpc& W = A.w;
     DynCoef<double> c = A.car;
     c.tyre = TYRE;
-    // ---------------- predict (lane 0, serial RK4): xs = rollout(ubar) ----------------
-    // the only rollout site (a second one makes the compiler outline it and spill);
+    // ---------------- predict: xs = rollout(ubar) ----------------
+    // Serial: lane 0 walks the stages (RK4, algebraic tan-alpha form).  After a QP step
+    // (tries == 1, ST_NEWTON_ROLLOUT, linear tyre) the new rollout is found instead by chord-Newton
+    // sweeps from the pre-step trajectory, whose Jacobians A_k are still in s.J: every lane
+    // evaluates its own stage, F(x_k, u_k) -> defect c_k = F_y - y_{k+1} (6 lateral/longitudinal
+    // states; s and t do not enter F and are prefix sums of their increments), then lanes 0..5
+    // sweep delta_{k+1} = c_k + A_k delta_k, y_{k+1} += delta_{k+1}.  Accepted when every defect is
+    // below 1e-13 (1 + |y|): the same trajectory as the serial rollout to rounding, at the cost of
+    // one RK4 step per sweep instead of N - 1; otherwise (not converged in ST_NEWTON_MAX sweeps,
+    // non-finite) the serial rollout runs.  The chord iteration converges linearly at a rate set by
+    // the step's size (scripts/newton_rollout_study.py: 3-10 sweeps for the linear tyre's SQP
+    // steps; the Fiala tyre's saturation often needs more, so it keeps the serial rollout).
+    // One RK4 call site for both modes (a second one makes the compiler outline it and spill).
     // flag[1]: finite, flag[2]: inside the spatial model's domain (Ux > 0, s' > 0)
     ST_STAMP(t_p0)
-    if (l == 0) {
-      double x[8];
+    {
+      bool newton = ST_NEWTON_ROLLOUT && TYRE == VC_TYRE_LINEAR && tries == 1 && sq >= ST_NEWTON_FROM_SQ;
+      double* scr = &s.u.l.trow[0][0];  // defects / increments [N-1][8]: dead between the IPM and the linearisation
+      for (int nit = 0;; ++nit) {
+        double x[8];
+        bool fin = true, dom = true;
+        double err = 0.0;
+        const bool act = newton ? (l < N - 1) : (l == 0);
+        const int kk0 = newton ? (l < N - 1 ? l : 0) : 0;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) x[i] = s.xs[0][i];
-      bool fin = true, dom = dyn_in_domain(x, s.kap[0]);
-      for (int kk = 0; kk < N - 1; ++kk) {
-        const double u2[2] = {s.ub[kk][0], s.ub[kk][1]};
-        const double kp = s.kap[kk];
-        double xn[8];
-        const double th = dyn_fx_split(u2[0]);  // one tanh per step, not per evaluation
-        rk4_apply<double, 8>(x, s.dsv[kk], [&](const double* xx, double* f) { dyn_spatial_ode_alg_th<double, double>(xx, u2, th, kp, c, f); }, xn);
+        for (int i = 0; i < 8; ++i) x[i] = s.xs[kk0][i];
+        if (!newton) dom = dyn_in_domain(x, s.kap[0]);
+        const int nsteps = newton ? 1 : N - 1;
+        if (act) {
+          for (int st = 0; st < nsteps; ++st) {
+            const int kk = newton ? kk0 : st;
+            const double u2[2] = {s.ub[kk][0], s.ub[kk][1]};
+            const double kp = s.kap[kk];
+            double xn[8];
+            const double th = dyn_fx_split(u2[0]);  // one tanh per step, not per evaluation
+            rk4_apply<double, 8>(x, s.dsv[kk], [&](const double* xx, double* f) { dyn_spatial_ode_alg_th<double, double>(xx, u2, th, kp, c, f); }, xn);
+            if (newton) {
+              constexpr int yr[6] = {0, 1, 2, 3, 5, 6};
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          x[i] = xn[i];
-          s.xs[kk + 1][i] = xn[i];
-          fin = fin && isfinite(xn[i]);
+              for (int r = 0; r < 6; ++r) {
+                const double yn = s.xs[kk + 1][yr[r]];
+                const double cd = xn[yr[r]] - yn;
+                scr[kk * 8 + r] = cd;
+                err = fmax(err, fabs(cd) / (1.0 + fabs(yn)));
+              }
+              scr[kk * 8 + 6] = xn[4] - x[4];
+              scr[kk * 8 + 7] = xn[7] - x[7];
+#pragma unroll
+              for (int i = 0; i < 8; ++i) fin = fin && isfinite(xn[i]);
+            } else {
+#pragma unroll
+              for (int i = 0; i < 8; ++i) {
+                x[i] = xn[i];
+                s.xs[kk + 1][i] = xn[i];
+                fin = fin && isfinite(xn[i]);
+              }
+              dom = dom && dyn_in_domain(x, s.kap[kk + 1]);
+            }
+          }
         }
-        dom = dom && dyn_in_domain(x, s.kap[kk + 1]);
+        if (!newton) {
+          if (l == 0) {
+            s.flag[1] = fin ? 1 : 0;
+            s.flag[2] = (fin && dom) ? 1 : 0;
+            if (first && !fin) s.flag[0] = VC_NONFINITE;
+          }
+          break;
+        }
+        WSYNC();
+        const bool allfin = __all(fin ? 1 : 0) != 0;
+        err = wmax(err);
+        if (allfin && err <= 1e-13) {
+          // converged: s and t as prefix sums of the stage increments, domain test in parallel
+          if (l == 0) {
+            double sv = s.xs[0][4], tv = s.xs[0][7];
+            for (int kk = 0; kk < N - 1; ++kk) {
+              sv += scr[kk * 8 + 6];
+              tv += scr[kk * 8 + 7];
+              s.xs[kk + 1][4] = sv;
+              s.xs[kk + 1][7] = tv;
+            }
+          }
+          WSYNC();
+          bool ok = true, fn = true;
+          if (l < N) {
+            double xk[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+              xk[i] = s.xs[l][i];
+              fn = fn && isfinite(xk[i]);
+            }
+            ok = fn && dyn_in_domain(xk, s.kap[l]);
+          }
+          const bool allf = __all(fn ? 1 : 0) != 0, allok = __all(ok ? 1 : 0) != 0;
+          if (l == 0) {
+            s.flag[1] = allf ? 1 : 0;
+            s.flag[2] = (allf && allok) ? 1 : 0;
+          }
+          break;
+        }
+        if (!allfin || nit + 1 >= ST_NEWTON_MAX) {
+          newton = false;  // the serial rollout (from s.xs[0], which the sweeps never change)
+          continue;
+        }
+        // chord sweep over the stages, lanes 0..5 own the six y-components of delta
+        {
+          constexpr int yr[6] = {0, 1, 2, 3, 5, 6};
+          const int r = l < 6 ? l : 0;
+          double d = 0.0;
+          for (int kk = 0; kk < N - 1; ++kk) {
+            double acc = scr[kk * 8 + r];
+#pragma unroll
+            for (int cc = 0; cc < 6; ++cc) acc += s.J[kk][r][cc] * bcast(d, cc);
+            d = acc;
+            if (l < 6) s.xs[kk + 1][yr[r]] += d;
+          }
+        }
+        WSYNC();
       }
-      s.flag[1] = fin ? 1 : 0;
-      s.flag[2] = (fin && dom) ? 1 : 0;
-      if (first && !fin) s.flag[0] = VC_NONFINITE;
     }
     WSYNC();
     ST_ACC(ST_PRED, t_p0)
