@@ -151,3 +151,50 @@ def test_st_sqp_n60_batch_nonsolved_are_infeasible(dyn_params):
         assert (first >= 0).all() and farkas.all()
     ok = st == 0
     assert np.isfinite(us[ok]).all()
+
+
+def test_st_sqp_newton_rollout_is_the_rollout():
+    """Round 4: after the second QP step the linear-tyre kernel re-rolls the plan by chord-Newton
+    sweeps from the pre-step trajectory (st_sqp.hip ST_NEWTON_ROLLOUT).  Its x* must be the serial
+    rollout of u* (vc_rollout, one lane walking the stages) up to the accepted defects (1e-14
+    relative per stage) carried through the dynamics, on a C3-sized batch at 3 and at 10 SQP
+    iterations (more Newton rollouts).  Measured at a 1e-13 acceptance: 1.4e-13 and 3.0e-10 (the
+    low-speed lateral mode amplifies a stage defect); the bar, 1e-9, is 4 orders below X_TOL."""
+    from vcmpc import Context, _abi
+    from vcmpc.config import load_config, make_params
+    from vcmpc.workload import dynamic_batch
+    B = 4096
+    d = {k: v.astype(np.float64) for k, v in dynamic_batch(B, N=40, seed=78).items()}
+    for sqp in (3, 10):
+        cfg = load_config("dynamic_mpc")
+        cfg["qp"] = dict(cfg["qp"], sqp_iters=sqp)
+        with _ctx(40, cfg, "linear", max_batch=B) as ctx:
+            u0, xs, us, st, it = ctx.solve(d["x0"], d["kappa"], d["ds"], d["ubar"].copy())
+            xr = ctx.rollout(d["x0"], us, d["kappa"], d["ds"])[:, :40]
+        rel = np.abs(xs - xr).max(axis=(1, 2)) / (1.0 + np.abs(xr).max(axis=(1, 2)))
+        print(f"sqp {sqp}: solved {(st == 0).mean():.4f}, |x* - rollout(u*)| / scale max {rel.max():.2e}")
+        assert (st == 0).all()
+        assert rel.max() < 1e-9
+
+
+def test_st_sqp_low_speed_obstacles_converge():
+    """Round 4: the reference's RK4 step is unstable in the lateral mode at low speed (|eig A_k| 3-5
+    at Ux = 4 m/s, Fx = 0), so the open-loop dual-residual sweep amplified rounding ~1e30 over 60
+    stages once an obstacle's barrier gradient excited that mode and the interior point never met
+    its tolerance (every step of the recorded shoe obstacle run failed).  With the residual through
+    the closed-loop A + BK the first step from the recorded start (Ux = 4, s = 1, neutral warm
+    start, N = 60, shoe's 9 obstacles) solves, with and without obstacles, on both tracks."""
+    from vcmpc.config import load_config, obstacle_list
+    from vcmpc.controllers.cascaded_mpc import dyn_horizon_params
+    from vcmpc.environment import Track
+    x0 = np.array([[4.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0]])
+    for name in ("shoe", "ippodromo"):
+        tr = Track.load(name)
+        for obs in (True, False):
+            cfg = load_config("singletrack_mpc")
+            cfg["horizon"], cfg["obstacles"] = 60, obs
+            ds, kap = dyn_horizon_params(x0[:, 4], np.full((1, 60), 4.0), float(cfg["mpc_dt"]), tr.k)
+            with _ctx(60, cfg, "fiala", max_batch=1, obstacles=obstacle_list(tr, cfg)) as ctx:
+                u0, xs, us, st, it, dg = ctx.solve(x0, kap, ds, np.zeros((1, 60, 2)), diag=True)
+            print(f"{name} obstacles={obs}: status {int(st[0])}, iterations {int(it[0])}, diag {np.round(dg[0], 9)}")
+            assert st[0] == 0

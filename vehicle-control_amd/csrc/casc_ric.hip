@@ -86,7 +86,7 @@ struct CrJ {  // [A6 | B6 diag(S, 1 or S)] of one transition + 1 pad (49 doubles
 template <int N, int M>
 struct CrSmem {
   static constexpr int H = N + M;
-  double xs[H][8];    // prediction: single-track states k < N, point-mass (V, s, ey, epsi, t) k >= N
+  StageRows8<H> xs;   // prediction: single-track states k < N, point-mass (V, s, ey, epsi, t) k >= N (rotated rows)
   double ub[H][2];    // current ubar (stride 2: the odd stride 3 cost M = 40 its third workgroup per CU)
   double kap[H], dsv[H];
   CrJ J[H];           // J[k][row][col]: [A6 | B6 diag(S, 1 or S)] of the transition out of stage k
@@ -247,9 +247,9 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     s.ub[i][0] = A.ubar[((size_t)b * H + i) * 2];
     s.ub[i][1] = A.ubar[((size_t)b * H + i) * 2 + 1];
   }
-  if (l < 8) s.xs[0][l] = A.x0[(size_t)b * 8 + l];
+  if (l < 8) s.xs.at(0, l) = A.x0[(size_t)b * 8 + l];
   if (l >= N && l < H) {  // point-mass slots 5..7 are reported as 0 (free in the reference's NLP)
-    s.xs[l][5] = s.xs[l][6] = s.xs[l][7] = 0.0;
+    s.xs.at(l, 5) = s.xs.at(l, 6) = s.xs.at(l, 7) = 0.0;
   }
   if (l == 0) {
     s.flag[0] = VC_SOLVED;
@@ -284,7 +284,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       c.tyre = TYRE;
       double x[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) x[i] = s.xs[0][i];
+      for (int i = 0; i < 8; ++i) x[i] = s.xs.at(0, i);
       bool fin = true, dom = dyn_in_domain(x, s.kap[0]);
       for (int kk = 0; kk < N - 1; ++kk) {
         const double u2[2] = {s.ub[kk][0], s.ub[kk][1]};
@@ -295,7 +295,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           x[i] = xn[i];
-          s.xs[kk + 1][i] = xn[i];
+          s.xs.at(kk + 1, i) = xn[i];
           fin = fin && isfinite(xn[i]);
         }
         dom = dom && dyn_in_domain(x, s.kap[kk + 1]);
@@ -303,7 +303,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       double p[5];
       st_to_pm<double>(x, p);  // cascaded_mpc.py:256-277
 #pragma unroll
-      for (int i = 0; i < 5; ++i) s.xs[N][i] = p[i];
+      for (int i = 0; i < 5; ++i) s.xs.at(N, i) = p[i];
       dom = dom && pm_in_domain(p, s.kap[N]);
       for (int j = N; j < H - 1; ++j) {  // dynamic_point_mass.py:76-100, Euler
         const double u2[2] = {s.ub[j][0], s.ub[j][1]};
@@ -313,7 +313,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
           p[i] = p[i] + h * f[i];
-          s.xs[j + 1][i] = p[i];
+          s.xs.at(j + 1, i) = p[i];
           fin = fin && isfinite(p[i]);
         }
         dom = dom && pm_in_domain(p, s.kap[j + 1]);
@@ -362,7 +362,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
           D1 x[8], u2[2], xn[8];
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
-            x[i] = D1(s.xs[kk][i]);
+            x[i] = D1(s.xs.at(kk, i));
             x[i].d[0] = i == a0 ? 1.0 : 0.0;
           }
           u2[0] = D1(s.ub[kk][0]);
@@ -385,7 +385,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
           const int q = task, kk = q / 5, j = q % 5;
           D1 X5[5], o[7];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) X5[i] = D1(s.xs[kk][i]);
+          for (int i = 0; i < 4; ++i) X5[i] = D1(s.xs.at(kk, i));
           X5[4] = D1(s.ub[kk][0]);
 #pragma unroll
           for (int i = 0; i < 5; ++i) X5[i].d[0] = i == j ? 1.0 : 0.0;
@@ -405,7 +405,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
           const int a0 = pr == 0 ? 0 : (pr == 1 ? 3 : -1), a1 = pr == 0 ? 2 : -1;
 #pragma unroll
           for (int i = 0; i < 5; ++i) {
-            x[i] = D2(s.xs[j][i]);
+            x[i] = D2(s.xs.at(j, i));
             x[i].d[0] = i == a0 ? 1.0 : 0.0;
             x[i].d[1] = i == a1 ? 1.0 : 0.0;
           }
@@ -461,7 +461,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       c.tyre = TYRE;
       D1 X5[5];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) X5[i] = D1(s.xs[N - 1][i]);
+      for (int i = 0; i < 4; ++i) X5[i] = D1(s.xs.at(N - 1, i));
       X5[4] = D1(s.ub[N - 1][0]);
 #pragma unroll
       for (int i = 0; i < 5; ++i) X5[i].d[0] = i == l ? 1.0 : 0.0;
@@ -469,7 +469,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       s.u.l.gfy[1 + l] = fy.d[0];
       if (l == 0) s.u.l.gfy[0] = fy.v;
     } else if (l == 5) {
-      const double Ux = s.xs[N - 1][0], Uy = s.xs[N - 1][1];
+      const double Ux = s.xs.at(N - 1, 0), Uy = s.xs.at(N - 1, 1);
       const double q2 = Ux * Ux + Uy * Uy, V = sqrt(q2);
 #pragma unroll
       for (int r = 0; r < 6; ++r)
@@ -505,7 +505,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       const double Peng = kargs<CascSqpArgs>()->car.Peng;
       const double ds = s.dsv[k];
       // ey / s slots of this stage's state
-      const double ey = pm ? s.xs[k][2] : s.xs[k][5], sa = pm ? s.xs[k][1] : s.xs[k][4];
+      const double ey = pm ? s.xs.at(k, 2) : s.xs.at(k, 5), sa = pm ? s.xs.at(k, 1) : s.xs.at(k, 4);
       const double wdev = pm ? CW.w_dev_pm : W.w_dev, eylo = pm ? CW.ey_min_pm : W.ey_min,
                    eyhi = pm ? CW.ey_max_pm : W.ey_max;
       // boundary + deviation (cascaded_mpc.py:139-151, point mass :204-219), obstacles (:173-176)
@@ -580,7 +580,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       }
       // terminal on the last point-mass state (:279-304)
       if (k == H - 1) {
-        const double V = s.xs[k][0];
+        const double V = s.xs.at(k, 0);
         if (V >= W.max_speed) {
           Qc[Q00] += 2.0 * W.w_speed;
           qc[0] += 2.0 * W.w_speed * (V - W.max_speed);
@@ -588,7 +588,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
         Qc[Q11] += 2.0 * W.w_ey;
         qc[1] += 2.0 * W.w_ey * ey;
         Qc[Q22] += 2.0 * W.w_epsi;
-        qc[2] += 2.0 * W.w_epsi * s.xs[k][3];
+        qc[2] += 2.0 * W.w_epsi * s.xs.at(k, 3);
       }
       // rows (:101-128, point mass :190-195, trust region)
       const double on = stl ? 1.0 : 0.0;
@@ -598,9 +598,9 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
         for (int a = 0; a < 5; ++a) R.c[r][a] = 0.0;
       if (!pm) {
         const double mk = (stl && k >= 1) ? 1.0 : 0.0;
-        R.d[0] = s.xs[k][0] - W.Ux_min;
-        R.d[1] = W.delta_max - s.xs[k][3];
-        R.d[2] = s.xs[k][3] - W.delta_min;
+        R.d[0] = s.xs.at(k, 0) - W.Ux_min;
+        R.d[1] = W.delta_max - s.xs.at(k, 3);
+        R.d[2] = s.xs.at(k, 3) - W.delta_min;
         R.set(0, mk > 0.0); R.set(1, mk > 0.0); R.set(2, mk > 0.0);
 #pragma unroll
         for (int r = 0; r < 5; ++r) {
@@ -621,7 +621,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
         R.d[9] = dn;
         R.set(8, on > 0.0); R.set(9, on > 0.0);
       } else {
-        const double V = s.xs[k][0];
+        const double V = s.xs.at(k, 0);
         R.d[0] = V - CW.V_min;
         R.set(0, on > 0.0);
         R.d[1] = R.d[2] = 1.0;
@@ -1070,7 +1070,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     A.u_out[(size_t)b * 2 * H + e] = v;
   }
   for (int e = l; e < 8 * H; e += WTH) {
-    const double v = s.xs[e >> 3][e & 7];
+    const double v = s.xs.at(e >> 3, e & 7);
     finite = finite && isfinite(v);
     A.x_out[(size_t)b * 8 * H + e] = v;
   }

@@ -85,16 +85,14 @@ struct StJT {
 };
 template <int N>
 using StJ = StJT<(N == 30 || N == 60) ? 8 : 9>;
-// Row strides of xs / ub: odd (9, 3; conflict-free lane-per-stage reads) where the LDS allows;
-// N = 60 takes 8 / 2 -- a block above 53,248 B leaves two workgroups per CU instead of three
-// (measured: rocprofv3 LDS_Block_Size 53,248 ran three per CU, 54,272 two; r04)
-template <int N>
-constexpr int st_xs_w() { return N == 60 ? 8 : 9; }
+// Row stride of ub: odd (3; conflict-free lane-per-stage reads) where the LDS allows, N = 60 takes
+// 2 -- a block above 53,248 B leaves two workgroups per CU instead of three (measured: rocprofv3
+// LDS_Block_Size 53,248 ran three per CU, 54,272 two; r04).  xs: rotated rows of 8 (StageRows8)
 template <int N>
 constexpr int st_ub_w() { return N == 60 ? 2 : 3; }
 template <int N>
 struct StSmem {
-  double xs[N][st_xs_w<N>()];  // prediction (N columns, dynamics for k < N-1); [8] pad where 9
+  StageRows8<N> xs;   // prediction (N columns, dynamics for k < N-1), rotated rows (vc_kernels.hpp)
   double ub[N][st_ub_w<N>()];  // current ubar; [2] pad where 3
   double kap[N], dsv[N];
   StJ<N> J[N];         // J[k][row][col], cols Ux, Uy, r, delta, ey, epsi | dFx, dw
@@ -137,6 +135,9 @@ struct StSmem {
 #endif
 #ifndef ST_NEWTON_FROM_SQ
 #define ST_NEWTON_FROM_SQ 1  // from the second QP step on (the first, from the warm start, is the largest)
+#endif
+#ifndef ST_NEWTON_TOL
+#define ST_NEWTON_TOL 1e-14  // accepted defect, relative to 1 + |y|
 #endif
 #ifndef ST_NEWTON_MAX
 #define ST_NEWTON_MAX 12
@@ -269,7 +270,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     s.ub[i][0] = A.ubar[((size_t)b * N + i) * 2];
     s.ub[i][1] = A.ubar[((size_t)b * N + i) * 2 + 1];
   }
-  if (l < 8) s.xs[0][l] = A.x0[(size_t)b * 8 + l];
+  if (l < 8) s.xs.at(0, l) = A.x0[(size_t)b * 8 + l];
   if (l == 0) s.flag[0] = VC_SOLVED;
 #ifdef VC_TIMING
   uint64_t tacc[ST_NSLOT] = {};
@@ -327,8 +328,9 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     // evaluates its own stage, F(x_k, u_k) -> defect c_k = F_y - y_{k+1} (6 lateral/longitudinal
     // states; s and t do not enter F and are prefix sums of their increments), then lanes 0..5
     // sweep delta_{k+1} = c_k + A_k delta_k, y_{k+1} += delta_{k+1}.  Accepted when every defect is
-    // below 1e-13 (1 + |y|): the same trajectory as the serial rollout to rounding, at the cost of
-    // one RK4 step per sweep instead of N - 1; otherwise (not converged in ST_NEWTON_MAX sweeps,
+    // below ST_NEWTON_TOL (1 + |y|): the serial rollout's trajectory up to those defects carried
+    // through the dynamics (measured <= 3e-10 relative at 1e-13, tests/test_gpu_st_sqp.py), at the
+    // cost of one RK4 step per sweep instead of N - 1; otherwise (not converged in ST_NEWTON_MAX sweeps,
     // non-finite) the serial rollout runs.  The chord iteration converges linearly at a rate set by
     // the step's size (scripts/newton_rollout_study.py: 3-10 sweeps for the linear tyre's SQP
     // steps; the Fiala tyre's saturation often needs more, so it keeps the serial rollout).
@@ -345,7 +347,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
         const bool act = newton ? (l < N - 1) : (l == 0);
         const int kk0 = newton ? (l < N - 1 ? l : 0) : 0;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) x[i] = s.xs[kk0][i];
+        for (int i = 0; i < 8; ++i) x[i] = s.xs.at(kk0, i);
         if (!newton) dom = dyn_in_domain(x, s.kap[0]);
         const int nsteps = newton ? 1 : N - 1;
         if (act) {
@@ -360,7 +362,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
               constexpr int yr[6] = {0, 1, 2, 3, 5, 6};
 #pragma unroll
               for (int r = 0; r < 6; ++r) {
-                const double yn = s.xs[kk + 1][yr[r]];
+                const double yn = s.xs.at(kk + 1, yr[r]);
                 const double cd = xn[yr[r]] - yn;
                 scr[kk * 8 + r] = cd;
                 err = fmax(err, fabs(cd) / (1.0 + fabs(yn)));
@@ -373,7 +375,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
 #pragma unroll
               for (int i = 0; i < 8; ++i) {
                 x[i] = xn[i];
-                s.xs[kk + 1][i] = xn[i];
+                s.xs.at(kk + 1, i) = xn[i];
                 fin = fin && isfinite(xn[i]);
               }
               dom = dom && dyn_in_domain(x, s.kap[kk + 1]);
@@ -391,15 +393,15 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
         WSYNC();
         const bool allfin = __all(fin ? 1 : 0) != 0;
         err = wmax(err);
-        if (allfin && err <= 1e-13) {
+        if (allfin && err <= ST_NEWTON_TOL) {
           // converged: s and t as prefix sums of the stage increments, domain test in parallel
           if (l == 0) {
-            double sv = s.xs[0][4], tv = s.xs[0][7];
+            double sv = s.xs.at(0, 4), tv = s.xs.at(0, 7);
             for (int kk = 0; kk < N - 1; ++kk) {
               sv += scr[kk * 8 + 6];
               tv += scr[kk * 8 + 7];
-              s.xs[kk + 1][4] = sv;
-              s.xs[kk + 1][7] = tv;
+              s.xs.at(kk + 1, 4) = sv;
+              s.xs.at(kk + 1, 7) = tv;
             }
           }
           WSYNC();
@@ -408,7 +410,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
             double xk[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
-              xk[i] = s.xs[l][i];
+              xk[i] = s.xs.at(l, i);
               fn = fn && isfinite(xk[i]);
             }
             ok = fn && dyn_in_domain(xk, s.kap[l]);
@@ -421,7 +423,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
           break;
         }
         if (!allfin || nit + 1 >= ST_NEWTON_MAX) {
-          newton = false;  // the serial rollout (from s.xs[0], which the sweeps never change)
+          newton = false;  // the serial rollout (from state 0, which the sweeps never change)
           continue;
         }
         // chord sweep over the stages, lanes 0..5 own the six y-components of delta
@@ -434,7 +436,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
 #pragma unroll
             for (int cc = 0; cc < 6; ++cc) acc += s.J[kk][r][cc] * bcast(d, cc);
             d = acc;
-            if (l < 6) s.xs[kk + 1][yr[r]] += d;
+            if (l < 6) s.xs.at(kk + 1, yr[r]) += d;
           }
         }
         WSYNC();
@@ -480,7 +482,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
           D2 x[8], u2[2], xn[8];
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
-            x[i] = D2(s.xs[kk][i]);
+            x[i] = D2(s.xs.at(kk, i));
             x[i].d[0] = i == a0 ? 1.0 : 0.0;
             x[i].d[1] = i == a1 ? 1.0 : 0.0;
           }
@@ -506,7 +508,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
           const int q = task - NLIN, kk = q / 5, j = q % 5;
           D1 X5[5], o[7];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) X5[i] = D1(s.xs[kk][i]);
+          for (int i = 0; i < 4; ++i) X5[i] = D1(s.xs.at(kk, i));
           X5[4] = D1(s.ub[kk][0]);
 #pragma unroll
           for (int i = 0; i < 5; ++i) X5[i].d[0] = i == j ? 1.0 : 0.0;
@@ -532,7 +534,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     for (int e = 0; e < 9; ++e) qc[e] = 0.0;
     {
       const double ds = s.dsv[k];
-      const double ey = s.xs[k][5];
+      const double ey = s.xs.at(k, 5);
       // boundary + deviation (cascaded_mpc.py:139-151), obstacle barrier (:173-176) in ey
       const double cdev = W.w_dev * ds;
       const double blo = ey < W.ey_min ? W.w_b * ds : 0.0, bhi = ey > W.ey_max ? W.w_b * ds : 0.0;
@@ -540,7 +542,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       qc[4] += 2.0 * (cdev * ey + blo * (ey - W.ey_min) + bhi * (ey - W.ey_max));
       if (A.obs.n > 0) {
         double po, qo;
-        obstacle_ey_model<double>(A.obs, s.xs[k][4], ey, W.w_obs * ds, po, qo);
+        obstacle_ey_model<double>(A.obs, s.xs.at(k, 4), ey, W.w_obs * ds, po, qo);
         Qc[Q44] += qo;
         qc[4] += po;
       }
@@ -581,7 +583,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       }
       // terminal (:290-303)
       if (k == N - 1) {
-        const double Ux = s.xs[k][0];
+        const double Ux = s.xs.at(k, 0);
         if (Ux >= W.max_speed) {
           Qc[Q00] += 2.0 * W.w_speed;
           qc[0] += 2.0 * W.w_speed * (Ux - W.max_speed);
@@ -589,13 +591,13 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
         Qc[Q44] += 2.0 * W.w_ey;
         qc[4] += 2.0 * W.w_ey * ey;
         Qc[Q55] += 2.0 * W.w_epsi;
-        qc[5] += 2.0 * W.w_epsi * s.xs[k][6];
+        qc[5] += 2.0 * W.w_epsi * s.xs.at(k, 6);
       }
       // rows (:101-128, trust region)
       const double mk = (stl && k >= 1) ? 1.0 : 0.0;
-      R.d[0] = s.xs[k][0] - W.Ux_min;
-      R.d[1] = W.delta_max - s.xs[k][3];
-      R.d[2] = s.xs[k][3] - W.delta_min;
+      R.d[0] = s.xs.at(k, 0) - W.Ux_min;
+      R.d[1] = W.delta_max - s.xs.at(k, 3);
+      R.d[2] = s.xs.at(k, 3) - W.delta_min;
       R.m[0] = R.m[1] = R.m[2] = mk;
 #pragma unroll
       for (int r = 0; r < 5; ++r) {
@@ -1083,7 +1085,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     A.u_out[(size_t)b * 2 * N + e] = v;
   }
   for (int e = l; e < 8 * N; e += WTH) {
-    const double v = s.xs[e >> 3][e & 7];
+    const double v = s.xs.at(e >> 3, e & 7);
     finite = finite && isfinite(v);
     A.x_out[(size_t)b * 8 * N + e] = v;
   }

@@ -105,6 +105,20 @@ __device__ __forceinline__ void obstacle_ey_model(const vc_obstacles& o, T s, T 
   q = qs > T(0) ? qs : T(0);
 }
 
+// Per-stage state rows of the Riccati SQP kernels (st_sqp.hip, casc_ric.hip): 8 doubles a row, row k
+// rotated by k / 4 (element i of row k in slot (i + k / 4) mod 8).  A lane-per-stage read of one
+// element then hits 32 distinct bank pairs over a 32-lane ds_read_b64 group (dword address
+// 16 k + 2 ((i + k / 4) mod 8) mod 64: k mod 4 and k / 4 mod 8 both vary), where the plain stride of
+// 8 doubles put lanes k and k + 4 on the same banks (8-way) and an odd stride of 9 costs a ninth
+// double per stage -- at N = 60 / the cascaded H = 60 the difference between three workgroups per
+// CU and two.
+template <int R>
+struct StageRows8 {
+  double m[R][8];
+  __device__ __forceinline__ double& at(int k, int i) { return m[k][(i + (k >> 2)) & 7]; }
+  __device__ __forceinline__ const double& at(int k, int i) const { return m[k][(i + (k >> 2)) & 7]; }
+};
+
 // Fused kinematic LTV-MPC step (kin_ltv.hip, condensed, N = 20; kin_ric.hip, stagewise).
 struct KinLtvArgs {
   const double* x0;     // [B][6]
