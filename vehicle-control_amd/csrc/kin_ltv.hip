@@ -52,6 +52,10 @@
 #ifndef KIN_POLISH_WARM
 #define KIN_POLISH_WARM 1  // polish multipliers start from the interior point's (0: from zero, round 3)
 #endif
+#ifndef KIN_BWD_ROWS
+#define KIN_BWD_ROWS 0  // 1: backward solve reads the factor as packed rows (conflict-free reads, but the
+                        // row stores cost more: 2.8 % slower at C2, profiles/r04/kinab_r04m.txt)
+#endif
 #ifndef KIN_DOT_CH
 #define KIN_DOT_CH 8  // terms per chunk of the residual dot products
 #endif
@@ -315,6 +319,25 @@ __device__ __forceinline__ double rsq_nr(double d) {
   return inv;
 }
 
+// After a factorisation: row k of L (entries i < k) to Lc[k (k-1)/2 + i], packed rows, for the
+// backward sweep -- its lanes i then read L[k][i] at consecutive addresses (the column layout put
+// them one column apart: 4-6 way bank conflicts on every read, ~75 % of the kernel's conflict
+// cycles, r04 PMC).  Lane j stores entries i < j; the others go to the dummy slot (branch-free:
+// the compiler may reorder one lane's stores, so no store may land on another lane's entry).  The
+// factorisation's own column reads were issued before (LDS executes a wave's operations in order).
+template <int N>
+__device__ __forceinline__ void store_rows(const double (&Mr)[Dims<N>::n], Smem<N>& s, int lane) {
+#if KIN_BWD_ROWS
+  constexpr int n = Dims<N>::n;
+  static_assert(n * (n - 1) / 2 <= Smem<N>::LC_DUMMY, "packed rows fit the factor storage");
+  wave_sync();
+  const int lim = lane < n ? lane : 0;
+  const int base = lim * (lim - 1) / 2;
+#pragma unroll
+  for (int i = 0; i < n - 1; ++i) s.Lc[i < lim ? base + i : Smem<N>::LC_DUMMY] = Mr[i];
+#endif
+}
+
 // In-place right-looking Cholesky of the SPD matrix whose row `lane` is Mr (the lower
 // part: entries above the diagonal are not kept).  On return s.Lc holds the columns of L,
 // s.dinv the inverse pivots 1/L_kk (uniform reads), and Mr row `lane` of L strictly below
@@ -409,6 +432,7 @@ __device__ bool cholesky(double (&Mr)[Dims<N>::n], Smem<N>& s, int lane) {
   }
   Mr[n - 2] = lane > n - 2 ? Mr[n - 2] : 0.0;
   Mr[n - 1] = 0.0;
+  store_rows<N>(Mr, s, lane);
   wave_sync();  // factor and inverse pivots visible to the solves
   return ok;
 }
@@ -418,10 +442,11 @@ __device__ bool cholesky(double (&Mr)[Dims<N>::n], Smem<N>& s, int lane) {
 // row registers zero on and above the diagonal (cholesky), so lane k's accumulator stops
 // changing once y_k is taken and y = acc / L_kk at the end -- no per-step select (a finite
 // factor times 0 subtracts exactly 0: the same values as collecting y_k per step).  Backward
-// sweep: lane i reads L[k][i] (column i of the factor) from LDS at immediate offsets of one
-// per-lane base, prefetched one 8-step chunk ahead, and x_i is written into lane i at step i
-// by v_writelane (entries k < i of the read are the previous column's storage: after step i
-// they no longer matter) -- cheaper than a zero-or-entry address select per element.  (A four-unknown blocked variant
+// sweep: lane i reads L[k][i] (row k of the packed rows, store_rows; or column i of the factor)
+// from LDS at immediate offsets of one per-lane base, prefetched one 8-step chunk ahead, and x_i
+// is written into lane i at step i by v_writelane (entries k <= i of the read are other rows'
+// storage: after step i they no longer matter) -- cheaper than a zero-or-entry address select
+// per element.  (A four-unknown blocked variant
 // was 13 % slower: the sweeps are bound by instruction issue, profiles/r03/section_cycles_r03g.txt.)
 template <int N>
 __device__ double chol_solve(const double (&Lr)[Dims<N>::n], const Smem<N>& s, double b, int lane) {
@@ -429,7 +454,11 @@ __device__ double chol_solve(const double (&Lr)[Dims<N>::n], const Smem<N>& s, d
   constexpr int CH = 8;
   static_assert(n % CH == 0, "backward prefetch chunks");
   const int row = lane < n ? lane : 0;
+#if KIN_BWD_ROWS
+  lds_cdouble* col = lds_opaque(&s.Lc[row]);  // col[k (k-1) / 2] = L[k][row] for k > row (store_rows)
+#else
   lds_cdouble* col = lds_opaque(&s.Lc[lc_base<n>(row)]);  // col[k] = L[k][row] for k > row
+#endif
   const double dj = s.dinv[row];
   double acc = b;
 #pragma unroll
@@ -437,6 +466,16 @@ __device__ double chol_solve(const double (&Lr)[Dims<N>::n], const Smem<N>& s, d
   acc *= dj;                                                           // y
   double x = 0.0;
   double lk[2][CH];
+#if KIN_BWD_ROWS
+  auto fetch = [&](int c, int buf) {  // L[k][row] for k = n-1-c*CH ... n-CH-c*CH
+    // lanes at or below k read the next rows' entries (finite; multiplied only after x_row is out)
+#pragma unroll
+    for (int q = 0; q < CH; ++q) {
+      const int k = n - 1 - c * CH - q;
+      lk[buf][q] = col[k * (k - 1) / 2];
+    }
+  };
+#else
   lds_cdouble* zero = lds_opaque(&s.zrow[0]);
   auto fetch = [&](int c, int buf) {  // L[k][row] for k = n-1-c*CH ... n-CH-c*CH
     // a lane whose row is at or below every k of the chunk reads zeros at one shared address
@@ -445,6 +484,7 @@ __device__ double chol_solve(const double (&Lr)[Dims<N>::n], const Smem<N>& s, d
 #pragma unroll
     for (int q = 0; q < CH; ++q) lk[buf][q] = src[n - 1 - c * CH - q];
   };
+#endif
   fetch(0, 0);
 #pragma unroll
   for (int c = 0; c < n / CH; ++c) {  // L' x = y: lane i < k needs L[k][i]
@@ -766,6 +806,7 @@ __device__ bool factor_blocked(double (&Mr)[Dims<N>::n], d4 (&acc)[Tiles<N>::NT]
       }
     }
   }
+  store_rows<N>(Mr, s, lane);
   wave_sync();  // factor and inverse pivots visible to the solves
   return ok;
 }
