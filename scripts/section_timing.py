@@ -63,3 +63,5 @@ with Context(N=20, max_batch=B, params=p) as c:
         sel = its == k
         if sel.any():
             print(f"  iters {k:2d}: {sel.sum():4d} problems, total cycles mean {tot[sel].mean():.0f} max {tot[sel].max():.0f}")
+    if os.environ.get("SEC_DUMP"):  # per-problem arrays for offline tail analysis
+        np.savez(os.environ["SEC_DUMP"], cyc=cyc, its=its, rounds=dg[:, 3], tot=tot)

@@ -56,6 +56,18 @@
 #define KIN_BWD_ROWS 0  // 1: backward solve reads the factor as packed rows (conflict-free reads, but the
                         // row stores cost more: 2.8 % slower at C2, profiles/r04/kinab_r04m.txt)
 #endif
+#ifndef KIN_POLISH_CG
+#define KIN_POLISH_CG 1  // polish equality solve: conjugate gradients on the multipliers (0: augmented-Lagrangian passes)
+#endif
+#ifndef KIN_NU_TOL
+#define KIN_NU_TOL 1e-10  // CG also runs until the multiplier step R e is below this x scale (0: off)
+#endif
+#ifndef KIN_TAPIA
+#define KIN_TAPIA 1  // polish's first active set from the last step's Tapia indicators (0: lambda > s)
+#endif
+#ifndef KIN_TAPIA_F
+#define KIN_TAPIA_F 1.02  // ratio gap that makes the indicators decisive (else lambda > s)
+#endif
 #ifndef KIN_DOT_CH
 #define KIN_DOT_CH 8  // terms per chunk of the residual dot products
 #endif
@@ -1115,6 +1127,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
   // Mehrotra iteration with the same recursion takes the same iterations on the C2 batch and its
   // true residuals end at the same 9.4e-11 / 3.5e-12 (scaled), polish certifying all 1,024.
   double rd = 0.0, rlo_b = 0.0, rhi_b = 0.0, rlo_c = 0.0, rhi_c = 0.0;
+  int tapb = 0;  // KIN_TAPIA: two bits per constraint side (1 active, 2 inactive, 0 undecided)
   if (finite) {
 #pragma unroll 1
     for (;;) {
@@ -1221,6 +1234,22 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
           pp1 = d1 * d2; pp2 = d3 * d4; pp3 = e1 * e2; pp4 = e3 * e4;
         } else {
           const double al = 0.99 * amax;
+#if KIN_TAPIA
+          {
+            // Tapia indicators of this step (El-Bakry, Tapia, Tsuchiya, Zhang 1996): near the
+            // solution an active side's slack shrinks by a factor the multiplier does not, an
+            // inactive side's multiplier the other way round -- with the interior point's loose
+            // stopping rule (mu <= 1e-10 scale) weakly active bounds still have slacks ~1e-3 above
+            // their multipliers, and lambda > s misses them (122 of the 1,024 C2 problems, each a
+            // polish round; scripts/polish_cg_study.py).  il, is: 1 / the pre-step values.
+            auto tap = [&](double dl, double il, double dsv, double is) -> int {
+              const double lr = fma(al * dl, il, 1.0), sr = fma(al * dsv, is, 1.0);
+              return lr > KIN_TAPIA_F * sr ? 1 : (sr > KIN_TAPIA_F * lr ? 2 : 0);
+            };
+            tapb = tap(d2, illo_b, d1, islo_b) | (tap(d4, ilhi_b, d3, ishi_b) << 2) |
+                   (tap(e2, illo_c, e1, islo_c) << 4) | (tap(e4, ilhi_c, e3, ishi_c) << 6);
+          }
+#endif
           z = (lane < n) ? z + al * dz : z;
           bx.slo += al * d1; bx.llo += al * d2; bx.shi += al * d3; bx.lhi += al * d4;
           cs.slo += al * e1; cs.llo += al * e2; cs.shi += al * e3; cs.lhi += al * e4;
@@ -1248,10 +1277,19 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
     constexpr double AL_RHO = 1e4;
     constexpr int AL_MAX = 16;
     const double ptol = 1e-9 * scale;
+#if KIN_TAPIA
+    // decisive indicators first, lambda > s where the last step left them undecided
+    auto guess = [&](bool has, double l, double sv, int t) { return has && (t == 1 || (t == 0 && l > sv)); };
+    bool alo_b = guess(bx.hasLo, bx.llo, bx.slo, tapb & 3);
+    bool ahi_b = guess(bx.hasHi, bx.lhi, bx.shi, (tapb >> 2) & 3);
+    bool alo_c = guess(cs.hasLo, cs.llo, cs.slo, (tapb >> 4) & 3);
+    bool ahi_c = guess(cs.hasHi, cs.lhi, cs.shi, (tapb >> 6) & 3);
+#else
     bool alo_b = bx.hasLo && bx.llo > bx.slo;
     bool ahi_b = bx.hasHi && bx.lhi > bx.shi;
     bool alo_c = cs.hasLo && cs.llo > cs.slo;
     bool ahi_c = cs.hasHi && cs.lhi > cs.shi;
+#endif
 #pragma unroll 1
     for (int round = 0; round < A.qp.polish; ++round) {
       no_hoist();
@@ -1336,6 +1374,71 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
       // to the fixed point instead of at 0 (KIN_POLISH_WARM; the fixed point does not depend on
       // the start: same certified z).  Rows the AL does not enforce (rho_c = 0) keep 0.
       double nu_c = (KIN_POLISH_WARM && act && rho_c > 0.0) ? ((ahi_c ? cs.lhi : 0.0) - (alo_c ? cs.llo : 0.0)) : 0.0;
+#if KIN_POLISH_CG
+      // The passes are Richardson's iteration nu += R e on S dnu = e(nu), S = G_A M^-1 G_A' (M the
+      // factored matrix, R = diag(rho_c)): it contracts by 1 - min eig(R S) per pass, up to 14 passes
+      // on the slowest C2 problems (profiles/r04/sec_r04f.txt).  KIN_POLISH_CG solves the same
+      // system by conjugate gradients preconditioned with R -- same cost per iteration (one
+      // triangular solve pair, one G' and one G product), same fixed point, and R S has its
+      // eigenvalues clustered below 1, so CG needs a few.  z follows nu exactly: dz = -M^-1 G' dnu.
+      const bool al_act = act && rho_c > 0.0;
+      const double bnd_al = alo_c ? cs.lo : cs.hi;
+      double zp = 0.0, emax = 0.0;
+      {
+        wave_sync();
+        s.vc[lane] = (lane < NC) ? (nu_c - rho_c * bnd_c) : 0.0;
+        wave_sync();
+        const double rhs = (lane < n) ? (fixed ? zfix : (base - gt_dot<N>(s, lane))) : 0.0;
+        zp = chol_solve<N>(Mr, s, rhs, lane);
+        wave_sync();
+        s.vz[lane] = (lane < n) ? zp : 0.0;
+        wave_sync();
+        const double yr = grow_dot<N>(s, lane);
+        double rr = al_act ? (yr - bnd_al) : 0.0;  // e(nu), the active rows' violation
+        // stop when the violation is below 1e-14 scale and (KIN_NU_TOL) the multiplier step R e
+        // below KIN_NU_TOL scale: rho_c reaches 1e10 on rows with a small free part, and a
+        // violation at rounding level then still leaves multipliers off by more than the dual
+        // check's 1e-9 scale -- the active set cycled (two C2-like problems of 4,096, seed 7)
+        const double ie = 1.0 / (1e-14 * scale), inu = KIN_NU_TOL > 0.0 ? 1.0 / (KIN_NU_TOL * scale) : 0.0;
+        auto crit = [&](double r) { return wave_max(fmax(fabs(r) * ie, fabs(rho_c * r) * inu)); };
+#ifdef VC_TIMING
+        tacc[T_PPASS] += 1;
+#endif
+        if (crit(rr) > 1.0) {
+          double pd = rho_c * rr;  // preconditioned residual = first direction
+          double rz = wave_sum(rr * pd);
+#pragma unroll 1
+          for (int it = 1; it < AL_MAX; ++it) {
+            no_hoist();
+            wave_sync();
+            s.vc[lane] = (lane < NC) ? pd : 0.0;
+            wave_sync();
+            const double gtp = gt_dot<N>(s, lane);
+            const double zq = chol_solve<N>(Mr, s, (lane < n && !fixed) ? gtp : 0.0, lane);  // M^-1 G' p
+            wave_sync();
+            s.vz[lane] = (lane < n) ? zq : 0.0;
+            wave_sync();
+            const double gq = grow_dot<N>(s, lane);
+            const double q = al_act ? gq : 0.0;  // S p on the active rows
+            const double pq = wave_sum(pd * q);
+#ifdef VC_TIMING
+            tacc[T_PPASS] += 1;
+#endif
+            if (!(pq > 0.0)) break;  // uniform: a direction S does not see (the KKT check decides)
+            const double al = rz / pq;
+            nu_c = fma(al, pd, nu_c);
+            zp = fma(-al, zq, zp);
+            rr = fma(-al, q, rr);
+            if (crit(rr) <= 1.0) break;
+            const double zt = rho_c * rr;
+            const double rzn = wave_sum(rr * zt);
+            pd = fma(rzn / rz, pd, zt);
+            rz = rzn;
+          }
+        }
+      }
+      VC_TACC(T_PAL, t_pal0)
+#else
       double zp = 0.0, emax = 0.0;
 #pragma unroll 1
       for (int pass = 0; pass < AL_MAX; ++pass) {
@@ -1360,6 +1463,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
         if (emax <= 1e-14 * scale) break;
       }
       VC_TACC(T_PAL, t_pal0)
+#endif
       // KKT check of zp
       wave_sync();
       s.vz[lane] = (lane < n) ? zp : 0.0;
@@ -1367,6 +1471,9 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
       wave_sync();
       const double grad = (lane < n) ? (h_dot<N>(s, lane) + gj + gt_dot<N>(s, lane)) : 0.0;
       const double ypc = grow_dot<N>(s, lane);
+#if KIN_POLISH_CG
+      emax = wave_max(al_act ? fabs(ypc - bnd_al) : 0.0);  // the true violation, not CG's recurrence
+#endif
       // dual violations (> 0 is wrong-signed): box multiplier of an active bound is
       // -grad (upper) / grad (lower); state-row multiplier is nu (upper) / -nu (lower)
       const double dv_b = (lane < n) ? (ahi_b ? grad : (alo_b ? -grad : -1.0)) : -1.0;
