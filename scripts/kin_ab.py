@@ -52,6 +52,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--child", nargs=2)
+    ap.add_argument("--keep", help="directory to keep each library's u / status / iters (.npz) in")
     ap.add_argument("libs", nargs="*")
     a = ap.parse_args()
     if a.child:
@@ -63,6 +64,9 @@ def main():
         subprocess.run([sys.executable, __file__, "--batch", str(a.batch), "--reps", str(a.reps),
                         "--child", lib, out], check=True, timeout=300)
         z = np.load(out)
+        if a.keep:
+            os.makedirs(a.keep, exist_ok=True)
+            np.savez(os.path.join(a.keep, f"{i}_{os.path.basename(lib)}.npz"), u=z["u"], st=z["st"], it=z["it"])
         if ref is None:
             ref = z
         r = {"kernel_ms_mean": float(z["ms"].mean()), "kernel_ms_min": float(z["ms"].min()),

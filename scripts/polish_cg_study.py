@@ -119,12 +119,16 @@ guesses = {"lam > s": lami > si,
 lr, sr = lami / lamp, si / sp
 for TF in [float(x) for x in os.environ.get("TAPIA_F", "1.5,2,4").split(",")]:
     guesses[f"hyb{TF:g}"] = np.where(lr > TF * sr, True, np.where(sr > TF * lr, False, lami > si))
+# strict indicators: a side is called active only if its multiplier held (ratio >= 1 - TS) while its
+# slack dropped (ratio <= TS), inactive the other way round; lambda > s otherwise
+for TS in [float(x) for x in os.environ.get("TAPIA_S", "").split(",") if x]:
+    guesses[f"strict{TS:g}"] = np.where((lr >= 1 - TS) & (sr <= TS), True, np.where((sr >= 1 - TS) & (lr <= TS), False, lami > si))
 for name, act in guesses.items():
     wrong = (act != exact).sum(1)
     print(f"guess {name:8s}: problems with a misclassified row {int((wrong > 0).sum())} of {B}, rows {int(wrong.sum())}")
 
 
-def polish_sim(H, g, C, dd, lam, s, mode, rounds_max=10, act0=None):
+def polish_sim(H, g, C, dd, lam, s, mode, rounds_max=10, act0=None, zx=None):
     scale = 1.0 + max(np.abs(g).max(), np.abs(dd).max())
     hmax = max(np.diag(H).max(), 1.0)
     ptol = 1e-9 * scale
@@ -187,18 +191,20 @@ def polish_sim(H, g, C, dd, lam, s, mode, rounds_max=10, act0=None):
         dv = np.where(act, -lamf, -np.inf)
         pv = np.where(act, -np.inf, C @ zp - dd)
         if dv.max() <= ptol and pv.max() <= ptol:
-            return rnd + 1, total, np.abs(e).max() <= ptol if len(rows) else True
+            ok = np.abs(e).max() <= ptol if len(rows) else True
+            return rnd + 1, total, ok, np.abs(zp - zx).max() if (ok and zx is not None) else 0.0
         if dv.max() > ptol:
             act[np.argmax(dv)] = False
         else:
             act[np.argmax(pv)] = True
-    return rounds_max, total, False
+    return rounds_max, total, False, 0.0
 
 
-for gname, mode in [("lam > s", "al"), ("lam > s", "cg"), ("tapia", "cg")] + [(k, "cg") for k in guesses if k.startswith("hyb")]:
+for gname, mode in [("lam > s", "al"), ("lam > s", "cg"), ("tapia", "cg")] + [(k, "cg") for k in guesses if k.startswith(("hyb", "strict"))]:
     out = np.array([polish_sim(sol["H"][i], sol["g"][i], sol["C"][i], sol["d"][i], lami[i], si[i], mode,
-                               act0=guesses[gname][i]) for i in range(B)])
+                               act0=guesses[gname][i], zx=sol["z"][i]) for i in range(B)])
     print(f"polish from the interior point at tol {tol:g} [{gname}, {mode}]: rounds mean {out[:, 0].mean():.2f} max {out[:, 0].max():.0f}, "
-          f"solves mean {out[:, 1].mean():.2f} max {out[:, 1].max():.0f}, certified {out[:, 2].mean():.3f}")
+          f"solves mean {out[:, 1].mean():.2f} max {out[:, 1].max():.0f}, certified {out[:, 2].mean():.3f}, "
+          f"certified but |z - z*| > 1e-6: {int((out[:, 3] > 1e-6).sum())} (max {out[:, 3].max():.1e})")
     worst = np.argsort(out[:, 1])[::-1][:6]
     print("  most solves (problem, rounds, solves):", [(int(j), int(out[j, 0]), int(out[j, 1])) for j in worst])

@@ -62,6 +62,12 @@
 #ifndef KIN_NU_TOL
 #define KIN_NU_TOL 1e-10  // CG also runs until the multiplier step R e is below this x scale (0: off)
 #endif
+#ifndef KIN_EARLY_F
+#define KIN_EARLY_F 100.0  // first polish attempt at this x the interior point's tolerance (0: only at it)
+#endif
+#ifndef KIN_EARLY_ROUNDS
+#define KIN_EARLY_ROUNDS 2  // active-set rounds of that attempt before the interior point resumes
+#endif
 #ifndef KIN_TAPIA
 #define KIN_TAPIA 1  // polish's first active set from the last step's Tapia indicators (0: lambda > s)
 #endif
@@ -1128,6 +1134,17 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
   // true residuals end at the same 9.4e-11 / 3.5e-12 (scaled), polish certifying all 1,024.
   double rd = 0.0, rlo_b = 0.0, rhi_b = 0.0, rlo_c = 0.0, rhi_c = 0.0;
   int tapb = 0;  // KIN_TAPIA: two bits per constraint side (1 active, 2 inactive, 0 undecided)
+  // KIN_EARLY_F: the polish is first tried once the interior point reaches tol_early; if that
+  // attempt does not certify within KIN_EARLY_ROUNDS rounds the interior point resumes from its
+  // iterate (the polish changes none of its state) to tol and the polish runs again.  With the
+  // Tapia guess 99.6 % of the C2 problems certify at 100 x tol, 1.15 interior-point iterations
+  // earlier on average (scripts/early_polish_study.py).
+  const double tol_early = KIN_EARLY_F > 0.0 ? fmax(tol, KIN_EARLY_F * tol) : tol;
+  double tol_cur = tol_early;
+  bool polished = false, pchol_fail = false;
+  int rounds = 0;
+#pragma unroll 1
+  for (;;) {
   if (finite) {
 #pragma unroll 1
     for (;;) {
@@ -1148,7 +1165,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
       const double mu = wave_sum(bx.slo * bx.llo + bx.shi * bx.lhi + cs.slo * cs.llo + cs.shi * cs.lhi) / mtot;
       const double res =
           wave_max(fmax(fmax(fabs(rd), fmax(fabs(rlo_b), fabs(rhi_b))), fmax(fabs(rlo_c), fabs(rhi_c))));
-      converged = res <= tol && mu <= tol;
+      converged = res <= tol_cur && mu <= tol_cur;
       last_res = res;
       last_mu = mu;
       if (converged || it >= max_iter || !isfinite(res) || !isfinite(mu)) break;
@@ -1271,8 +1288,6 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
   // violated constraint added (oracle/qp.py:polish uses the same rule with a
   // direct KKT solve).  If no candidate certifies within qp.polish rounds, the
   // converged interior-point iterate is kept.
-  bool polished = false, pchol_fail = false;
-  int rounds = 0;
   if ((converged || near) && A.qp.polish > 0) {
     constexpr double AL_RHO = 1e4;
     constexpr int AL_MAX = 16;
@@ -1290,8 +1305,9 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
     bool alo_c = cs.hasLo && cs.llo > cs.slo;
     bool ahi_c = cs.hasHi && cs.lhi > cs.shi;
 #endif
+    const int max_rounds = tol_cur > tol ? min(A.qp.polish, KIN_EARLY_ROUNDS) : A.qp.polish;
 #pragma unroll 1
-    for (int round = 0; round < A.qp.polish; ++round) {
+    for (int round = 0; round < max_rounds; ++round) {
       no_hoist();
       rounds = round + 1;
       const bool fixed = (lane < n) && (alo_b || ahi_b);
@@ -1480,7 +1496,10 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
       const double dv_c = (lane < NC) ? (ahi_c ? -nu_c : (alo_c ? nu_c : -1.0)) : -1.0;
       // primal violations of the inactive constraints
       const double pv_b = (lane < n && !fixed) ? fmax(bx.lo - zp, zp - bx.hi) : -1.0;
-      const double pv_c = (lane < NC && !(alo_c || ahi_c))
+      // every row the equality solve does not enforce is checked against its bounds: the inactive
+      // ones, and active ones without a free variable (rho_c = 0: fixed inputs alone decide them --
+      // unchecked, an early attempt's guess certified a point 9e-3 off the optimum, C4 problem 23921)
+      const double pv_c = (lane < NC && !(act && rho_c > 0.0))
                               ? fmax(cs.hasLo ? cs.lo - ypc : -1.0, cs.hasHi ? ypc - cs.hi : -1.0)
                               : -1.0;
       const double dmax = wave_max(fmax(dv_b, dv_c));
@@ -1513,6 +1532,12 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
   }
 
   VC_TACC(T_POLISH, t_pol0)
+  // (a polish factorisation that fails also resumes: the interior point's state is intact)
+  if (polished || !converged || chol_fail || tol_cur <= tol) break;
+  tol_cur = tol;  // the early attempt did not certify: back to the interior point
+  converged = false;
+  pchol_fail = false;
+  }
   VC_TSTAMP(t_out0)
   // ---- outputs -------------------------------------------------------------------
   int32_t st;
