@@ -1309,7 +1309,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
 #pragma unroll 1
     for (int round = 0; round < max_rounds; ++round) {
       no_hoist();
-      rounds = round + 1;
+      ++rounds;  // over both attempts (diag[3]; bench.py prices each round as an iteration)
       const bool fixed = (lane < n) && (alo_b || ahi_b);
       const double zfix = fixed ? (alo_b ? bx.lo : bx.hi) : 0.0;
       const uint64_t fmask = __ballot(fixed);
