@@ -81,6 +81,9 @@ struct KrSmem {
   int flag;
 };
 
+#ifndef KR_TAPIA
+#define KR_TAPIA 0  // polish's active set from the last step's Tapia indicators where decisive (kin_ltv.hip)
+#endif
 #ifndef KR_RES_RECUR
 #define KR_RES_RECUR 1  // dual residual carried by the steps (0: adjoint sweep every iteration)
 #endif
@@ -329,6 +332,7 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
   for (int e = 0; e < NV; ++e) qmax = fmax(qmax, fabs(qc[e]));
   qmax = wmax(stl ? qmax : 0.0);
   double sl[NRW], la[NRW];
+  int tapb = 0;  // KR_TAPIA: two bits per row (1 active, 2 inactive, 0 undecided), from the last step
 #pragma unroll
   for (int i = 0; i < NRW; ++i) {
     sl[i] = m[i] > 0.0 ? fmax(d[i], 1.0) : 1.0;
@@ -598,7 +602,10 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
   auto polish = [&]() -> bool {
     bool act[NRW], elr[3];
 #pragma unroll
-    for (int i = 0; i < NRW; ++i) act[i] = m[i] > 0.0 && la[i] > sl[i];
+    for (int i = 0; i < NRW; ++i) {
+      const int t = KR_TAPIA ? (tapb >> (2 * i)) & 3 : 0;
+      act[i] = m[i] > 0.0 && (t == 1 || (t == 0 && la[i] > sl[i]));
+    }
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       elr[j] = me[j] > 0.0 && te[j] > le[j];
@@ -884,6 +891,14 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
     rd_carry = (1.0 - alpha) * rdm;
     have_rd = true;
     if (stl) {
+#if KR_TAPIA
+      tapb = 0;
+#pragma unroll
+      for (int i = 0; i < NRW; ++i) {
+        const double lr = 1.0 + alpha * dla[i] / la[i], sr = 1.0 + alpha * dsa[i] / sl[i];
+        tapb |= (m[i] > 0.0 ? (lr > 1.02 * sr ? 1 : (sr > 1.02 * lr ? 2 : 0)) : 0) << (2 * i);
+      }
+#endif
 #pragma unroll
       for (int i = 0; i < NRW; ++i) {
         if (m[i] > 0.0) {
