@@ -82,7 +82,8 @@ struct KrSmem {
 };
 
 #ifndef KR_TAPIA
-#define KR_TAPIA 0  // polish's active set from the last step's Tapia indicators where decisive (kin_ltv.hip)
+#define KR_TAPIA 0  // polish's active set from the last step's Tapia indicators where decisive (kin_ltv.hip);
+                     // off: N = 50 fell from 810 K to 370 K solves/s at equal iterations (profiles/r04/krab_r04x.txt)
 #endif
 #ifndef KR_RES_RECUR
 #define KR_RES_RECUR 1  // dual residual carried by the steps (0: adjoint sweep every iteration)
