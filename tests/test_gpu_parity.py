@@ -173,6 +173,22 @@ def test_solve_full_batch_properties(ctx, kin_W):
     assert np.abs(ustar[idx] - ref["u_star"]).max() < U_TOL
 
 
+def test_c4_early_polish_regressions(ctx, kin_W):
+    """C4 problems (kinematic_batch(65536, seed=31)) where the polish's first attempt at 100 x the
+    interior point's tolerance once certified a point 9e-3 off the optimum (23921: an active state
+    row with every variable fixed went unchecked), plus the C4 problems that sat furthest from the
+    oracle in the r04 comparison (profiles/r04/kinab_c4diff.txt)."""
+    from vcmpc.workload import kinematic_batch
+    d = kinematic_batch(65536, seed=31)
+    idx = np.array([23921, 7832, 39971, 13063])
+    sub = {k: np.ascontiguousarray(v[idx]) for k, v in d.items()}
+    ref = Q.kin_ltv_solve(sub["x0"], sub["ubar"], sub["kappa"], sub["ds"], L, kin_W)
+    assert ref["polished"].all()
+    u0, xbar, ustar, status, iters = _solve(ctx, sub)
+    assert (status == 0).all()
+    assert np.abs(ustar - ref["u_star"]).max() < U_TOL
+
+
 def test_edge_batches(ctx, kin_golden):
     g = kin_golden
     e = {k: np.ascontiguousarray(g[k][:0]) for k in ("x0", "kappa", "ds", "ubar")}
