@@ -458,22 +458,11 @@ def cpu_baseline_casc(data, sample):
 
 C5_VEHICLES, C5_STEPS = 8192, 500
 C4_TOTAL = 65536
-C4_CHUNK = 8192   # the C4 problem set is generated in 8192-problem chunks (seed + chunk index),
-                  # so every world size solves the same 65536 problems
-
-
 def c4_shard(total, rank, world, seed):
-    """This rank's contiguous C4 shard [lo, hi) of `total` kinematic problems."""
-    import numpy as np
-
-    from vcmpc.workload import kinematic_batch, shard
-    lo, hi = shard(total, rank, world)
-    parts = []
-    for c in range(lo // C4_CHUNK, -(-hi // C4_CHUNK)):
-        a, b = c * C4_CHUNK, min((c + 1) * C4_CHUNK, total)
-        d = kinematic_batch(b - a, N=N_HORIZON, seed=seed + 1000003 * (c + 1))
-        parts.append({k: v[max(lo, a) - a:min(hi, b) - a] for k, v in d.items()})
-    return lo, hi, {k: np.ascontiguousarray(np.concatenate([p[k] for p in parts])) for k in parts[0]}
+    """This rank's contiguous C4 shard [lo, hi) of `total` kinematic problems (SURVEY 8(e));
+    vcmpc.workload.c4_shard, shared with tests/test_gpu_certify.py."""
+    from vcmpc.workload import c4_shard as shard_of
+    return shard_of(total, rank, world, seed, N=N_HORIZON)
 
 
 def run_c4(args, dev, stream, rank, world, dist, steps):

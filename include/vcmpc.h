@@ -235,7 +235,12 @@ int vc_solve(vc_ctx* ctx, int B, const void* x0, const void* kappa, const void* 
  *   [0] final scaled KKT residual, [1] final scaled complementarity mu,
  *   [2] flags: 1 = interior-point factorisation failed, 2 = interior point
  *       converged, 4 = active-set polish certified, 8 = polish factorisation failed,
- *   [3] polish rounds used.  diag follows the pointer convention of `flags`. */
+ *   [3] polish rounds used.  diag follows the pointer convention of `flags`.
+ * Kinematic (kin_ltv) [0] is the true residual of the interior point's last iterate.
+ * Single-track / cascaded SQP contexts: [2] = 1 any QP failed, 2 every QP converged,
+ * 16 the SQP stopped early (a QP after the first had no solution: its step was refused and
+ * the earlier iterate returned, so `status` reflects the QPs before it only); [3] the largest
+ * interior-point iteration count of one QP. */
 int vc_solve_diag(vc_ctx* ctx, int B, const void* x0, const void* kappa, const void* ds,
                   void* xbar, void* ubar, void* u0, int32_t* status, int32_t* iters, void* diag,
                   int flags);

@@ -49,6 +49,7 @@ import numpy as np
 from . import dyn_sqp as D
 from . import models as M
 from . import obstacles as OB
+from .qp import Gram
 
 IUX, IUY, IR, ID, IS, IEY, IEP, IT = range(8)
 PV, PS, PEY, PEP, PT = range(5)
@@ -191,11 +192,12 @@ def casc_qp(x0, ubar, kappa, ds, p, W, tyre="fiala"):
     Hm = np.zeros((B, n, n))
     g = np.zeros((B, n))
     eye = np.eye(n)
+    gram = Gram(B, n)
 
     def add_square(c, r0, row):
         c = np.broadcast_to(np.asarray(c, np.float64), (B,))
         row = np.broadcast_to(row, (B, n))
-        Hm[:] += 2.0 * c[:, None, None] * row[:, :, None] * row[:, None, :]
+        gram.add(2.0 * c, row)
         g[:] += 2.0 * (c * r0)[:, None] * row
 
     def ey_terms(ey, row, s, dsk, lo, hi, wdev):
@@ -204,7 +206,7 @@ def casc_qp(x0, ubar, kappa, ds, p, W, tyre="fiala"):
         add_square(np.where(ey > hi, W["w_b"] * dsk, 0.0), ey - hi, row)
         if W.get("obstacles"):
             p_o, q_o = OB.ey_model(s, ey, W["w_obs"] * dsk, W["obstacles"], W.get("obs_margin_min", OB.MARGIN_MIN))
-            Hm[:] += q_o[:, None, None] * row[:, :, None] * row[:, None, :]
+            gram.add(q_o, row)
             g[:] += p_o[:, None] * row
 
     def lin_row(grad, k):
@@ -242,6 +244,7 @@ def casc_qp(x0, ubar, kappa, ds, p, W, tyre="fiala"):
     g[:] += W["w_time"] * Gl[:, PT]
     add_square(W["w_ey"], xl[:, PEY], Gl[:, PEY])
     add_square(W["w_epsi"], xl[:, PEP], Gl[:, PEP])
+    gram.flush(Hm)
     Hm[:] += 2.0 * W["prox"] * eye
 
     rows, rhs = [], []

@@ -54,6 +54,7 @@ import numpy as np
 
 from . import models as M
 from . import obstacles as OB
+from .qp import Gram
 
 IUX, IUY, IR, ID, IS, IEY, IEP, IT = range(8)
 IFX, IW = 0, 1
@@ -219,10 +220,11 @@ def dyn_qp(x0, ubar, kappa, ds, p, W, tyre="linear"):
     H = np.zeros((B, n, n))
     g = np.zeros((B, n))
     eye = np.eye(n)
+    gram = Gram(B, n)
 
     def add_square(c, r0, row):
         c = np.broadcast_to(np.asarray(c, np.float64), (B,))
-        H[:] += 2.0 * c[:, None, None] * row[:, :, None] * row[:, None, :]
+        gram.add(2.0 * c, row)
         g[:] += 2.0 * (c * r0)[:, None] * row
 
     def lin_row(grad, k):
@@ -238,7 +240,7 @@ def dyn_qp(x0, ubar, kappa, ds, p, W, tyre="linear"):
         if W.get("obstacles"):  # cascaded_mpc.py:173-176, convexified in ey (obstacles.py)
             p_o, q_o = OB.ey_model(xbar[:, k, IS], ey, W["w_obs"] * ds[:, k], W["obstacles"],
                                    W.get("obs_margin_min", OB.MARGIN_MIN))
-            H[:] += q_o[:, None, None] * row[:, :, None] * row[:, None, :]
+            gram.add(q_o, row)
             g[:] += p_o[:, None] * row
         add_square(W["w_w"], ubar[:, k, IW], np.broadcast_to(eye[2 * k + 1], (B, n)))
         for ax in ("f", "r"):
@@ -253,6 +255,7 @@ def dyn_qp(x0, ubar, kappa, ds, p, W, tyre="linear"):
     g += W["w_time"] * G[:, kN, IT]
     add_square(W["w_ey"], xbar[:, kN, IEY], G[:, kN, IEY])
     add_square(W["w_epsi"], xbar[:, kN, IEP], G[:, kN, IEP])
+    gram.flush(H)
     H += 2.0 * W["prox"] * eye
 
     rows, rhs = [], []

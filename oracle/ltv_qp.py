@@ -39,6 +39,7 @@ import numpy as np
 
 from . import models as M
 from . import obstacles as OB
+from .qp import Gram
 
 IV, ID, IS, IEY, IEP, IT = range(6)
 IA, IW = 0, 1
@@ -125,11 +126,12 @@ def kin_qp(x0, ubar, kappa, ds, L, W, x_ws=None):
 
     H = np.zeros((B, n, n))
     g = np.zeros((B, n))
+    gram = Gram(B, n)
 
     def add_square(c, r0, row):
         # c * (r0 + row.dz)^2  -> H += 2c row row', g += 2c r0 row
         c = np.broadcast_to(np.asarray(c, np.float64), (B,))
-        H[:] += 2.0 * c[:, None, None] * row[:, :, None] * row[:, None, :]
+        gram.add(2.0 * c, row)
         g[:] += 2.0 * (c * r0)[:, None] * row
 
     # stage costs on ey_n (n = 0 is constant: G[:,0] = 0)
@@ -145,7 +147,7 @@ def kin_qp(x0, ubar, kappa, ds, L, W, x_ws=None):
         if W.get("obstacles"):  # kinematic_mpc.py:130-133, convexified in ey (obstacles.py)
             p_o, q_o = OB.ey_model(xbar[:, k, IS], ey, W["w_obs"] * ds[:, k], W["obstacles"],
                                    W.get("obs_margin_min", OB.MARGIN_MIN))
-            H[:] += q_o[:, None, None] * row[:, :, None] * row[:, None, :]
+            gram.add(q_o, row)
             g[:] += (p_o + q_o * (eyv - ey))[:, None] * row
     # input costs: w_w w^2 and slew w_a (a_{n+1}-a_n)^2
     for k in range(N):
@@ -161,6 +163,7 @@ def kin_qp(x0, ubar, kappa, ds, L, W, x_ws=None):
     add_square(W["w_ey"], xv[:, N, IEY], G[:, N, IEY])
     add_square(W["w_epsi"], xv[:, N, IEP], G[:, N, IEP])
     # proximal term prox*||dz||^2
+    gram.flush(H)
     H += 2.0 * W["prox"] * np.eye(n)
 
     # inequalities C dz <= d

@@ -21,6 +21,28 @@ from __future__ import annotations
 import numpy as np
 
 
+class Gram:
+    """Gauss-Newton Hessian H += sum_t c_t row_t row_t' over a batch, collected term by term
+    and formed as one batched matrix product R' diag(c) R at flush() -- the same sum as
+    rank-1 updates one at a time, in one BLAS call (the rank-1 loop was 80 % of building a
+    single-track N = 60 QP)."""
+
+    def __init__(self, B, n):
+        self.B, self.n = B, n
+        self.c, self.rows = [], []
+
+    def add(self, c, row):
+        self.c.append(np.broadcast_to(np.asarray(c, np.float64), (self.B,)))
+        self.rows.append(np.broadcast_to(np.asarray(row, np.float64), (self.B, self.n)))
+
+    def flush(self, H):
+        if self.rows:
+            R = np.stack(self.rows, axis=1)
+            Cw = np.stack(self.c, axis=1)
+            H += np.matmul(np.swapaxes(R * Cw[..., None], 1, 2), R)
+        self.c, self.rows = [], []
+
+
 def _max_step(v, dv):
     """Largest a in (0, 1] with v + a dv >= 0 (rowwise over the batch)."""
     with np.errstate(divide="ignore", invalid="ignore"):

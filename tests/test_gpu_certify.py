@@ -1,0 +1,159 @@
+"""Every problem of every bench-size batch against the KKT conditions of the oracle-built QP.
+
+The other parity tests compare the kernels with the oracle on golden sets and strided samples.
+Every "solved" status at bench scale otherwise rests on the kernel's own certificate.  The round-4
+early polish certified C4 problem 23921 9e-3 off the optimum, and only a kernel A/B caught it.
+So here every returned answer of each bench batch is checked independently of the kernel:
+
+* KKT certificate (oracle/certify.py): the QP (H, g, C, d) is rebuilt by the oracle restatement
+  at the kernel's own linearisation point.  Multipliers are recovered by NNLS on the rows the
+  answer makes active.  Stationarity, primal and dual feasibility and complementarity must all
+  hold to CERT_TOL * scale for every problem the kernel reports solved.  scale = 1 + max(|g|, |d|)
+  is the interior point's own scale.
+* The oracle's exact optimum of the same QP (active-set polish, certified; interior point where
+  the seeded polish does not certify): max ||u* - u*_oracle||_inf over the whole set is printed
+  and held to the north star's 1e-5.  The unseeded oracle (interior point + polish from z = 0)
+  runs on a strided sample and must agree with the seeded one.
+* SQP batches (single-track, cascaded): every QP of the SQP is certified.  The kernel is run
+  with sqp_iters = 1 .. K, so its iterates u_0 .. u_K are known, and QP k is rebuilt at u_{k-1}.
+  The oracle's own SQP (exact QPs at its own iterates, the contract's domain and stopping rules)
+  gives u*_oracle.
+
+Sets: the C2 batch (1,024), the bench's C4 problem set (65,536, vcmpc.workload.c4_shard), the
+C4-style kinematic_batch(65536, seed = 31) where 23921 lives, kinematic N = 50 (8,192), C3
+(4,096, N = 40, 3 SQP iterations), single-track N = 60 (4,096) and cascaded 20 + 40 (4,096).
+These are the bench legs' own seeds (bench.py, rank 0).  A failure here is a kernel bug to fix.
+"""
+import numpy as np
+import pytest
+
+from oracle import certify as CF
+
+pytestmark = pytest.mark.gpu
+
+CERT_TOL = 1e-9     # KKT residuals, x scale
+U_TOL = 1e-5        # north star: ||u* - u*_oracle||_inf (kinematic: m/s^2, rad/s; SQP: N, rad/s)
+L = 2.5
+
+
+def _kin_ctx(N, B, solver=0):
+    from vcmpc import Context, _abi
+    from vcmpc.config import load_config, make_params
+    cfg = load_config("kinematic_mpc")
+    cfg["qp"] = dict(cfg.get("qp") or {}, solver=solver)
+    p = make_params(kin_car=load_config("kinematic_car"), kin_mpc=cfg)
+    return Context(model=_abi.VC_MODEL_KINEMATIC, N=N, max_batch=B, dtype=_abi.VC_F64, params=p)
+
+
+def _kin_set(name):
+    from vcmpc.workload import c4_shard, kinematic_batch
+    if name == "c2":
+        return 20, kinematic_batch(1024, N=20, seed=31)          # bench.py main(), rank 0
+    if name == "c4_bench":
+        return 20, c4_shard(65536, 0, 1, 31)[2]                   # bench.py run_c4, all ranks' shards
+    if name == "c4_seed31":
+        return 20, kinematic_batch(65536, N=20, seed=31)          # where 23921 lives
+    if name == "n50":
+        return 50, kinematic_batch(8192, N=50, seed=77)           # test_kin_ric_batch_properties_n50
+    raise ValueError(name)
+
+
+def _summary(name, solved, cert, ok, err):
+    s = cert["scale"]
+    print(f"{name}: {int(solved.sum())}/{len(solved)} solved, certified {int((ok & solved).sum())}; "
+          f"max stat {np.max(cert['stat'][solved] / s[solved]):.2e}, pfeas {np.max(cert['pfeas'][solved] / s[solved]):.2e}, "
+          f"comp {np.max(cert['comp'][solved] / s[solved]):.2e} (x scale); "
+          f"max |u* - u*_oracle|_inf over the set {err:.3e}")
+
+
+@pytest.mark.parametrize("name", ["c2", "c4_bench", "c4_seed31", "n50"])
+def test_kinematic_batch_every_problem_certified(name, kin_W):
+    N, d = _kin_set(name)
+    B = len(d["x0"])
+    with _kin_ctx(N, B) as c:
+        u0, xs, us, st, it = c.solve(d["x0"], d["kappa"], d["ds"], d["ubar"].copy())
+    z = (us - d["ubar"]).reshape(B, 2 * N)
+    r = CF.certify_batch("kin", z, dict(W=kin_W, L=L), {k: d[k] for k in ("x0", "ubar", "kappa", "ds")},
+                         chunk=2048 if N == 20 else 512, independent_every=64 if N == 20 else 32)
+    solved = st == 0
+    ok = CF.kkt_ok(r, CERT_TOL)
+    err_all = np.abs(z - r["z_exact"]).max(axis=1)
+    _summary(f"kinematic {name} (N={N})", solved, r, ok, float(err_all[solved].max()))
+    assert solved.all(), np.nonzero(~solved)[0][:10]
+    bad = np.nonzero(solved & ~ok)[0]
+    assert len(bad) == 0, [(int(b), float(r["stat"][b] / r["scale"][b]), float(err_all[b])) for b in bad[:10]]
+    assert r["exact_ok"].all()
+    assert err_all.max() < U_TOL
+    # the unseeded oracle agrees with the seeded one (the optimum is unique)
+    idx = r["indep_idx"]
+    assert r["indep_ok"].all()
+    assert np.abs(r["z_indep"] - r["z_exact"][idx]).max() < 1e-9
+
+
+def _dyn_ctx(kind, N, B, cfg, tyre):
+    from vcmpc import Context, _abi
+    from vcmpc.config import load_config, make_params
+    params = make_params(dyn_car=load_config("dynamic_car"), dyn_mpc=cfg, tyre=tyre)
+    model = _abi.VC_MODEL_CASCADED if kind == "casc" else _abi.VC_MODEL_DYNAMIC
+    return Context(model=model, N=N, max_batch=B, dtype=_abi.VC_F64, params=params)
+
+
+def _sqp_set(name):
+    from vcmpc.config import load_config
+    from vcmpc.workload import cascaded_batch, dynamic_batch
+    if name == "c3":          # bench.py run_c3, rank 0
+        d = {k: v.astype(np.float64) for k, v in dynamic_batch(4096, N=40, seed=31).items()}
+        return "dyn", 40, d, load_config("dynamic_mpc"), "linear"
+    if name == "st_n60":      # bench.py singletrack_n60_f64
+        d = {k: v.astype(np.float64) for k, v in dynamic_batch(4096, N=60, seed=31).items()}
+        return "dyn", 60, d, load_config("singletrack_mpc"), "linear"
+    if name == "cascaded":    # bench.py run_casc
+        return "casc", 20, cascaded_batch(4096, seed=31), load_config("cascaded_mpc"), "fiala"
+    raise ValueError(name)
+
+
+@pytest.mark.parametrize("name", ["c3", "st_n60", "cascaded"])
+def test_sqp_batch_every_qp_certified(name, dyn_params):
+    from oracle import casc_sqp as CS
+    from oracle import dyn_sqp as D
+    kind, N, d, cfg, tyre = _sqp_set(name)
+    B = len(d["x0"])
+    K = int(cfg["qp"]["sqp_iters"])
+    us, stop, st_k = [d["ubar"].copy()], [], []
+    for k in range(1, K + 1):
+        ck = dict(cfg, qp=dict(cfg["qp"], sqp_iters=k))
+        with _dyn_ctx(kind, N, B, ck, tyre) as c:
+            u0, xs, u, st, it, dg = c.solve(d["x0"], d["kappa"], d["ds"], d["ubar"].copy(), diag=True)
+        us.append(u)
+        stop.append((dg[:, 2].astype(int) & 16) > 0)
+        st_k.append(st)
+    us, stop = np.stack(us), np.stack(stop)
+    W = CS.casc_weights(cfg) if kind == "casc" else D.dyn_weights(cfg)
+    r = CF.certify_sqp_batch(kind, us, stop, dict(W=W, p=dyn_params, tyre=tyre),
+                             {k: d[k] for k in ("x0", "kappa", "ds")}, chunk=128)
+    solved = st_k[-1] == 0
+    lim = CERT_TOL * r["scale"]
+    ok = (r["stat"] <= lim) & (r["pfeas"] <= lim) & (r["dfeas"] <= lim) & (r["comp"] <= lim)
+    sc = CF.sqp_scale(kind, us.shape[2], N)
+    err = np.abs(us[-1] - r["u_oracle"]).max(axis=(1, 2))
+    print(f"{name}: {int(solved.sum())}/{B} solved at K = {K}; stopped early at QP k: {stop.sum(axis=1).tolist()}; "
+          f"step lengths < 1: {(r['alpha'] < 1).sum(axis=1).tolist()}")
+    fails = []
+    for k in range(K):
+        # QP k is the kernel's where the k-run reports solved and did not stop at QP k
+        req = (st_k[k] == 0) & ~stop[k]
+        s = r["scale"][k]
+        bad = np.nonzero(req & ~ok[k])[0]
+        print(f"  QP {k + 1}: required {int(req.sum())}, certified {int((ok[k] & req).sum())}; max stat "
+              f"{np.max(r['stat'][k][req] / s[req]):.2e} pfeas {np.max(r['pfeas'][k][req] / s[req]):.2e} comp "
+              f"{np.max(r['comp'][k][req] / s[req]):.2e}; max |dz - dz_oracle| {r['dz_err'][k][req].max():.2e} "
+              f"(scaled); uncertified {[(int(b), float(r['stat'][k][b] / s[b]), float(r['dz_err'][k][b])) for b in bad[:6]]}")
+        fails += [(k + 1, int(b)) for b in bad]
+        assert r["exact_ok"][k][req].all()
+    worst = np.argsort(-np.where(solved, err, 0))[:5]
+    print(f"  max |u* - u*_oracle|_inf over the solved set: {err[solved].max():.3e} (N, rad/s); "
+          f"in QP units {np.abs((us[-1] - r['u_oracle']) / sc).max(axis=(1, 2))[solved].max():.3e}; "
+          f"> 1e-5: {int((err[solved] > U_TOL).sum())}; worst {[(int(b), float(err[b])) for b in worst]}")
+    assert not fails, fails[:20]
+    assert (solved.mean() >= 0.997), np.bincount(st_k[-1])
+    assert err[solved].max() < U_TOL

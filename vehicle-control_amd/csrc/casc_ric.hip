@@ -260,7 +260,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
   WSYNC();
 
   int it_total = 0, it_max = 0;
-  bool all_conv = true, any_fail = false;
+  bool all_conv = true, any_fail = false, stopped = false;  // stopped: a later QP ended the SQP early
   double last_res = 0.0, last_mu = 0.0;
   const double tol_r = 1e-10, tol_mu = 1e-13;
 
@@ -1041,7 +1041,10 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     // (kin_merit.hip) and oracle/dyn_sqp.py alike.  (Applying the unconverged iterate and
     // reporting the whole step non-solved threw away a plan from converged QPs: the
     // single-track N = 60 obstacle run on the shoe track lost the car, scripts/band_trace.py.)
-    if (CR_KEEP_ITERATE && sq > 0 && !conv) break;
+    if (CR_KEEP_ITERATE && sq > 0 && !conv) {
+      stopped = true;
+      break;
+    }
     all_conv = all_conv && conv;
     any_fail = any_fail || fail;
 
@@ -1087,7 +1090,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       constexpr size_t DS = VC_CASC_DIAG_COLS;  // the ABI's row stride (no section counters here)
       A.diag[(size_t)b * DS + 0] = last_res;
       A.diag[(size_t)b * DS + 1] = last_mu;
-      A.diag[(size_t)b * DS + 2] = double((any_fail ? 1 : 0) | (all_conv ? 2 : 0));
+      A.diag[(size_t)b * DS + 2] = double((any_fail ? 1 : 0) | (all_conv ? 2 : 0) | (stopped ? 16 : 0));
       A.diag[(size_t)b * DS + 3] = double(it_max);
     }
   }

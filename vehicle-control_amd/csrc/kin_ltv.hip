@@ -74,6 +74,18 @@
 #ifndef KIN_TAPIA_F
 #define KIN_TAPIA_F 1.02  // ratio gap that makes the indicators decisive (else lambda > s)
 #endif
+#ifndef KIN_DUAL_TOL
+// polish: a multiplier of the wrong sign is accepted up to this x scale.  The cost is nearly flat
+// along the acceleration directions (curvature 2 prox = 2e-4), so a wrong-signed multiplier
+// lam moves the answer by ~lam / 2e-4: at 1e-9 scale (the round-4 value) C4 problem 33696 kept
+// a box bound whose multiplier was -2e-7 and landed 4e-4 off the optimum (tests/test_gpu_certify.py)
+#define KIN_DUAL_TOL 1e-12
+#endif
+#ifndef KIN_AL_RHO
+#define KIN_AL_RHO 1e1  // polish: augmented-Lagrangian weight of an active row, x max diag(H) / |free part|^2 (1e4 in
+                        // round 4: the factored matrix's condition number left C4 problems 6e-6 off the optimum;
+                        // 1e1 keeps every C4 problem within 5e-9 at the same cost, profiles/r05/alrho_r05a.log)
+#endif
 #ifndef KIN_DOT_CH
 #define KIN_DOT_CH 8  // terms per chunk of the residual dot products
 #endif
@@ -1132,7 +1144,26 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
   // matrix-vector products per iteration (G z, H z, G' lambda) by five multiplies; the oracle's
   // Mehrotra iteration with the same recursion takes the same iterations on the C2 batch and its
   // true residuals end at the same 9.4e-11 / 3.5e-12 (scaled), polish certifying all 1,024.
+  // The carried values never end the loop on their own: once they pass the stopping test the
+  // true residuals are recomputed from z, lambda and decide (the normal-equation solves are not
+  // exact, so the true residual stalls at a level set by the condition number, and a carried
+  // value that drifted below it must not certify convergence -- nor land in diag[0]).
   double rd = 0.0, rlo_b = 0.0, rhi_b = 0.0, rlo_c = 0.0, rhi_c = 0.0;
+  auto true_residuals = [&]() {
+    wave_sync();
+    s.vz[lane] = (lane < n) ? z : 0.0;
+    s.vc[lane] = (lane < NC) ? (cs.lhi - cs.llo) : 0.0;
+    wave_sync();
+    const double yc = grow_dot<N>(s, lane);
+    rd = (lane < n) ? (h_dot<N>(s, lane) + gj + (bx.lhi - bx.llo) + gt_dot<N>(s, lane)) : 0.0;
+    rlo_b = bx.hasLo ? (z - bx.lo - bx.slo) : 0.0;
+    rhi_b = bx.hasHi ? (bx.hi - z - bx.shi) : 0.0;
+    rlo_c = cs.hasLo ? (yc - cs.lo - cs.slo) : 0.0;
+    rhi_c = cs.hasHi ? (cs.hi - yc - cs.shi) : 0.0;
+  };
+  auto max_residual = [&]() {
+    return wave_max(fmax(fmax(fabs(rd), fmax(fabs(rlo_b), fabs(rhi_b))), fmax(fabs(rlo_c), fabs(rhi_c))));
+  };
   int tapb = 0;  // KIN_TAPIA: two bits per constraint side (1 active, 2 inactive, 0 undecided)
   // KIN_EARLY_F: the polish is first tried once the interior point reaches tol_early; if that
   // attempt does not certify within KIN_EARLY_ROUNDS rounds the interior point resumes from its
@@ -1150,21 +1181,13 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
     for (;;) {
       no_hoist();
       VC_TSTAMP(t_res0)
-      if (!KIN_RES_RECUR || it == 0) {
-        wave_sync();
-        s.vz[lane] = (lane < n) ? z : 0.0;
-        s.vc[lane] = (lane < NC) ? (cs.lhi - cs.llo) : 0.0;
-        wave_sync();
-        const double yc = grow_dot<N>(s, lane);
-        rd = (lane < n) ? (h_dot<N>(s, lane) + gj + (bx.lhi - bx.llo) + gt_dot<N>(s, lane)) : 0.0;
-        rlo_b = bx.hasLo ? (z - bx.lo - bx.slo) : 0.0;
-        rhi_b = bx.hasHi ? (bx.hi - z - bx.shi) : 0.0;
-        rlo_c = cs.hasLo ? (yc - cs.lo - cs.slo) : 0.0;
-        rhi_c = cs.hasHi ? (cs.hi - yc - cs.shi) : 0.0;
-      }
+      if (!KIN_RES_RECUR || it == 0) true_residuals();
       const double mu = wave_sum(bx.slo * bx.llo + bx.shi * bx.lhi + cs.slo * cs.llo + cs.shi * cs.lhi) / mtot;
-      const double res =
-          wave_max(fmax(fmax(fabs(rd), fmax(fabs(rlo_b), fabs(rhi_b))), fmax(fabs(rlo_c), fabs(rhi_c))));
+      double res = max_residual();
+      if (KIN_RES_RECUR && it > 0 && res <= tol_cur && mu <= tol_cur) {
+        true_residuals();  // the carried residual would stop here: the true one decides
+        res = max_residual();
+      }
       converged = res <= tol_cur && mu <= tol_cur;
       last_res = res;
       last_mu = mu;
@@ -1289,9 +1312,9 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
   // direct KKT solve).  If no candidate certifies within qp.polish rounds, the
   // converged interior-point iterate is kept.
   if ((converged || near) && A.qp.polish > 0) {
-    constexpr double AL_RHO = 1e4;
+    constexpr double AL_RHO = KIN_AL_RHO;
     constexpr int AL_MAX = 16;
-    const double ptol = 1e-9 * scale;
+    const double ptol = 1e-9 * scale, dtol = KIN_DUAL_TOL * scale;
 #if KIN_TAPIA
     // decisive indicators first, lambda > s where the last step left them undecided
     auto guess = [&](bool has, double l, double sv, int t) { return has && (t == 1 || (t == 0 && l > sv)); };
@@ -1504,7 +1527,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
                               : -1.0;
       const double dmax = wave_max(fmax(dv_b, dv_c));
       const double pmax = wave_max(fmax(pv_b, pv_c));
-      if (dmax <= ptol && pmax <= ptol) {
+      if (dmax <= dtol && pmax <= ptol) {
         if (emax <= ptol) {
           z = (lane < n) ? zp : z;
           polished = true;
@@ -1512,7 +1535,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
         break;  // certified, or the equality solve did not converge: keep the IPM iterate
       }
       // change one constraint: the lowest lane holding the worst violation
-      const bool dual = dmax > ptol;
+      const bool dual = dmax > dtol;
       const double worst = dual ? dmax : pmax;
       const double vb = dual ? dv_b : pv_b, vcr = dual ? dv_c : pv_c;
       const uint64_t who = __ballot(fmax(vb, vcr) == worst);

@@ -146,6 +146,22 @@ struct StSmem {
 #define ST_RES_RECUR 1  // dual residual carried by the steps (0: adjoint sweep every iteration)
 #endif
 
+#ifndef ST_POLISH
+#define ST_POLISH 3  // active-set polish rounds after each converged QP (0: off, the round-4 kernel)
+#endif
+#ifndef ST_AL_RHO
+#define ST_AL_RHO 1e2  // polish: augmented-Lagrangian weight of an active row, x (1 + max diag Q) / |c|^2
+#endif
+#ifndef ST_AL_PASSES
+#define ST_AL_PASSES 16
+#endif
+#ifndef ST_CERT_PTOL
+#define ST_CERT_PTOL 1e-11  // polish certificate: inactive-row violation, x (1 + max |q|)
+#endif
+#ifndef ST_CERT_DTOL
+#define ST_CERT_DTOL 1e-12  // polish certificate: wrong-signed multiplier, x (1 + max |q|)
+#endif
+
 #ifndef ST_KEEP_ITERATE
 #define ST_KEEP_ITERATE 1  // a later QP without a solution keeps the iterate (0: applies it, step non-solved)
 #endif
@@ -296,7 +312,8 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
   }
 
   int it_total = 0, it_max = 0;
-  bool all_conv = true, any_fail = false;
+  bool all_conv = true, any_fail = false, stopped = false;  // stopped: a later QP ended the SQP early
+  bool all_pol = true;  // every converged QP's answer certified by the active-set polish
   double last_res = 0.0, last_mu = 0.0;
   const double tol_r = 1e-10, tol_mu = 1e-13;
 
@@ -878,6 +895,27 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       return wmax(rmax);
     };
 
+    // stage lanes: s.u.q.Qt[k] = Qc + sum_i w_i c_i c_i' (the barrier weights of the interior
+    // point, or the augmented-Lagrangian weights of the polish)
+    auto put_qt = [&](const double* w) {
+      double Qt[NQ];
+#pragma unroll
+      for (int e = 0; e < NQ; ++e) Qt[e] = Qc[e];
+      Qt[Q00] += w[0];
+      Qt[Q33] += w[1] + w[2];
+      Qt[Q88] += w[8] + w[9];
+      Qt[Q77] += w[10] + w[11];
+      constexpr int ix[5] = {0, 1, 2, 3, 7};
+#pragma unroll
+      for (int r = 0; r < 5; ++r)
+#pragma unroll
+        for (int a = 0; a < 5; ++a)
+#pragma unroll
+          for (int e = a; e < 5; ++e) Qt[qslot(ix[a], ix[e])] += w[3 + r] * R.c[r][a] * R.c[r][e];
+#pragma unroll
+      for (int e = 0; e < NQ; ++e) s.u.q.Qt[k][e] = Qt[e];
+    };
+
     // ---------------- interior point (Mehrotra predictor-corrector) ----------------
     int it = 0;
     bool conv = false, fail = false;
@@ -914,22 +952,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       if (stl) {
 #pragma unroll
         for (int e = 0; e < 9; ++e) s.u.q.g[k][e] = grk[e];
-        double Qt[NQ];
-#pragma unroll
-        for (int e = 0; e < NQ; ++e) Qt[e] = Qc[e];
-        Qt[Q00] += wg[0];
-        Qt[Q33] += wg[1] + wg[2];
-        Qt[Q88] += wg[8] + wg[9];
-        Qt[Q77] += wg[10] + wg[11];
-        constexpr int ix[5] = {0, 1, 2, 3, 7};
-#pragma unroll
-        for (int r = 0; r < 5; ++r)
-#pragma unroll
-          for (int a = 0; a < 5; ++a)
-#pragma unroll
-            for (int e = a; e < 5; ++e) Qt[qslot(ix[a], ix[e])] += wg[3 + r] * R.c[r][a] * R.c[r][e];
-#pragma unroll
-        for (int e = 0; e < NQ; ++e) s.u.q.Qt[k][e] = Qt[e];
+        put_qt(wg);
       } else {
         rpm = 0.0;
         mus = 0.0;
@@ -1050,13 +1073,125 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     }
     it_total += it;
     it_max = max(it_max, it);
+
+    // ---------------- active-set polish (round 5) ----------------
+    // The interior point stops at mu <= 1e-13 with a floor acceptance near the end, and its
+    // iterate is then as far from the QP's optimum as its weakly active rows allow: up to 1e-6 in
+    // the scaled units on the bench's C3 / N = 60 batches, i.e. 1e-3 N (tests/test_gpu_certify.py,
+    // every QP of every problem against the oracle-built QP).  The polish solves the QP on the
+    // active set the interior point identified (lambda > s) exactly: an augmented Lagrangian
+    // (Q + sum_A rho_i c_i c_i', one Riccati factorisation) whose passes are Newton steps from the
+    // current point -- the gradient Q v + q + sum_A c_i (lm_i + rho_i (c_i v - d_i)) is recomputed
+    // stage-locally each pass, so the factor's rounding is refined away instead of entering the
+    // answer -- with multiplier updates lm_i += rho_i (c_i v - d_i) until the active rows hold.
+    // Certified when the inactive rows are feasible and the active multipliers nonnegative;
+    // otherwise the violated rows join and the negative ones leave (ST_POLISH rounds), and an
+    // uncertified polish keeps the interior point's iterate.
+    bool pol_qp = false;
+    if (ST_POLISH > 0 && conv) {
+      double hs = 0.0, qs = 0.0;
+      if (stl) {
+        hs = fmax(fmax(fmax(Qc[Q00], Qc[Q11]), fmax(Qc[Q22], Qc[Q33])),
+                  fmax(fmax(Qc[Q44], Qc[Q55]), fmax(fmax(Qc[Q66], Qc[Q77]), Qc[Q88])));
+#pragma unroll
+        for (int e = 0; e < 9; ++e) qs = fmax(qs, fabs(qc[e]));
+      }
+      hs = 1.0 + wmax(hs);
+      qs = 1.0 + wmax(qs);
+      double rho[NR];
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        double cn2 = 1.0;
+        if (i >= 3 && i < 8) {
+          cn2 = 0.0;
+#pragma unroll
+          for (int a = 0; a < 5; ++a) cn2 += R.c[i - 3][a] * R.c[i - 3][a];
+        }
+        rho[i] = ST_AL_RHO * hs / fmax(cn2, 1e-30);
+      }
+      bool act[NR];
+#pragma unroll
+      for (int i = 0; i < NR; ++i) act[i] = stl && R.m[i] > 0.0 && la[i] > sl[i];
+#pragma unroll 1
+      for (int round = 0; round < ST_POLISH; ++round) {
+        double w[NR], lm[NR], vp[9], val[NR];
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          w[i] = act[i] ? rho[i] : 0.0;
+          lm[i] = act[i] ? la[i] : 0.0;
+        }
+        if (stl) put_qt(w);
+        WSYNC();
+        if (!factor()) break;  // keep the interior point's iterate
+#pragma unroll
+        for (int e = 0; e < 9; ++e) vp[e] = vk[e];
+        bool al_conv = false;
+#pragma unroll 1
+        for (int p = 0; p < ST_AL_PASSES; ++p) {
+          if (stl) {
+            double g9[9], y[NR];
+            row_values(R, vp, val);
+#pragma unroll
+            for (int i = 0; i < NR; ++i) y[i] = act[i] ? lm[i] + rho[i] * (val[i] - R.d[i]) : 0.0;
+            qmul(Qc, vp, g9);
+#pragma unroll
+            for (int e = 0; e < 9; ++e) g9[e] += qc[e];
+            row_adjoint(R, y, g9);
+#pragma unroll
+            for (int e = 0; e < 9; ++e) s.u.q.g[k][e] = g9[e];
+          }
+          WSYNC();
+          lq_solve();
+          double emax = 0.0;
+          if (stl) {
+#pragma unroll
+            for (int e = 0; e < 9; ++e) vp[e] += s.u.q.g[k][e];
+            row_values(R, vp, val);
+#pragma unroll
+            for (int i = 0; i < NR; ++i) {
+              const double r = act[i] ? val[i] - R.d[i] : 0.0;
+              lm[i] += rho[i] * r;
+              emax = fmax(emax, fabs(r));
+            }
+          }
+          WSYNC();
+          if (wmax(emax) <= 1e-14 * qs) {
+            al_conv = true;
+            break;
+          }
+        }
+        // certificate: inactive rows feasible, active multipliers nonnegative
+        bool viol[NR], neg[NR], bad = false;
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          viol[i] = stl && R.m[i] > 0.0 && !act[i] && val[i] - R.d[i] > ST_CERT_PTOL * qs;
+          neg[i] = act[i] && lm[i] < -ST_CERT_DTOL * qs;
+          bad = bad || viol[i] || neg[i];
+        }
+        if (al_conv && __all(bad ? 0 : 1) != 0) {
+          if (stl) {
+#pragma unroll
+            for (int e = 0; e < 9; ++e) vk[e] = vp[e];
+          }
+          pol_qp = true;
+          break;
+        }
+#pragma unroll
+        for (int i = 0; i < NR; ++i) act[i] = (act[i] || viol[i]) && !neg[i];
+      }
+      WSYNC();
+    }
+    all_pol = all_pol && (pol_qp || !conv);
     // a QP after the first without a solution (an infeasible linearisation: the interior point
     // diverges) refuses its own step and ends the SQP at the current iterate, whose rollout is
     // s.xs; the step's status is then that of the QPs before it -- the kinematic SQP's rule
     // (kin_merit.hip) and oracle/dyn_sqp.py alike.  (Applying the unconverged iterate and
     // reporting the whole step non-solved threw away a plan from converged QPs: the
     // single-track N = 60 obstacle run on the shoe track lost the car, scripts/band_trace.py.)
-    if (ST_KEEP_ITERATE && sq > 0 && !conv) break;
+    if (ST_KEEP_ITERATE && sq > 0 && !conv) {
+      stopped = true;
+      break;
+    }
     all_conv = all_conv && conv;
     any_fail = any_fail || fail;
 
@@ -1108,7 +1243,8 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
 #endif
       A.diag[(size_t)b * DS + 0] = last_res;
       A.diag[(size_t)b * DS + 1] = last_mu;
-      A.diag[(size_t)b * DS + 2] = double((any_fail ? 1 : 0) | (all_conv ? 2 : 0));
+      A.diag[(size_t)b * DS + 2] =
+          double((any_fail ? 1 : 0) | (all_conv ? 2 : 0) | (all_pol ? 4 : 0) | (stopped ? 16 : 0));
       A.diag[(size_t)b * DS + 3] = double(it_max);
     }
   }

@@ -81,6 +81,22 @@ def shard(B_total: int, rank: int, world: int):
     return lo, lo + per + (1 if rank < rem else 0)
 
 
+C4_CHUNK = 8192   # the C4 problem set is generated in 8192-problem chunks (seed + chunk index),
+                  # so every world size solves the same problems
+
+
+def c4_shard(total: int, rank: int, world: int, seed: int = 31, N: int = 20):
+    """Contiguous shard [lo, hi) of the C4 problem set of `total` kinematic problems
+    and its data; chunk c of C4_CHUNK problems is kinematic_batch(seed = seed + 1000003 (c + 1))."""
+    lo, hi = shard(total, rank, world)
+    parts = []
+    for c in range(lo // C4_CHUNK, -(-hi // C4_CHUNK)):
+        a, b = c * C4_CHUNK, min((c + 1) * C4_CHUNK, total)
+        d = kinematic_batch(b - a, N=N, seed=seed + 1000003 * (c + 1))
+        parts.append({k: v[max(lo, a) - a:min(hi, b) - a] for k, v in d.items()})
+    return lo, hi, {k: np.ascontiguousarray(np.concatenate([p[k] for p in parts])) for k in parts[0]}
+
+
 # ----------------------------------------------------------------------------
 # C3 / C5: dynamic single-track SQP-MPC, N = 40, fp32
 # ----------------------------------------------------------------------------
