@@ -75,6 +75,41 @@ C3_FLOP_ITER = (sum(2 * (2 * k) * 7 * 7 + (2 * k) ** 2 * 7 for k in range(1, C3_
 C3_FLOP_SQP = 4 * (C3_N - 1) * 9 * 300 + C3_n * (C3_N - 1) * 7 * 7 * 2
 
 
+# ---- roctx ranges: one per timed leg, so a rocprofv3 --kernel-trace --marker-trace pass can be
+# split per leg (scripts/leg_stats.py -> profiles/<round>/kernel_leg_stats_*.csv): the same kernel
+# runs in several legs (kin_ltv_kernel<20> in C2 and C4, st_sqp_kernel<60> at 5 and 40 SQP
+# iterations, casc_ric at 3 and 40), and a per-grid average mixes them
+_ROCTX = None
+
+
+def _roctx():
+    global _ROCTX
+    if _ROCTX is None:
+        import ctypes
+        _ROCTX = False
+        for name in ("librocprofiler-sdk-roctx.so.1", "libroctx64.so.4", "libroctx64.so"):
+            try:
+                lib = ctypes.CDLL(name)
+                lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
+                _ROCTX = lib
+                break
+            except (OSError, AttributeError):
+                continue
+    return _ROCTX
+
+
+def leg_push(name):
+    lib = _roctx()
+    if lib:
+        lib.roctxRangePushA(("leg:" + name).encode())
+
+
+def leg_pop():
+    lib = _roctx()
+    if lib:
+        lib.roctxRangePop()
+
+
 def c3_bytes(N, word):
     """Compulsory HBM bytes per single-track solve: in x0 + kappa + ds + ubar, out u* + x*
     (N columns) + u0, + status + iters."""
@@ -135,6 +170,9 @@ def parse():
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 sharded measurement")
     ap.add_argument("--no-kin-legs", action="store_true",
                     help="skip the stagewise kinematic legs (N = 20 Riccati, N = 50 = kinematic.yaml)")
+    ap.add_argument("--latency-calls", type=int, default=200,
+                    help="single-vehicle drop-in latency: timed command + drive steps per controller")
+    ap.add_argument("--no-latency", action="store_true", help="skip the single-vehicle latency legs")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU work: each rank only takes its C2/C4/C5 shards and runs the counter "
                          "collective over gloo (tests the launcher and the rank logic on a CPU host)")
@@ -272,7 +310,7 @@ def cpu_baseline_c3(data, sample):
                       f"complex-step linearisation + exact QP, numpy fp64, 1 thread) in {dt:.2f} s"}
 
 
-def run_c3(args, dev, stream, rank, dist, steps, f64=False, N=C3_N, cfg_name="dynamic_mpc", qp=None):
+def run_c3(args, dev, stream, rank, dist, steps, f64=False, N=C3_N, cfg_name="dynamic_mpc", qp=None, leg="c3"):
     """Secondary measurement: BASELINE config 3 on this rank (weak scaling).  f64=True runs
     the same workload through the fp64 stagewise-Riccati kernel (csrc/st_sqp.hip); with
     N = 60 / cfg_name = "singletrack_mpc" it is the reference's own single-track horizon."""
@@ -312,10 +350,12 @@ def run_c3(args, dev, stream, rank, dist, steps, f64=False, N=C3_N, cfg_name="dy
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     dist.barrier()
     torch.cuda.synchronize(dev)
+    leg_push(leg)
     t0 = time.perf_counter()
     for i in range(steps):
         step(events[i])
     torch.cuda.synchronize(dev)
+    leg_pop()
     dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
@@ -368,7 +408,7 @@ CA_FLOP_SQP = (CA_N - 1) * 10 * 4 * 400 + (CA_M - 1) * 7 * 60 + CA_n * (CA_N * 8
 CONVERGED_QP = {"prox": 0.01, "sqp_iters": 40}
 
 
-def run_casc(args, dev, stream, rank, dist, steps, qp=None):
+def run_casc(args, dev, stream, rank, dist, steps, qp=None, leg="cascaded"):
     """Cascaded NMPC (horizon_pm = 40) on this rank, B problems per GPU, fp64."""
     import numpy as np
     import torch
@@ -405,10 +445,12 @@ def run_casc(args, dev, stream, rank, dist, steps, qp=None):
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     dist.barrier()
     torch.cuda.synchronize(dev)
+    leg_push(leg)
     t0 = time.perf_counter()
     for i in range(steps):
         step(events[i])
     torch.cuda.synchronize(dev)
+    leg_pop()
     dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
@@ -465,7 +507,7 @@ def c4_shard(total, rank, world, seed):
     return shard_of(total, rank, world, seed, N=N_HORIZON)
 
 
-def run_c4(args, dev, stream, rank, world, dist, steps):
+def run_c4(args, dev, stream, rank, world, dist, steps, leg="c4"):
     """BASELINE config 4: 65536 kinematic LTV-MPC problems (N = 20, fp64) in total, one
     contiguous shard per rank (8192 per GPU at 8 GPUs), no data-path collective; `value`
     = all problems / the slowest rank's time (strong scaling over the fixed 65536)."""
@@ -499,10 +541,12 @@ def run_c4(args, dev, stream, rank, world, dist, steps):
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     dist.barrier()
     torch.cuda.synchronize(dev)
+    leg_push(leg)
     t0 = time.perf_counter()
     for i in range(steps):
         step(events[i])
     torch.cuda.synchronize(dev)
+    leg_pop()
     dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
@@ -512,8 +556,8 @@ def run_c4(args, dev, stream, rank, world, dist, steps):
     ctx.close()
     return {"metric": "MPC solves/sec (batched, N=20), C4 problem set sharded over the ranks",
             "value": solves / elapsed_max, "unit": "solves/s", "steps": steps,
-            "ms_per_step": elapsed_max / steps * 1e3, "kernel_ms_max": kern_ms_max, "dtype": "f64",
-            "scaling": "strong",
+            "ms_per_step": elapsed_max / steps * 1e3, "kernel": "kin_ltv_kernel<20>", "kernel_ms": kern_ms,
+            "kernel_ms_max": kern_ms_max, "dtype": "f64", "scaling": "strong",
             "config": {"workload": f"C4 kinematic-bicycle LTV-MPC, {args.c4_total} problems in total, N={N_HORIZON}, "
                                    f"fp64, contiguous shards", "total_batch": args.c4_total,
                        "batch_per_gpu_rank0": B, "parallelism": f"dp{world} (contiguous shards, no collective "
@@ -522,7 +566,7 @@ def run_c4(args, dev, stream, rank, world, dist, steps):
                        "iters_max_rank0": int(it.max())}}
 
 
-def run_kin_leg(args, dev, stream, rank, dist, steps, N, solver, B):
+def run_kin_leg(args, dev, stream, rank, dist, steps, N, solver, B, leg="kin"):
     """A kinematic LTV-MPC leg beside C2: the stagewise-Riccati kernel (csrc/kin_ric.hip) at
     BASELINE's N = 20 (solver = 1, vs the condensed kin_ltv.hip of `value`) and at the
     reference's own horizon N = 50 (config/controllers/kinematic.yaml:2)."""
@@ -558,10 +602,12 @@ def run_kin_leg(args, dev, stream, rank, dist, steps, N, solver, B):
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     dist.barrier()
     torch.cuda.synchronize(dev)
+    leg_push(leg)
     t0 = time.perf_counter()
     for i in range(steps):
         step(events[i])
     torch.cuda.synchronize(dev)
+    leg_pop()
     dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
@@ -664,11 +710,13 @@ def run_c5(args, dev, stream, rank, world, dist):
     ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     dist.barrier()
     torch.cuda.synchronize(dev)
+    leg_push("c5")
     t0 = time.perf_counter()
     ev[0].record(stream)
     log_x, _, nfail = sim.ctx.simulate(sim.x, sim.xbar, sim.ubar, K, sim.mpc_dt, sim.dt, log=True, nfail=sim.nfail)
     ev[1].record(stream)
     torch.cuda.synchronize(dev)
+    leg_pop()
     dist.barrier()
     elapsed = time.perf_counter() - t0
     gpu_ms = ev[0].elapsed_time(ev[1])
@@ -691,6 +739,77 @@ def run_c5(args, dev, stream, rank, world, dist):
            "closed_loop_rank0": {"on_track_frac": on_track, "max_abs_ey": max_ey, "mean_progress_m": progress,
                                  "nonsolved_frac": nf / (B * K)}}
     return out, x_all, track
+
+
+# the reference's only published numbers: per-step wall time of command + drive for ONE vehicle
+# (simulation/racing.py:231-233, CasADi/IPOPT + HSL MA27 on one unrecorded CPU thread; medians of
+# experiments/data/*/*_elapsed.npy)
+RECORDED_IPOPT_MEDIAN_MS = {"singletrack_n50": 55.7, "singletrack_n60": 75.4, "cascaded_n20_m15": 33.4,
+                            "cascaded_n20_m35": 39.3}
+
+
+def run_latency(args, dev):
+    """Single-vehicle latency of the drop-in controllers: one command(state) + car.drive(action)
+    per step (racing.py:231-233 / kinracing.py:283-290), host pointers, one vehicle, closed loop on
+    ippodromo; median / p90 / mean over `calls` steps after 20 warm-up steps.  Config: the
+    reference's own controller yamls (kinematic N = 20 and kinematic.yaml's N = 50, obstacles off;
+    single-track N = 50 / 60 = the recorded singletrack runs; cascaded 20 + 15 / 20 + 40)."""
+    import numpy as np
+
+    from vcmpc.config import load_config
+    from vcmpc.controllers import CascadedMPC, KinematicMPC
+    from vcmpc.environment import Track
+    from vcmpc.models import DynamicCar, DynamicPointMass, KinematicCar
+    track = Track.load("ippodromo")
+    calls = args.latency_calls
+
+    def kin(N):
+        cfg = load_config("kinematic_mpc")
+        cfg["horizon"], cfg["obstacles"] = N, False
+        car = KinematicCar(load_config("kinematic_car"), track)
+        car.state = car.create_state(v=5.0, s=1.0)
+        return car, KinematicMPC(car, cfg)
+
+    def dyn(cfg_name, N, M=None):
+        cfg = load_config(cfg_name)
+        cfg["horizon"], cfg["obstacles"] = N, False
+        if M is not None:
+            cfg["horizon_pm"] = M
+        car = DynamicCar(load_config("dynamic_car"), track, tyre="fiala")
+        car.state = car.create_state(Ux=8.0, s=1.0)
+        return car, CascadedMPC(car, DynamicPointMass(load_config("dynamic_car"), track), cfg)
+
+    legs = {"kinematic_n20": lambda: kin(20), "kinematic_n50": lambda: kin(50),
+            "singletrack_n50": lambda: dyn("singletrack_mpc", 50), "singletrack_n60": lambda: dyn("singletrack_mpc", 60),
+            "cascaded_n20_m15": lambda: dyn("cascaded_mpc", 20, 15), "cascaded_n20_m40": lambda: dyn("cascaded_mpc", 20, 40)}
+    out = {}
+    for name, make in legs.items():
+        try:
+            np.random.seed(31)
+            car, mpc = make()
+            ts, solved = [], 0
+            for i in range(20 + calls):
+                t0 = time.perf_counter()
+                a = mpc.command(car.state)
+                car.drive(a)
+                dt = time.perf_counter() - t0
+                if i >= 20:
+                    ts.append(dt)
+                    solved += int(np.asarray(mpc.status).reshape(-1)[0] == 0)
+            ts = np.array(ts) * 1e3
+            out[name] = {"median_ms": float(np.median(ts)), "p90_ms": float(np.percentile(ts, 90)),
+                         "mean_ms": float(ts.mean()), "calls": calls, "solved_frac": solved / calls,
+                         "s_end_m": float(car.state.values[2 if name.startswith("kin") else 4])}
+            if name in RECORDED_IPOPT_MEDIAN_MS:
+                out[name]["recorded_ipopt_median_ms"] = RECORDED_IPOPT_MEDIAN_MS[name]
+        except Exception as e:  # reported, never fatal
+            out[name] = {"error": f"{type(e).__name__}: {e}"}
+    out["note"] = ("one vehicle, command(state) + drive(action) per step through the drop-in controllers "
+                   "(host numpy in/out, H2D + one solve launch + D2H per command; drive = the device plant "
+                   "step), closed loop on ippodromo from s = 1 m; recorded_ipopt_median_ms = the reference's "
+                   "recorded CasADi/IPOPT medians (experiments/data, unrecorded CPU) -- historical context, "
+                   "not a same-host comparison")
+    return out
 
 
 def main():
@@ -747,10 +866,12 @@ def main():
               for _ in range(args.steps)]
     dist.barrier()
     torch.cuda.synchronize(dev)
+    leg_push("c2")
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(events[i])
     torch.cuda.synchronize(dev)
+    leg_pop()
     dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
@@ -782,7 +903,7 @@ def main():
     if not args.no_kin_legs:
         for name, N, solver in (("c2_riccati", N_HORIZON, 1), ("kinematic_n50", 50, 1)):
             try:
-                kin_legs[name] = run_kin_leg(args, dev, stream, rank, dist, max(3, args.steps // 4), N, solver, B)
+                kin_legs[name] = run_kin_leg(args, dev, stream, rank, dist, max(3, args.steps // 4), N, solver, B, leg=name)
             except Exception as e:
                 kin_legs[name] = {"error": f"{type(e).__name__}: {e}"}
     c3 = c3_data = c3f = st60 = st60c = None
@@ -803,19 +924,19 @@ def main():
                                 "r03); measured with --c3-f32 only")
         if args.c3_f32:
             try:
-                c3f, _ = run_c3(args, dev, stream, rank, dist, max(3, args.steps // 4))
+                c3f, _ = run_c3(args, dev, stream, rank, dist, max(3, args.steps // 4), leg="c3_f32")
             except Exception as e:
                 c3f = {"error": f"{type(e).__name__}: {e}"}
         try:
             st60, _ = run_c3(args, dev, stream, rank, dist, max(3, args.steps // 4), f64=True, N=60,
-                             cfg_name="singletrack_mpc")
+                             cfg_name="singletrack_mpc", leg="singletrack_n60_f64")
         except Exception as e:
             st60 = {"error": f"{type(e).__name__}: {e}"}
         # what a reference-equivalent answer costs: the converged SQP setting of the replay against
         # IPOPT's recorded solutions (tests/test_gpu_replay.py: prox 0.01, 40 SQP iterations)
         try:
             st60c, _ = run_c3(args, dev, stream, rank, dist, 2, f64=True, N=60, cfg_name="singletrack_mpc",
-                              qp=CONVERGED_QP)
+                              qp=CONVERGED_QP, leg="singletrack_n60_converged")
         except Exception as e:
             st60c = {"error": f"{type(e).__name__}: {e}"}
     ca = ca_data = cac = None
@@ -825,7 +946,7 @@ def main():
         except Exception as e:
             ca = {"error": f"{type(e).__name__}: {e}"}
         try:
-            cac, _ = run_casc(args, dev, stream, rank, dist, 2, qp=CONVERGED_QP)
+            cac, _ = run_casc(args, dev, stream, rank, dist, 2, qp=CONVERGED_QP, leg="cascaded_converged")
         except Exception as e:
             cac = {"error": f"{type(e).__name__}: {e}"}
     c5 = c5_aux = None
@@ -834,6 +955,10 @@ def main():
             c5, *c5_aux = run_c5(args, dev, stream, rank, world, dist)
         except Exception as e:
             c5 = {"error": f"{type(e).__name__}: {e}"}
+
+    lat = None
+    if world == 1 and not args.no_latency:
+        lat = run_latency(args, dev)
 
     if rank == 0:
         value = solves / elapsed_max
@@ -921,6 +1046,8 @@ def main():
             out["cascaded_converged"] = cac
         if c5 is not None:
             out["c5"] = c5
+        if lat is not None:
+            out["latency"] = lat
         print(json.dumps(out), flush=True)
     ctx.close()
     dist.shutdown()

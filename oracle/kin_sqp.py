@@ -167,7 +167,11 @@ def noise_step(alpha, phi0, p1, D):
     directions such as the last acceleration, whose only cost is the 1e-4 slew) is below what
     the merit can resolve, and the SQP would otherwise stop short of the KKT point."""
     sc = np.maximum(1.0, np.abs(phi0))
-    return (alpha == 0.0) & (np.abs(D) <= NOISE_D * sc) & (p1 <= phi0 + NOISE_PHI * sc)
+    # finite merits only (csrc/kin_merit.hip alike): from outside the domain (phi0 = inf) the tests
+    # below hold for any p1, and the full step would leave the domain again
+    with np.errstate(invalid="ignore"):
+        return ((alpha == 0.0) & np.isfinite(phi0) & np.isfinite(p1) & (np.abs(D) <= NOISE_D * sc)
+                & (p1 <= phi0 + NOISE_PHI * sc))
 
 
 def line_search_ms(x0, ubar, dz, x, dx, kappa, ds, L, W):

@@ -1,7 +1,8 @@
 #!/bin/bash
-# Round-end measurement: the bench line, a rocprofv3 kernel-stats pass over the headline legs
-# without the C4 leg (C4 launches the same kin_ltv_kernel<20> on 65,536 problems, which would
-# mix into the C2 kernel's average), and the PMC passes (scripts/pmc_profile.sh).
+# Round-end measurement: the bench line, a rocprofv3 kernel-trace + marker-trace pass over every
+# leg (bench.py wraps each timed leg in a roctx range; scripts/leg_stats.py splits the dispatches
+# per leg, so C2 and C4 -- both kin_ltv_kernel<20> -- and the 3- and 40-iteration SQP legs get
+# rows of their own), and the PMC passes (scripts/pmc_profile.sh).
 # usage: bash scripts/final_profile.sh <tag>
 set -u
 TAG=${1:-r02}
@@ -13,8 +14,9 @@ cd "$ROOT"
 timeout -k 10 600 python bench.py --steps 20 --warmup 3 > "$OUT/bench_$TAG.log" 2>&1
 rc=$?; echo "bench rc=$rc"; [ $rc -ge 124 ] && exit $rc
 cd /tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof_$TAG" -o run -- \
-    python3 "$ROOT/bench.py" --steps 20 --warmup 3 --no-cpu-baseline --no-c4 > "$OUT/rocprof_$TAG.log" 2>&1
+timeout -k 10 600 rocprofv3 --kernel-trace --marker-trace --stats -f csv -d "$OUT/prof_$TAG" -o run -- \
+    python3 "$ROOT/bench.py" --steps 20 --warmup 3 --no-cpu-baseline --no-latency > "$OUT/rocprof_$TAG.log" 2>&1
 rc=$?; echo "rocprof rc=$rc"; [ $rc -ge 124 ] && exit $rc
 cd "$ROOT"
+python scripts/leg_stats.py "$OUT/prof_$TAG" > "$OUT/kernel_leg_stats_$TAG.csv"
 bash scripts/pmc_profile.sh "$TAG" --no-c4

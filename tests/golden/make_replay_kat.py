@@ -7,7 +7,8 @@ Runs: cascaded7_ippodromo (N = 20 + M = 40, cascaded.yaml's shape and weights),
 singletrack_ippodromo (N = 60), and (round 4) every recorded run with the obstacle barrier on
 (singletrack_obstacles_shoe, cascaded_obstacles{1,2}_ippodromo, cascaded_obstacles_shoe,
 race_obstacles_shoe's two cars) plus the shoe-track runs without obstacles (singletrack_shoe,
-race{1,2}_shoe's two cars).  Not included: cascaded_giantObstacle{1,2,3}_ippodromo -- their
+race{1,2}_shoe's two cars), and (round 5) race1_ippodromo's single-track N = 50 and the cascaded
+tails M = 15 / 25 / 35 of race1/2/3_ippodromo -- every recorded horizon shape.  Not included: cascaded_giantObstacle{1,2,3}_ippodromo -- their
 obstacle set is recorded nowhere (the runs' configs hold only the controller; the reference's
 ippodromo.yaml has the ordinary obstacles, and the recorded paths swerve to |ey| 5-6 m round a
 different large obstacle in each run: at s ~ 30 in run 1, s ~ 170-185 on opposite sides in runs
@@ -32,7 +33,11 @@ RUNS = [("cascaded7_ippodromo", "cascaded"), ("singletrack_ippodromo", "singletr
         ("cascaded_obstacles2_ippodromo", "cascaded"), ("cascaded_obstacles_shoe", "cascaded"),
         ("race_obstacles_shoe", "singletrack"),
         ("race_obstacles_shoe", "cascaded"), ("singletrack_shoe", "singletrack"), ("race1_shoe", "singletrack"),
-        ("race1_shoe", "cascaded"), ("race2_shoe", "singletrack"), ("race2_shoe", "cascaded")]
+        ("race1_shoe", "cascaded"), ("race2_shoe", "singletrack"), ("race2_shoe", "cascaded"),
+        # round 5: every remaining recorded horizon shape -- single-track N = 50 (race1_ippodromo,
+        # BASELINE.md's first row) and the cascaded tails M = 15 / 25 / 35 (race1/2/3_ippodromo)
+        ("race1_ippodromo", "singletrack"), ("race1_ippodromo", "cascaded"), ("race2_ippodromo", "cascaded"),
+        ("race3_ippodromo", "cascaded")]
 
 
 def key(run, ctl):

@@ -113,3 +113,18 @@ def test_replay_obstacle_and_shoe_runs(data, run):
     assert r["dw_median"] < (1e-3 if casc else 1e-4)
     assert r["frac_within_1pct"] > (0.25 if casc else 0.6)
     assert r["plan_dev_median_m"] < (0.05 if casc else 0.01)
+
+
+# Round 5: every remaining recorded horizon shape (tests/golden/make_replay_kat.py) -- single-track
+# N = 50 (race1_ippodromo, BASELINE.md's first row: 431 recorded IPOPT commands) and the cascaded
+# tails M = 15 / 25 / 35 (race1/2/3_ippodromo).  Same converged setting, windows and bars as the
+# round-4 runs above, stated before measuring: single-track <= 1 % non-solved, median |dFx| < 1 N,
+# median |dw| < 1e-4, > 60 % within 1 %, median plan deviation < 0.01 m; cascaded <= 1 %, < 20 N,
+# < 1e-3, > 25 %, < 0.05 m; every plan finite.
+REPLAY_R5 = ["race1_ippodromo:singletrack", "race1_ippodromo:cascaded", "race2_ippodromo:cascaded",
+             "race3_ippodromo:cascaded"]
+
+
+@pytest.mark.parametrize("run", REPLAY_R5)
+def test_replay_every_recorded_horizon_shape(data, run):
+    test_replay_obstacle_and_shoe_runs(data, run)

@@ -132,6 +132,22 @@ struct CrSmem {
 #define CR_RES_RECUR 1  // dual residual carried by the steps (0: adjoint sweep every iteration)
 #endif
 
+#ifndef CR_POLISH
+#define CR_POLISH 3  // active-set polish rounds after each converged QP (0: off, the round-4 kernel)
+#endif
+#ifndef CR_AL_RHO
+#define CR_AL_RHO 1e2  // polish: augmented-Lagrangian weight of an active row, x (1 + max diag Q) / |c|^2
+#endif
+#ifndef CR_AL_PASSES
+#define CR_AL_PASSES 16
+#endif
+#ifndef CR_CERT_PTOL
+#define CR_CERT_PTOL 1e-11  // polish certificate: inactive-row violation, x (1 + max |q|)
+#endif
+#ifndef CR_CERT_DTOL
+#define CR_CERT_DTOL 1e-12  // polish certificate: wrong-signed multiplier, x (1 + max |q|)
+#endif
+
 #ifndef CR_KEEP_ITERATE
 #define CR_KEEP_ITERATE 1  // a later QP without a solution keeps the iterate (0: applies it, step non-solved)
 #endif
@@ -261,6 +277,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
 
   int it_total = 0, it_max = 0;
   bool all_conv = true, any_fail = false, stopped = false;  // stopped: a later QP ended the SQP early
+  bool all_pol = true;  // every converged QP's answer certified by the active-set polish
   double last_res = 0.0, last_mu = 0.0;
   const double tol_r = 1e-10, tol_mu = 1e-13;
 
@@ -883,6 +900,27 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       return wmax(rmax);
     };
 
+    // stage lanes: s.u.q.Qt[k] = Qc + sum_i w_i c_i c_i' (the barrier weights of the interior
+    // point, or the augmented-Lagrangian weights of the polish)
+    auto put_qt = [&](const double* w) {
+      double Qt[NQ];
+#pragma unroll
+      for (int e = 0; e < NQ; ++e) Qt[e] = Qc[e];
+      Qt[Q00] += w[0];
+      Qt[Q33] += w[1] + w[2];
+      Qt[Q88] += w[8] + w[9];
+      Qt[Q77] += w[10] + w[11];
+      constexpr int ix[5] = {0, 1, 2, 3, 7};
+#pragma unroll
+      for (int r = 0; r < 5; ++r)
+#pragma unroll
+        for (int a = 0; a < 5; ++a)
+#pragma unroll
+          for (int e = a; e < 5; ++e) Qt[qslot(ix[a], ix[e])] += w[3 + r] * R.c[r][a] * R.c[r][e];
+#pragma unroll
+      for (int e = 0; e < NQ; ++e) s.u.q.Qt[k][e] = Qt[e];
+    };
+
     // ---------------- interior point (Mehrotra predictor-corrector) ----------------
     int it = 0;
     bool conv = false, fail = false;
@@ -917,22 +955,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       if (stl) {
 #pragma unroll
         for (int e = 0; e < 9; ++e) s.u.q.g[k][e] = grk[e];
-        double Qt[NQ];
-#pragma unroll
-        for (int e = 0; e < NQ; ++e) Qt[e] = Qc[e];
-        Qt[Q00] += wg[0];
-        Qt[Q33] += wg[1] + wg[2];
-        Qt[Q88] += wg[8] + wg[9];
-        Qt[Q77] += wg[10] + wg[11];
-        constexpr int ix[5] = {0, 1, 2, 3, 7};
-#pragma unroll
-        for (int r = 0; r < 5; ++r)
-#pragma unroll
-          for (int a = 0; a < 5; ++a)
-#pragma unroll
-            for (int e = a; e < 5; ++e) Qt[qslot(ix[a], ix[e])] += wg[3 + r] * R.c[r][a] * R.c[r][e];
-#pragma unroll
-        for (int e = 0; e < NQ; ++e) s.u.q.Qt[k][e] = Qt[e];
+        put_qt(wg);
       } else {
         rpm = 0.0;
         mus = 0.0;
@@ -1035,6 +1058,114 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     }
     it_total += it;
     it_max = max(it_max, it);
+
+    // ---------------- active-set polish (round 5; st_sqp.hip has the same) ----------------
+    // The interior point's iterate is only as close to the QP's optimum as its weakly active rows
+    // allow (tests/test_gpu_certify.py: up to 1e-6 in the scaled units on the bench batch, 1e-3 N).
+    // The QP on the active set it identified (lambda > s) is solved exactly by an augmented
+    // Lagrangian (one Riccati factorisation of Q + sum_A rho_i c_i c_i') whose passes are Newton
+    // steps from the current point (the gradient recomputed stage-locally, so the factor's rounding
+    // is refined away) with multiplier updates, then certified (inactive rows feasible, active
+    // multipliers nonnegative); otherwise the violated rows join and the negative ones leave.
+    bool pol_qp = false;
+    if (CR_POLISH > 0 && conv) {
+      double hs = 0.0, qs = 0.0;
+      if (stl) {
+        hs = fmax(fmax(fmax(Qc[Q00], Qc[Q11]), fmax(Qc[Q22], Qc[Q33])),
+                  fmax(fmax(Qc[Q44], Qc[Q55]), fmax(fmax(Qc[Q66], Qc[Q77]), Qc[Q88])));
+#pragma unroll
+        for (int e = 0; e < 9; ++e) qs = fmax(qs, fabs(qc[e]));
+      }
+      hs = 1.0 + wmax(hs);
+      qs = 1.0 + wmax(qs);
+      // row i's weight (recomputed where used: an array of 12 would stay live across the polish)
+      const double rho_h = CR_AL_RHO * hs;
+      auto rho = [&](int i) -> double {
+        double cn2 = 1.0;
+        if (i >= 3 && i < 8) {
+          cn2 = 0.0;
+#pragma unroll
+          for (int a = 0; a < 5; ++a) cn2 += R.c[i - 3][a] * R.c[i - 3][a];
+        }
+        return rho_h / fmax(cn2, 1e-30);
+      };
+      uint32_t act = 0;  // bit i: row i active
+#pragma unroll
+      for (int i = 0; i < NR; ++i) act |= (stl && R.m(i) > 0.0 && la[i] > sl[i]) ? (1u << i) : 0u;
+#pragma unroll 1
+      for (int round = 0; round < CR_POLISH; ++round) {
+        // the interior point's slacks / multipliers are dead from here: sl holds the polish's
+        // iterate and la its multipliers (a later round starts from the last round's)
+        double w[NR], val[NR];
+        double* const lm = la;
+        double* const vp = sl;
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          const bool ai = (act >> i) & 1u;
+          w[i] = ai ? rho(i) : 0.0;
+          lm[i] = ai ? lm[i] : 0.0;
+        }
+        if (stl) put_qt(w);
+        WSYNC();
+        if (!factor()) break;  // keep the interior point's iterate
+#pragma unroll
+        for (int e = 0; e < 9; ++e) vp[e] = vk[e];
+        bool al_conv = false;
+#pragma unroll 1
+        for (int p = 0; p < CR_AL_PASSES; ++p) {
+          if (stl) {
+            double g9[9], y[NR];
+            row_values(R, vp, val);
+#pragma unroll
+            for (int i = 0; i < NR; ++i) y[i] = ((act >> i) & 1u) ? lm[i] + rho(i) * (val[i] - R.d[i]) : 0.0;
+            qmul(Qc, vp, g9);
+#pragma unroll
+            for (int e = 0; e < 9; ++e) g9[e] += qc[e];
+            row_adjoint(R, y, g9);
+#pragma unroll
+            for (int e = 0; e < 9; ++e) s.u.q.g[k][e] = g9[e];
+          }
+          WSYNC();
+          lq_solve();
+          double emax = 0.0;
+          if (stl) {
+#pragma unroll
+            for (int e = 0; e < 9; ++e) vp[e] += s.u.q.g[k][e];
+            row_values(R, vp, val);
+#pragma unroll
+            for (int i = 0; i < NR; ++i) {
+              const double r = ((act >> i) & 1u) ? val[i] - R.d[i] : 0.0;
+              lm[i] += rho(i) * r;
+              emax = fmax(emax, fabs(r));
+            }
+          }
+          WSYNC();
+          if (wmax(emax) <= 1e-14 * qs) {
+            al_conv = true;
+            break;
+          }
+        }
+        // certificate: inactive rows feasible, active multipliers nonnegative
+        uint32_t viol = 0, neg = 0;
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          const bool ai = (act >> i) & 1u;
+          viol |= (stl && R.m(i) > 0.0 && !ai && val[i] - R.d[i] > CR_CERT_PTOL * qs) ? (1u << i) : 0u;
+          neg |= (ai && lm[i] < -CR_CERT_DTOL * qs) ? (1u << i) : 0u;
+        }
+        if (al_conv && __all((viol | neg) ? 0 : 1) != 0) {
+          if (stl) {
+#pragma unroll
+            for (int e = 0; e < 9; ++e) vk[e] = vp[e];
+          }
+          pol_qp = true;
+          break;
+        }
+        act = (act | viol) & ~neg;
+      }
+      WSYNC();
+    }
+    all_pol = all_pol && (pol_qp || !conv);
     // a QP after the first without a solution (an infeasible linearisation: the interior point
     // diverges) refuses its own step and ends the SQP at the current iterate, whose rollout is
     // s.xs; the step's status is then that of the QPs before it -- the kinematic SQP's rule
@@ -1090,7 +1221,8 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       constexpr size_t DS = VC_CASC_DIAG_COLS;  // the ABI's row stride (no section counters here)
       A.diag[(size_t)b * DS + 0] = last_res;
       A.diag[(size_t)b * DS + 1] = last_mu;
-      A.diag[(size_t)b * DS + 2] = double((any_fail ? 1 : 0) | (all_conv ? 2 : 0) | (stopped ? 16 : 0));
+      A.diag[(size_t)b * DS + 2] =
+          double((any_fail ? 1 : 0) | (all_conv ? 2 : 0) | (all_pol ? 4 : 0) | (stopped ? 16 : 0));
       A.diag[(size_t)b * DS + 3] = double(it_max);
     }
   }

@@ -35,30 +35,6 @@
 #include "vc_models.hpp"
 #include "vcmpc.h"
 
-#ifndef KIN_BLOCKED
-#define KIN_BLOCKED 1  // interior-point factorisation: panels + matrix-core trailing updates (0: row-per-lane `cholesky`)
-#endif
-#ifndef KIN_G_DOTS_CHUNKED
-#define KIN_G_DOTS_CHUNKED 1  // G-row / G-column dots as chunked lds_dot (0: rolled loops, no scratch)
-#endif
-#ifndef KIN_RES_RECUR
-// interior-point residuals carried by the step instead of recomputed from z, lambda each
-// iteration (0: three matrix-vector products per iteration, the round-3 form)
-#define KIN_RES_RECUR 1
-#endif
-#ifndef KIN_POLISH_BLOCKED
-#define KIN_POLISH_BLOCKED 1  // polish factorisation: the interior point's blocked one (0: row-per-lane)
-#endif
-#ifndef KIN_POLISH_WARM
-#define KIN_POLISH_WARM 1  // polish multipliers start from the interior point's (0: from zero, round 3)
-#endif
-#ifndef KIN_BWD_ROWS
-#define KIN_BWD_ROWS 0  // 1: backward solve reads the factor as packed rows (conflict-free reads, but the
-                        // row stores cost more: 2.8 % slower at C2, profiles/r04/kinab_r04m.txt)
-#endif
-#ifndef KIN_POLISH_CG
-#define KIN_POLISH_CG 1  // polish equality solve: conjugate gradients on the multipliers (0: augmented-Lagrangian passes)
-#endif
 #ifndef KIN_NU_TOL
 #define KIN_NU_TOL 1e-10  // CG also runs until the multiplier step R e is below this x scale (0: off)
 #endif
@@ -67,9 +43,6 @@
 #endif
 #ifndef KIN_EARLY_ROUNDS
 #define KIN_EARLY_ROUNDS 2  // active-set rounds of that attempt before the interior point resumes
-#endif
-#ifndef KIN_TAPIA
-#define KIN_TAPIA 1  // polish's first active set from the last step's Tapia indicators (0: lambda > s)
 #endif
 #ifndef KIN_TAPIA_F
 #define KIN_TAPIA_F 1.02  // ratio gap that makes the indicators decisive (else lambda > s)
@@ -277,7 +250,6 @@ __device__ __forceinline__ double lds_dot(lds_cdouble* a, lds_cdouble* b) {
   return a0 + a1;
 }
 
-#if KIN_G_DOTS_CHUNKED
 // y_r = G_r . v for lane r (v broadcast in s.vz); rows have <= 2(N-1) nonzeros
 template <int N>
 __device__ double grow_dot(const Smem<N>& s, int lane) {
@@ -296,41 +268,6 @@ __device__ double gt_dot(const Smem<N>& s, int lane) {
   return lane < n ? a : 0.0;
 }
 
-#else
-// y_r = G_r . v for lane r (v broadcast in s.vz); rows have <= 2(N-1) nonzeros
-template <int N>
-__device__ double grow_dot(const Smem<N>& s, int lane) {
-  constexpr int NC = Dims<N>::NC;
-  const int r = lane < NC ? lane : 0;
-  lds_cdouble* g = lds_opaque(&s.G[r][0]);
-  lds_cdouble* v = lds_opaque(&s.vz[0]);
-  double a0 = 0.0, a1 = 0.0;
-#pragma unroll 4
-  for (int i = 0; i < 2 * (N - 1); i += 2) {
-    a0 += g[i] * v[i];
-    a1 += g[i + 1] * v[i + 1];
-  }
-  return lane < NC ? a0 + a1 : 0.0;
-}
-
-// (G' v)_j for lane j (v broadcast in s.vc)
-template <int N>
-__device__ double gt_dot(const Smem<N>& s, int lane) {
-  constexpr int n = Dims<N>::n, NC = Dims<N>::NC;
-  constexpr int LD = Dims<N>::LD;
-  const int j = lane < n ? lane : 0;
-  lds_cdouble* g = lds_opaque(&s.G[0][j]);
-  lds_cdouble* v = lds_opaque(&s.vc[0]);
-  double a0 = 0.0, a1 = 0.0;
-#pragma unroll 4
-  for (int r = 0; r < NC; r += 2) {
-    a0 += g[r * LD] * v[r];
-    a1 += g[(r + 1) * LD] * v[r + 1];
-  }
-  return lane < n ? a0 + a1 : 0.0;
-}
-
-#endif
 
 // (H v)_j for lane j (v broadcast in s.vz)
 template <int N>
@@ -357,15 +294,6 @@ __device__ __forceinline__ double rsq_nr(double d) {
 // factorisation's own column reads were issued before (LDS executes a wave's operations in order).
 template <int N>
 __device__ __forceinline__ void store_rows(const double (&Mr)[Dims<N>::n], Smem<N>& s, int lane) {
-#if KIN_BWD_ROWS
-  constexpr int n = Dims<N>::n;
-  static_assert(n * (n - 1) / 2 <= Smem<N>::LC_DUMMY, "packed rows fit the factor storage");
-  wave_sync();
-  const int lim = lane < n ? lane : 0;
-  const int base = lim * (lim - 1) / 2;
-#pragma unroll
-  for (int i = 0; i < n - 1; ++i) s.Lc[i < lim ? base + i : Smem<N>::LC_DUMMY] = Mr[i];
-#endif
 }
 
 // In-place right-looking Cholesky of the SPD matrix whose row `lane` is Mr (the lower
@@ -484,11 +412,7 @@ __device__ double chol_solve(const double (&Lr)[Dims<N>::n], const Smem<N>& s, d
   constexpr int CH = 8;
   static_assert(n % CH == 0, "backward prefetch chunks");
   const int row = lane < n ? lane : 0;
-#if KIN_BWD_ROWS
-  lds_cdouble* col = lds_opaque(&s.Lc[row]);  // col[k (k-1) / 2] = L[k][row] for k > row (store_rows)
-#else
   lds_cdouble* col = lds_opaque(&s.Lc[lc_base<n>(row)]);  // col[k] = L[k][row] for k > row
-#endif
   const double dj = s.dinv[row];
   double acc = b;
 #pragma unroll
@@ -496,16 +420,6 @@ __device__ double chol_solve(const double (&Lr)[Dims<N>::n], const Smem<N>& s, d
   acc *= dj;                                                           // y
   double x = 0.0;
   double lk[2][CH];
-#if KIN_BWD_ROWS
-  auto fetch = [&](int c, int buf) {  // L[k][row] for k = n-1-c*CH ... n-CH-c*CH
-    // lanes at or below k read the next rows' entries (finite; multiplied only after x_row is out)
-#pragma unroll
-    for (int q = 0; q < CH; ++q) {
-      const int k = n - 1 - c * CH - q;
-      lk[buf][q] = col[k * (k - 1) / 2];
-    }
-  };
-#else
   lds_cdouble* zero = lds_opaque(&s.zrow[0]);
   auto fetch = [&](int c, int buf) {  // L[k][row] for k = n-1-c*CH ... n-CH-c*CH
     // a lane whose row is at or below every k of the chunk reads zeros at one shared address
@@ -514,7 +428,6 @@ __device__ double chol_solve(const double (&Lr)[Dims<N>::n], const Smem<N>& s, d
 #pragma unroll
     for (int q = 0; q < CH; ++q) lk[buf][q] = src[n - 1 - c * CH - q];
   };
-#endif
   fetch(0, 0);
 #pragma unroll
   for (int c = 0; c < n / CH; ++c) {  // L' x = y: lane i < k needs L[k][i]
@@ -1137,7 +1050,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
   double last_res = 0.0, last_mu = 0.0;
   double Mr[n];
   // Residuals: dual rd = H z + g + C' lambda (lane j < n), primal r = C z + s - d per row side.
-  // KIN_RES_RECUR: computed once at the start point and then carried by the step -- the
+  // Computed once at the start point and then carried by the step -- the
   // direction solves the linearised KKT system, whose dual and primal rows are linear, so a step
   // of length al scales every residual by (1 - al) exactly (H dz + wb dz + eb + G'(wc G dz + ec)
   // = -rd by the normal equations; d1 = dz + rlo_b etc. by construction).  That replaces three
@@ -1164,7 +1077,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
   auto max_residual = [&]() {
     return wave_max(fmax(fmax(fabs(rd), fmax(fabs(rlo_b), fabs(rhi_b))), fmax(fabs(rlo_c), fabs(rhi_c))));
   };
-  int tapb = 0;  // KIN_TAPIA: two bits per constraint side (1 active, 2 inactive, 0 undecided)
+  int tapb = 0;  // Tapia indicators: two bits per constraint side (1 active, 2 inactive, 0 undecided)
   // KIN_EARLY_F: the polish is first tried once the interior point reaches tol_early; if that
   // attempt does not certify within KIN_EARLY_ROUNDS rounds the interior point resumes from its
   // iterate (the polish changes none of its state) to tol and the polish runs again.  With the
@@ -1181,10 +1094,10 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
     for (;;) {
       no_hoist();
       VC_TSTAMP(t_res0)
-      if (!KIN_RES_RECUR || it == 0) true_residuals();
+      if (it == 0) true_residuals();
       const double mu = wave_sum(bx.slo * bx.llo + bx.shi * bx.lhi + cs.slo * cs.llo + cs.shi * cs.lhi) / mtot;
       double res = max_residual();
-      if (KIN_RES_RECUR && it > 0 && res <= tol_cur && mu <= tol_cur) {
+      if (it > 0 && res <= tol_cur && mu <= tol_cur) {
         true_residuals();  // the carried residual would stop here: the true one decides
         res = max_residual();
       }
@@ -1202,18 +1115,11 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
       wave_sync();
       VC_TACC(T_RESID, t_res0)
       VC_TSTAMP(t_build0)
-#if KIN_BLOCKED
       d4 nacc[Tiles<N>::NT];
       build_normal_acc<N>(nacc, s, wlo_b + whi_b, hjj, lane);
       VC_TACC(T_BUILD, t_build0)
       VC_TSTAMP(t_chol0)
       const bool chol_ok = factor_blocked<N>(Mr, nacc, s, lane);
-#else
-      build_normal_mfma<N>(Mr, s, wlo_b + whi_b, hjj, lane);
-      VC_TACC(T_BUILD, t_build0)
-      VC_TSTAMP(t_chol0)
-      const bool chol_ok = cholesky<N>(Mr, s, lane);
-#endif
       VC_TACC(T_CHOL, t_chol0)
       if (!chol_ok) {
         // The barrier weights lambda/s of the active set (~1/mu) have made the
@@ -1274,7 +1180,6 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
           pp1 = d1 * d2; pp2 = d3 * d4; pp3 = e1 * e2; pp4 = e3 * e4;
         } else {
           const double al = 0.99 * amax;
-#if KIN_TAPIA
           {
             // Tapia indicators of this step (El-Bakry, Tapia, Tsuchiya, Zhang 1996): near the
             // solution an active side's slack shrinks by a factor the multiplier does not, an
@@ -1289,7 +1194,6 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
             tapb = tap(d2, illo_b, d1, islo_b) | (tap(d4, ilhi_b, d3, ishi_b) << 2) |
                    (tap(e2, illo_c, e1, islo_c) << 4) | (tap(e4, ilhi_c, e3, ishi_c) << 6);
           }
-#endif
           z = (lane < n) ? z + al * dz : z;
           bx.slo += al * d1; bx.llo += al * d2; bx.shi += al * d3; bx.lhi += al * d4;
           cs.slo += al * e1; cs.llo += al * e2; cs.shi += al * e3; cs.lhi += al * e4;
@@ -1315,19 +1219,12 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
     constexpr double AL_RHO = KIN_AL_RHO;
     constexpr int AL_MAX = 16;
     const double ptol = 1e-9 * scale, dtol = KIN_DUAL_TOL * scale;
-#if KIN_TAPIA
     // decisive indicators first, lambda > s where the last step left them undecided
     auto guess = [&](bool has, double l, double sv, int t) { return has && (t == 1 || (t == 0 && l > sv)); };
     bool alo_b = guess(bx.hasLo, bx.llo, bx.slo, tapb & 3);
     bool ahi_b = guess(bx.hasHi, bx.lhi, bx.shi, (tapb >> 2) & 3);
     bool alo_c = guess(cs.hasLo, cs.llo, cs.slo, (tapb >> 4) & 3);
     bool ahi_c = guess(cs.hasHi, cs.lhi, cs.shi, (tapb >> 6) & 3);
-#else
-    bool alo_b = bx.hasLo && bx.llo > bx.slo;
-    bool ahi_b = bx.hasHi && bx.lhi > bx.shi;
-    bool alo_c = cs.hasLo && cs.llo > cs.slo;
-    bool ahi_c = cs.hasHi && cs.lhi > cs.shi;
-#endif
     const int max_rounds = tol_cur > tol ? min(A.qp.polish, KIN_EARLY_ROUNDS) : A.qp.polish;
 #pragma unroll 1
     for (int round = 0; round < max_rounds; ++round) {
@@ -1358,7 +1255,6 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
       s.vc[lane] = rho_c;
       wave_sync();
       VC_TSTAMP(t_pf0)
-#if KIN_POLISH_BLOCKED
       {
         // the interior point's path: H + G' diag(rho_c) G in the accumulator tiles (s.vc =
         // rho_c; zero weights where no row is active), fixed rows / columns set to the identity
@@ -1387,36 +1283,16 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
           break;
         }
       }
-#else
-      if (__ballot(rho_c > 0.0)) {
-        build_normal_mfma<N>(Mr, s, 0.0, hjj, lane);
-      } else {  // no active state row (most problems): the reduced Hessian only
-        const int j0 = lane < n ? lane : 0;
-        lds_cdouble* Hrow = lds_opaque(&s.H[j0][0]);
-#pragma unroll
-        for (int i = 0; i < n; ++i) Mr[i] = (lane < n) ? Hrow[i] : 0.0;
-      }
-#pragma unroll
-      for (int i = 0; i < n; ++i) {  // reduced matrix: fixed rows/cols -> identity
-        const bool fi = (fmask >> i) & 1ull;
-        Mr[i] = fixed ? (i == lane ? 1.0 : 0.0) : (fi ? 0.0 : Mr[i]);
-      }
-      if (!cholesky<N>(Mr, s, lane)) {
-        pchol_fail = true;
-        break;
-      }
-#endif
       VC_TACC(T_UPDATE, t_pf0)
       VC_TSTAMP(t_pal0)
       // multiplier estimate: the interior point's own (lambda_hi - lambda_lo of an active row,
       // the sign convention of the check below), so the augmented-Lagrangian passes start next
-      // to the fixed point instead of at 0 (KIN_POLISH_WARM; the fixed point does not depend on
+      // to the fixed point instead of at 0 (the fixed point does not depend on
       // the start: same certified z).  Rows the AL does not enforce (rho_c = 0) keep 0.
-      double nu_c = (KIN_POLISH_WARM && act && rho_c > 0.0) ? ((ahi_c ? cs.lhi : 0.0) - (alo_c ? cs.llo : 0.0)) : 0.0;
-#if KIN_POLISH_CG
+      double nu_c = (act && rho_c > 0.0) ? ((ahi_c ? cs.lhi : 0.0) - (alo_c ? cs.llo : 0.0)) : 0.0;
       // The passes are Richardson's iteration nu += R e on S dnu = e(nu), S = G_A M^-1 G_A' (M the
       // factored matrix, R = diag(rho_c)): it contracts by 1 - min eig(R S) per pass, up to 14 passes
-      // on the slowest C2 problems (profiles/r04/sec_r04f.txt).  KIN_POLISH_CG solves the same
+      // on the slowest C2 problems (profiles/r04/sec_r04f.txt).  Conjugate gradients solve the same
       // system by conjugate gradients preconditioned with R -- same cost per iteration (one
       // triangular solve pair, one G' and one G product), same fixed point, and R S has its
       // eigenvalues clustered below 1, so CG needs a few.  z follows nu exactly: dz = -M^-1 G' dnu.
@@ -1477,32 +1353,6 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
         }
       }
       VC_TACC(T_PAL, t_pal0)
-#else
-      double zp = 0.0, emax = 0.0;
-#pragma unroll 1
-      for (int pass = 0; pass < AL_MAX; ++pass) {
-        no_hoist();
-        wave_sync();
-        s.vc[lane] = (lane < NC) ? (nu_c - rho_c * bnd_c) : 0.0;
-        wave_sync();
-        const double rhs = (lane < n) ? (fixed ? zfix : (base - gt_dot<N>(s, lane))) : 0.0;
-        zp = chol_solve<N>(Mr, s, rhs, lane);
-        wave_sync();
-        s.vz[lane] = (lane < n) ? zp : 0.0;
-        wave_sync();
-        // G_r . zp (zp carries zfix on fixed lanes): multiplier update
-        const double yr = grow_dot<N>(s, lane);
-        const bool al_act = act && rho_c > 0.0;
-        const double e = al_act ? (yr - (alo_c ? cs.lo : cs.hi)) : 0.0;
-        nu_c += rho_c * e;
-        emax = wave_max(fabs(e));
-#ifdef VC_TIMING
-        tacc[T_PPASS] += 1;
-#endif
-        if (emax <= 1e-14 * scale) break;
-      }
-      VC_TACC(T_PAL, t_pal0)
-#endif
       // KKT check of zp
       wave_sync();
       s.vz[lane] = (lane < n) ? zp : 0.0;
@@ -1510,9 +1360,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
       wave_sync();
       const double grad = (lane < n) ? (h_dot<N>(s, lane) + gj + gt_dot<N>(s, lane)) : 0.0;
       const double ypc = grow_dot<N>(s, lane);
-#if KIN_POLISH_CG
       emax = wave_max(al_act ? fabs(ypc - bnd_al) : 0.0);  // the true violation, not CG's recurrence
-#endif
       // dual violations (> 0 is wrong-signed): box multiplier of an active bound is
       // -grad (upper) / grad (lower); state-row multiplier is nu (upper) / -nu (lower)
       const double dv_b = (lane < n) ? (ahi_b ? grad : (alo_b ? -grad : -1.0)) : -1.0;

@@ -156,7 +156,10 @@ __global__ __launch_bounds__(64) void kin_merit_kernel(KinMeritArgs A) {
   const double sc = fmax(1.0, fabs(phi0));
   const double p1 = bcast(phi, 0);
   // no Armijo step: near a KKT point the promised decrease is below the merit's resolution
-  const bool noise = !mask && qp_ok && fabs(D) <= NOISE_D * sc && p1 <= phi0 + NOISE_PHI * sc;
+  // (finite merits only: from outside the domain, phi0 = inf, the comparisons below hold for any p1,
+  // an infinite one included, and the full step would leave the domain again)
+  const bool noise = !mask && qp_ok && isfinite(phi0) && isfinite(p1) && fabs(D) <= NOISE_D * sc &&
+                     p1 <= phi0 + NOISE_PHI * sc;
   const int pick = mask ? __builtin_ctzll(mask) : (noise ? 0 : -1);
   const double al = pick >= 0 ? ldexp(1.0, -pick) : 0.0;
   const double phia = pick >= 0 ? bcast(phi, pick) : phi0;

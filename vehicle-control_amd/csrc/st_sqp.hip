@@ -1098,27 +1098,31 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       }
       hs = 1.0 + wmax(hs);
       qs = 1.0 + wmax(qs);
-      double rho[NR];
-#pragma unroll
-      for (int i = 0; i < NR; ++i) {
+      // row i's weight (recomputed where used: an array of 12 would stay live across the polish)
+      const double rho_h = ST_AL_RHO * hs;
+      auto rho = [&](int i) -> double {
         double cn2 = 1.0;
         if (i >= 3 && i < 8) {
           cn2 = 0.0;
 #pragma unroll
           for (int a = 0; a < 5; ++a) cn2 += R.c[i - 3][a] * R.c[i - 3][a];
         }
-        rho[i] = ST_AL_RHO * hs / fmax(cn2, 1e-30);
-      }
+        return rho_h / fmax(cn2, 1e-30);
+      };
       bool act[NR];
 #pragma unroll
       for (int i = 0; i < NR; ++i) act[i] = stl && R.m[i] > 0.0 && la[i] > sl[i];
 #pragma unroll 1
       for (int round = 0; round < ST_POLISH; ++round) {
-        double w[NR], lm[NR], vp[9], val[NR];
+        // the interior point's slacks / multipliers are dead from here: sl holds the polish's
+        // iterate and la its multipliers (a later round starts from the last round's)
+        double w[NR], val[NR];
+        double* const lm = la;
+        double* const vp = sl;
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
-          w[i] = act[i] ? rho[i] : 0.0;
-          lm[i] = act[i] ? la[i] : 0.0;
+          w[i] = act[i] ? rho(i) : 0.0;
+          lm[i] = act[i] ? lm[i] : 0.0;
         }
         if (stl) put_qt(w);
         WSYNC();
@@ -1132,7 +1136,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
             double g9[9], y[NR];
             row_values(R, vp, val);
 #pragma unroll
-            for (int i = 0; i < NR; ++i) y[i] = act[i] ? lm[i] + rho[i] * (val[i] - R.d[i]) : 0.0;
+            for (int i = 0; i < NR; ++i) y[i] = act[i] ? lm[i] + rho(i) * (val[i] - R.d[i]) : 0.0;
             qmul(Qc, vp, g9);
 #pragma unroll
             for (int e = 0; e < 9; ++e) g9[e] += qc[e];
@@ -1150,7 +1154,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
 #pragma unroll
             for (int i = 0; i < NR; ++i) {
               const double r = act[i] ? val[i] - R.d[i] : 0.0;
-              lm[i] += rho[i] * r;
+              lm[i] += rho(i) * r;
               emax = fmax(emax, fabs(r));
             }
           }

@@ -44,11 +44,26 @@ DYN_OBS_SQP = 10
 
 def dyn_qp_block(config) -> dict:
     """The dynamic controllers' `qp` block: the config's own, with at least DYN_OBS_SQP SQP
-    iterations per step when obstacles are on."""
+    iterations per step when obstacles are on -- unless the block sets `obs_sqp_iters`, which
+    then is the count with obstacles.  A raised count is reported once per process (a silent
+    3 -> 10 roughly triples the cost of a step)."""
     qp = dict(config.get("qp") or {})
     if config.get("obstacles"):
-        qp["sqp_iters"] = max(int(qp.get("sqp_iters", 0)), DYN_OBS_SQP)
+        if qp.get("obs_sqp_iters") is not None:
+            qp["sqp_iters"] = int(qp["obs_sqp_iters"])
+        elif int(qp.get("sqp_iters", 0)) < DYN_OBS_SQP:
+            global _OBS_WARNED
+            if not _OBS_WARNED:
+                import warnings
+                warnings.warn(f"obstacles on: qp.sqp_iters {qp.get('sqp_iters')} raised to {DYN_OBS_SQP} per step "
+                              f"(DYN_OBS_SQP); set qp.obs_sqp_iters to choose the count", stacklevel=2)
+                _OBS_WARNED = True
+            qp["sqp_iters"] = DYN_OBS_SQP
+    qp.pop("obs_sqp_iters", None)
     return qp
+
+
+_OBS_WARNED = False
 
 
 def dyn_horizon_params(s0, ux_pred, mpc_dt, k_of_s):
