@@ -60,7 +60,7 @@
 extern "C" {
 #endif
 
-#define VCMPC_ABI_VERSION 10
+#define VCMPC_ABI_VERSION 11
 #define VC_MAX_OBSTACLES 16
 
 typedef struct vc_ctx vc_ctx;
@@ -169,7 +169,11 @@ typedef struct vc_casc_mpc {
  * dist - (r + 0.1) is floored at margin_min. */
 typedef struct vc_obstacles {
   int32_t n;          /* number of obstacles, 0..VC_MAX_OBSTACLES */
-  int32_t pad_;
+  int32_t inside;     /* 0: the margin is floored at margin_min everywhere below it (default);
+                         1: inside an obstacle beyond the floor band (dist - (r + 0.1) < -margin_min)
+                         the QP model takes the reference's own barrier w ds / (dist - r - 0.1),
+                         negative there; the floor then acts only in |dist - (r + 0.1)| <= margin_min
+                         (ABI 11; the kinematic merit keeps its C1 extension) */
   double margin_min;  /* floor of dist - (r + 0.1) in the barrier's derivatives [m] */
   double s[VC_MAX_OBSTACLES], ey[VC_MAX_OBSTACLES], radius[VC_MAX_OBSTACLES];
 } vc_obstacles;

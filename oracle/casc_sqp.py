@@ -205,7 +205,8 @@ def casc_qp(x0, ubar, kappa, ds, p, W, tyre="fiala"):
         add_square(np.where(ey < lo, W["w_b"] * dsk, 0.0), ey - lo, row)
         add_square(np.where(ey > hi, W["w_b"] * dsk, 0.0), ey - hi, row)
         if W.get("obstacles"):
-            p_o, q_o = OB.ey_model(s, ey, W["w_obs"] * dsk, W["obstacles"], W.get("obs_margin_min", OB.MARGIN_MIN))
+            p_o, q_o = OB.ey_model(s, ey, W["w_obs"] * dsk, W["obstacles"], W.get("obs_margin_min", OB.MARGIN_MIN),
+                                   inside=bool(W.get("obs_inside", False)))
             gram.add(q_o, row)
             g[:] += p_o[:, None] * row
 

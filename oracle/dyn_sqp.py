@@ -239,7 +239,8 @@ def dyn_qp(x0, ubar, kappa, ds, p, W, tyre="linear"):
         add_square(np.where(ey > W["ey_max"], W["w_b"] * ds[:, k], 0.0), ey - W["ey_max"], row)
         if W.get("obstacles"):  # cascaded_mpc.py:173-176, convexified in ey (obstacles.py)
             p_o, q_o = OB.ey_model(xbar[:, k, IS], ey, W["w_obs"] * ds[:, k], W["obstacles"],
-                                   W.get("obs_margin_min", OB.MARGIN_MIN))
+                                   W.get("obs_margin_min", OB.MARGIN_MIN),
+                                   inside=bool(W.get("obs_inside", False)))
             gram.add(q_o, row)
             g[:] += p_o[:, None] * row
         add_square(W["w_w"], ubar[:, k, IW], np.broadcast_to(eye[2 * k + 1], (B, n)))
@@ -327,3 +328,35 @@ def dyn_horizon_params(state, state_prediction, mpc_dt, N, k_of_s):
     ds = np.full(N, mpc_dt) * state_prediction[IUX, :N]
     s_traj = np.cumsum(ds) - ds[0] + state[IS]
     return ds, np.asarray(k_of_s(s_traj), np.float64)
+
+
+def closed_loop_cost(X, U, dt, p, W, obstacles=()):
+    """The reference NLP's single-track stage cost (cascaded_mpc.py:139-176, every if_else exact,
+    no proximal term) summed along an EXECUTED closed loop instead of a plan: state X[T, 8] and the
+    input U[T, 2] applied from it, with ds_n = s_{n+1} - s_n the arc length driven in step n, plus
+    the time term w_time t (cascaded_mpc.py:290-291) at the end.  A scalar by which two closed
+    loops of the same lap (the build's and the reference's recorded one) compare under the
+    reference's own objective; returns the total and its terms."""
+    X, U = np.asarray(X, np.float64), np.asarray(U, np.float64)
+    T = min(len(X), len(U)) - 1
+    x, u = X[:T], U[:T]
+    ds = np.maximum(X[1:T + 1, IS] - X[:T, IS], 1e-9)
+    ey = x[:, IEY]
+    terms = {
+        "deviation": W["w_dev"] * ds * ey ** 2,
+        "boundary": W["w_b"] * ds * (np.where(ey < W["ey_min"], (ey - W["ey_min"]) ** 2, 0.0)
+                                     + np.where(ey > W["ey_max"], (ey - W["ey_max"]) ** 2, 0.0)),
+        "w": W["w_w"] * u[:, IW] ** 2,
+    }
+    sf = stage_functions(np.concatenate([x[:, :4], u[:, :1]], axis=1), p)
+    terms["slip"] = W["w_slip"] * (np.maximum(np.real(sf["slip_f"]), 0.0) ** 2 + np.maximum(np.real(sf["slip_r"]), 0.0) ** 2)
+    dFx = np.diff(u[:, IFX], append=u[-1, IFX])
+    terms["Fx_slew"] = W["w_Fx"] / ds * dFx ** 2
+    bar = np.zeros(T)
+    for so, eo, r in obstacles:
+        bar += W["w_obs"] * ds / (np.hypot(x[:, IS] - so, ey - eo) - (r + 0.1))
+    terms["obstacles"] = bar
+    out = {k: float(v.sum()) for k, v in terms.items()}
+    out["time"] = float(W["w_time"] * T * dt)
+    out["total"] = float(sum(out.values()))
+    return out

@@ -146,7 +146,8 @@ def kin_qp(x0, ubar, kappa, ds, L, W, x_ws=None):
         add_square(np.where(hi, W["w_b"] * ds[:, k], 0.0), eyv - W["ey_max"], row)
         if W.get("obstacles"):  # kinematic_mpc.py:130-133, convexified in ey (obstacles.py)
             p_o, q_o = OB.ey_model(xbar[:, k, IS], ey, W["w_obs"] * ds[:, k], W["obstacles"],
-                                   W.get("obs_margin_min", OB.MARGIN_MIN))
+                                   W.get("obs_margin_min", OB.MARGIN_MIN),
+                                   inside=bool(W.get("obs_inside", False)))
             gram.add(q_o, row)
             g[:] += (p_o + q_o * (eyv - ey))[:, None] * row
     # input costs: w_w w^2 and slew w_a (a_{n+1}-a_n)^2

@@ -44,8 +44,10 @@ def barrier(s, ey, wds, obstacles):
     return out
 
 
-def ey_model(s, ey, wds, obstacles, margin_min=MARGIN_MIN):
-    """(p, q): slope and clamped curvature of phi at ey (arrays broadcast)."""
+def ey_model(s, ey, wds, obstacles, margin_min=MARGIN_MIN, inside=False):
+    """(p, q): slope and clamped curvature of phi at ey (arrays broadcast).  inside: beyond the
+    band |margin| <= margin_min inside an obstacle the reference's own (negative) barrier
+    instead of the floor (vc_obstacles.inside, csrc/vc_kernels.hpp)."""
     s, ey, wds = (np.asarray(v, np.float64) for v in (s, ey, wds))
     shape = np.broadcast(s, ey, wds).shape
     ps, qs = np.zeros(shape), np.zeros(shape)
@@ -54,7 +56,8 @@ def ey_model(s, ey, wds, obstacles, margin_min=MARGIN_MIN):
         e = ey - eo
         d = np.sqrt(a * a + e * e)
         dc = np.maximum(d, 1e-6)
-        m = np.maximum(d - (r + 0.1), margin_min)
+        m0 = d - (r + 0.1)
+        m = np.where(inside & (m0 < -margin_min), m0, np.maximum(m0, margin_min))
         d1 = e / dc
         dd = (a * a) / (dc * dc * dc)
         im = 1.0 / m

@@ -41,7 +41,7 @@ def config_for(run, rec):
     return cfg
 
 
-def replay(run, g, rec, sqp, skip=5, qp=None, dump=None, segments=1):
+def replay(run, g, rec, sqp, skip=5, qp=None, dump=None, segments=1, cfg_extra=None):
     """segments > 1: the run's T steps are cut into that many contiguous windows, replayed side
     by side as one batch (each window starts from the controller's own initial guess, so its
     first `skip` steps are the warm-up and are not compared) -- the same per-step comparison
@@ -53,6 +53,7 @@ def replay(run, g, rec, sqp, skip=5, qp=None, dump=None, segments=1):
     track = Track.load(track_of(run))
     car = DynamicCar(load_config("dynamic_car"), track, tyre="fiala")
     cfg = config_for(run, rec)
+    cfg.update(cfg_extra or {})   # e.g. obstacle_inside (vc_obstacles.inside: the reference's barrier inside)
     cfg["qp"] = dict(cfg["qp"], sqp_iters=sqp, **(qp or {}))
     X, U, P = g[f"{run}/state_traj"], g[f"{run}/action_traj"], g[f"{run}/preds"]
     T = min(len(X), len(U))

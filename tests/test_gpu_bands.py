@@ -185,6 +185,21 @@ def test_recorded_obstacle_and_shoe_runs_within_bands(key):
                  ey_absmax=float(np.abs(Xl[:, 5]).max()), nfail=int(out["nfail"].sum()), clearance=clear)
     print(f"{key}: build {stats} | recorded steps={rec['steps']} complete={rec['complete']} s_end={rec['s_end']:.1f} "
           f"Ux_median={rec['Ux_median']:.2f} |ey|max={rec['ey_absmax']:.2f} clearance={rec['clearance_min']}")
+    if rec["obstacles"] and rec["complete"]:
+        # the reference NLP's own stage cost (no prox) summed along both executed laps (oracle/dyn_sqp.py
+        # closed_loop_cost): which closed loop is better by the reference's objective
+        from oracle import dyn_sqp as D
+        from oracle import models as M
+        g = np.load(os.path.join(GOLDEN, "replay_kat.npz"))
+        if f"{key}/state_traj" in g:
+            p = M.dyn_params_from_config(load_config("dynamic_car"))
+            W = D.dyn_weights(cfg)
+            obs = [(o.s, o.ey, o.radius) for o in track.obstacles]
+            Xr, Ur = g[f"{key}/state_traj"], g[f"{key}/action_traj"]
+            lap = int(rec["lap_steps"])
+            jb = D.closed_loop_cost(X[:n + 1], U[:n + 1], 0.05, p, W, obs)
+            jr = D.closed_loop_cost(Xr[:lap + 1], Ur[1:lap + 2], 0.05, p, W, obs)
+            print(f"  closed-loop reference cost (lap): build {jb['total']:.2f} {jb} | recorded {jr['total']:.2f} {jr}")
     if rec["complete"]:
         assert len(done), f"no lap in {K} steps: s = {X[-1, 4]:.1f} of {track.length:.1f}"
         assert abs(n - rec["lap_steps"]) <= 0.04 * rec["lap_steps"], (n, rec["lap_steps"])

@@ -128,3 +128,25 @@ REPLAY_R5 = ["race1_ippodromo:singletrack", "race1_ippodromo:cascaded", "race2_i
 @pytest.mark.parametrize("run", REPLAY_R5)
 def test_replay_every_recorded_horizon_shape(data, run):
     test_replay_obstacle_and_shoe_runs(data, run)
+
+
+# Round 5: race_obstacles_shoe with the reference's own barrier inside the obstacle (vc_obstacles.inside,
+# ABI 11): the recorded cars drive 1.48 m inside an obstacle, where the reference's barrier
+# w ds / (dist - r - 0.1) is negative and the build's default floors the margin at 0.05 m.  With the
+# inside mode the QP model equals the reference's barrier everywhere except the band |margin| <= 0.05 m.
+# Bars: the round-4 ones above, stated before this measurement.
+@pytest.mark.parametrize("run", ["race_obstacles_shoe:singletrack", "race_obstacles_shoe:cascaded"])
+def test_replay_race_obstacles_shoe_reference_barrier(data, run):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(GOLDEN), "..", "scripts"))
+    from replay_recorded import replay
+    recs = json.loads(str(data["configs"]))
+    r = replay(run, data, recs[run], 40, qp={"prox": 0.01}, segments=24, cfg_extra={"obstacle_inside": True})
+    print(json.dumps({k: v for k, v in r.items() if k != "example_plan"}))
+    casc = run.endswith(":cascaded")
+    assert r["plan_nan_steps"] == 0
+    assert r["nonsolved"] <= 0.01 * r["steps"]
+    assert r["dFx_median"] < (20.0 if casc else 1.0)
+    assert r["dw_median"] < (1e-3 if casc else 1e-4)
+    assert r["frac_within_1pct"] > (0.25 if casc else 0.6)
+    assert r["plan_dev_median_m"] < (0.05 if casc else 0.01)

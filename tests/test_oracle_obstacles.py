@@ -113,3 +113,27 @@ def test_host_packing_and_track_obstacles():
     assert o.n == 7 and o.radius[0] == 1.0 and o.ey[2] == 3.0 and o.margin_min == _abi.OBS_MARGIN_MIN
     with pytest.raises(ValueError):
         obstacles_struct([(0, 0, 1)] * (_abi.VC_MAX_OBSTACLES + 1))
+
+
+def test_inside_mode_is_the_reference_barrier_inside():
+    """vc_obstacles.inside (ABI 11): inside an obstacle beyond the floor band the QP model is the
+    reference's own barrier w ds / (dist - r - 0.1) (negative there, cascaded_mpc.py:173-176): its
+    slope is the central difference of phi; the curvature is phi'' clamped at 0.  In the band
+    |margin| <= margin_min and outside the obstacle the two modes agree; default mode unchanged."""
+    obs = [(30.0, 0.0, 1.0)]
+    wds = 0.7
+    s = np.full(5, 30.4)
+    ey = np.array([0.0, 0.3, -0.5, 1.1, 2.5])          # margins -1.1, -0.8, -0.47, ~0.07, 1.43
+    m0 = np.hypot(s - 30.0, ey) - 1.1
+    p1, q1 = OB.ey_model(s, ey, wds, obs, inside=True)
+    p0, q0 = OB.ey_model(s, ey, wds, obs)
+    h = 1e-6
+    fd = (OB.barrier(s, ey + h, wds, obs) - OB.barrier(s, ey - h, wds, obs)) / (2 * h)
+    fdd = (OB.barrier(s, ey + h, wds, obs) - 2 * OB.barrier(s, ey, wds, obs) + OB.barrier(s, ey - h, wds, obs)) / h ** 2
+    deep = m0 < -OB.MARGIN_MIN
+    assert deep.sum() == 3
+    np.testing.assert_allclose(p1[deep], fd[deep], rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(q1[deep], np.maximum(fdd[deep], 0.0), rtol=1e-3, atol=1e-6)
+    np.testing.assert_array_equal(p1[~deep], p0[~deep])
+    np.testing.assert_array_equal(q1[~deep], q0[~deep])
+    assert not np.allclose(p1[deep], p0[deep])

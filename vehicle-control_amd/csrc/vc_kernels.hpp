@@ -93,7 +93,9 @@ __device__ __forceinline__ void obstacle_ey_model(const vc_obstacles& o, T s, T 
     const T d = sqrt(d2);
     const T dc = d > T(1e-6) ? d : T(1e-6);
     const T m0 = d - (T(o.radius[j]) + T(0.1));
-    const T m = m0 > mmin ? m0 : mmin;
+    // floored at margin_min; with o.inside the reference's own (negative) barrier beyond the
+    // band |m0| <= margin_min inside the obstacle (the slope w ds / m^2 is continuous at -mmin)
+    const T m = (o.inside && m0 < -mmin) ? m0 : (m0 > mmin ? m0 : mmin);
     const T d1 = e / dc;                  // d'(ey)
     const T dd = (a * a) / (dc * dc * dc);  // d''(ey)
     const T im = T(1) / m;

@@ -431,6 +431,7 @@ int vc_set_obstacles(vc_ctx* c, int n, const double* s, const double* ey, const 
   if (n > 0 && (!s || !ey || !radius)) return fail(c, VC_E_ARG, "null pointer");
   vc_obstacles o{};
   o.n = n;
+  o.inside = c->p.obs.inside;  // the barrier mode is the context's (vc_create's params)
   o.margin_min = margin_min > 0 ? margin_min : c->p.obs.margin_min;
   for (int j = 0; j < n; ++j) {
     o.s[j] = s[j];

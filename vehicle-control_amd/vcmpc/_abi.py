@@ -12,7 +12,7 @@ import os
 
 LIB_NAME = "libvcmpc.so"
 LIB_PATH = os.environ.get("VCMPC_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME))
-ABI_VERSION = 10
+ABI_VERSION = 11
 VC_MAX_OBSTACLES = 16
 OBS_MARGIN_MIN = 0.05  # VC_OBS_MARGIN_MIN (csrc/vc_kernels.hpp)
 
@@ -58,7 +58,7 @@ class vc_qp(C.Structure):
 
 
 class vc_obstacles(C.Structure):
-    _fields_ = [("n", C.c_int32), ("pad_", C.c_int32), ("margin_min", C.c_double),
+    _fields_ = [("n", C.c_int32), ("inside", C.c_int32), ("margin_min", C.c_double),
                 ("s", C.c_double * VC_MAX_OBSTACLES), ("ey", C.c_double * VC_MAX_OBSTACLES),
                 ("radius", C.c_double * VC_MAX_OBSTACLES)]
 

@@ -71,11 +71,14 @@ def kin_mpc_struct(cfg) -> _abi.vc_kin_mpc:
         w_obs=float(cw.get("obstacles", 0.0)))
 
 
-def obstacles_struct(obstacles=None, margin_min: float = _abi.OBS_MARGIN_MIN) -> _abi.vc_obstacles:
+def obstacles_struct(obstacles=None, margin_min: float = _abi.OBS_MARGIN_MIN,
+                     inside: bool = False) -> _abi.vc_obstacles:
     """Pack an obstacle list [(s, ey, radius), ...] (the `obstacle_data` rows of the
     reference's config/environment/*.yaml, read at environment/track.py:131-138).
-    None / [] = no barrier terms (the controller's ``obstacles: False``)."""
+    None / [] = no barrier terms (the controller's ``obstacles: False``).  inside: the
+    reference's own barrier inside an obstacle beyond the margin floor (vc_obstacles.inside)."""
     o = _abi.vc_obstacles()
+    o.inside = 1 if inside else 0
     rows = [tuple(float(v) for v in r) for r in (obstacles or [])]
     if len(rows) > _abi.VC_MAX_OBSTACLES:
         raise ValueError(f"{len(rows)} obstacles > VC_MAX_OBSTACLES = {_abi.VC_MAX_OBSTACLES}")
@@ -147,12 +150,12 @@ def casc_mpc_struct(cfg) -> _abi.vc_casc_mpc:
 
 
 def make_params(kin_car=None, dyn_car=None, kin_mpc=None, dyn_mpc=None, tyre: str = "fiala",
-                obstacles=None) -> _abi.vc_params:
+                obstacles=None, obstacle_inside: bool = False) -> _abi.vc_params:
     """Pack whichever configs are given into one ``vc_params`` (others zeroed).
     The QP knobs come from the controller config given (kinematic or dynamic);
     ``obstacles`` is the [(s, ey, radius), ...] list the barrier terms use."""
     p = _abi.vc_params()
-    p.obs = obstacles_struct(obstacles)
+    p.obs = obstacles_struct(obstacles, inside=obstacle_inside)
     if kin_car is not None:
         p.kin_car = _abi.vc_kin_car(l=float(kin_car["car"]["l"]))
     if dyn_car is not None:

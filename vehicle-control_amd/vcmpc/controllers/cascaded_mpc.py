@@ -101,7 +101,8 @@ class BatchedSingleTrackMPC(Controller):
         self.ctx = Context(model=_abi.VC_MODEL_DYNAMIC, N=self.N, max_batch=self.B, dtype=vdt, device=device,
                            params=make_params(dyn_car=car.config, dyn_mpc=dict(config, qp=dyn_qp_block(config)),
                                               tyre=getattr(car, "tyre", "fiala"),
-                                              obstacles=obstacle_list(car, config)))
+                                              obstacles=obstacle_list(car, config),
+                                              obstacle_inside=bool(config.get("obstacle_inside", False))))
         # warm starts: cascaded_mpc.py:72-76
         rng = np.random.RandomState(seed) if seed is not None else np.random
         self.state_prediction = np.ones((self.B, self.ns, self.N))
@@ -174,7 +175,8 @@ class BatchedCascadedMPC(Controller):
                            device=device,
                            params=make_params(dyn_car=car.config, dyn_mpc=dict(config, qp=dyn_qp_block(config)),
                                               tyre=getattr(car, "tyre", "fiala"),
-                                              obstacles=obstacle_list(car, config)))
+                                              obstacles=obstacle_list(car, config),
+                                              obstacle_inside=bool(config.get("obstacle_inside", False))))
         # warm starts: cascaded_mpc.py:72-76 (ones over H columns, Ux + 3 on the single-track part)
         rng = np.random.RandomState(seed) if seed is not None else np.random
         self.state_prediction = np.ones((self.B, self.ns, self.H))

@@ -60,7 +60,8 @@ class BatchedRacingSimulator:
         if self.dynamic:
             from .controllers.cascaded_mpc import dyn_qp_block  # obstacles: DYN_OBS_SQP iterations
             params = make_params(dyn_car=car.config, dyn_mpc=dict(cfg, qp=dyn_qp_block(cfg)),
-                                 tyre=getattr(car, "tyre", "fiala"), obstacles=obstacle_list(track, cfg))
+                                 tyre=getattr(car, "tyre", "fiala"), obstacles=obstacle_list(track, cfg),
+                                 obstacle_inside=bool(cfg.get("obstacle_inside", False)))
             if self.M > 0:  # cascaded SQP, fp64 (csrc/casc_ric.hip)
                 model, dtype = _abi.VC_MODEL_CASCADED, _abi.VC_F64
             else:
