@@ -54,7 +54,9 @@ FLOP_ITER = (2 * N_DEC * sum(2 * (1 + r % (N_HORIZON - 1)) for r in range(NC_ROW
              + N_DEC ** 3 // 3 + 2 * 2 * N_DEC * N_DEC                                  # Cholesky, 2 solves
              + 4 * (2 * NC_ROWS * N_DEC) + 2 * 2 * N_DEC * N_DEC)                       # mat-vecs
 FP64_VALU_PEAK = 78.6  # TFLOP/s
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r04", "pmc_summary.json")
+# newest committed PMC summary first (scripts/pmc_profile.sh -> scripts/pmc_summary.py)
+PMC_SUMMARIES = [os.path.join(ROOT, "profiles", r, "pmc_summary.json") for r in ("r05", "r04")]
+PMC_SUMMARY = next((p for p in PMC_SUMMARIES if os.path.exists(p)), PMC_SUMMARIES[0])
 
 # ---- C3: dynamic single-track SQP (fp32, N = 40) ------------------------------------
 C3_N, C3_NX = 40, 8

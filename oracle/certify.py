@@ -256,6 +256,25 @@ def _sqp_worker(job):
         return out
 
 
+def _gap_worker(job):
+    with _limit_threads():
+        H, g, C, d = _qp_data(job)
+        q = lambda z: 0.5 * np.einsum("bi,bij,bj->b", z, H, z) + np.einsum("bi,bi->b", g, z)
+        return q(job["z"]) - q(job["z_ref"])
+
+
+def objective_gap(kind, z, z_ref, common, per_problem, chunk=CHUNK, nproc=None):
+    """[B] q(z) - q(z_ref) of the oracle-built QPs (q = 1/2 z'Hz + g'z)."""
+    B = len(z)
+    jobs = []
+    for lo in range(0, B, chunk):
+        hi = min(B, lo + chunk)
+        j = dict(common, kind=kind, z=np.ascontiguousarray(z[lo:hi]), z_ref=np.ascontiguousarray(z_ref[lo:hi]))
+        j.update({k: np.ascontiguousarray(v[lo:hi]) for k, v in per_problem.items()})
+        jobs.append(j)
+    return np.concatenate(pool_map(_gap_worker, jobs, nproc))
+
+
 def certify_sqp_batch(kind, us, stop, common, per_problem, chunk=256, nproc=None):
     """certify every QP of an SQP batch (see _sqp_worker); us [K+1, B, H, 2], stop [K, B]."""
     B = us.shape[1]

@@ -27,7 +27,7 @@ for SET in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
   [ -z "$KEEP" ] && continue
   echo "== pass $i:$KEEP"
   timeout -k 10 -s KILL 240 rocprofv3 --kernel-trace --pmc $KEEP -d "$OUT/p$i" -o run -f csv -- \
-      python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-c5 --no-cpu-baseline $EXTRA > "$OUT/p$i.log" 2>&1
+      python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-c5 --no-cpu-baseline --no-latency $EXTRA > "$OUT/p$i.log" 2>&1
   rc=$?
   echo "   rc=$rc"
   if [ $rc -ge 124 ]; then echo "fatal rc=$rc, stopping"; exit $rc; fi

@@ -157,3 +157,38 @@ def test_sqp_batch_every_qp_certified(name, dyn_params):
     assert not fails, fails[:20]
     assert (solved.mean() >= 0.997), np.bincount(st_k[-1])
     assert err[solved].max() < U_TOL
+
+
+def test_kin_ltv_interior_point_status_rests_on_the_true_residual(kin_W):
+    """kin_ltv carries its interior-point residuals by the step (1 - alpha)
+    instead of recomputing them; the carried value must not end the loop on its own.  With the
+    polish off (qp.polish = 0) the returned z is the interior point's iterate, and for every problem
+    reported solved: diag[0] (the kernel's final residual / scale, now the true one) is within the
+    stopping tolerance; the host-side primal infeasibility of z (C z - d, oracle-built QP) is below
+    tol * scale (C z - d = r - s <= r with s >= 0); and the objective gap to the oracle's exact optimum
+    is at the duality-gap level m * mu <= m * tol * scale (with the slack of a few residual terms).  A
+    carried residual that drifted from the truth would show in both host checks."""
+    from vcmpc import Context, _abi
+    from vcmpc.config import load_config, make_params
+    from vcmpc.workload import kinematic_batch
+    cfg = load_config("kinematic_mpc")
+    cfg["qp"] = dict(cfg["qp"], polish=0)
+    tol = float(cfg["qp"]["tol"])
+    p = make_params(kin_car=load_config("kinematic_car"), kin_mpc=cfg)
+    d = kinematic_batch(1024, N=20, seed=31)
+    with Context(model=_abi.VC_MODEL_KINEMATIC, N=20, max_batch=1024, dtype=_abi.VC_F64, params=p) as c:
+        u0, xs, us, st, it, dg = c.solve(d["x0"], d["kappa"], d["ds"], d["ubar"].copy(), diag=True)
+    z = (us - d["ubar"]).reshape(1024, 40)
+    r = CF.certify_batch("kin", z, dict(W=kin_W, L=L), {k: d[k] for k in ("x0", "ubar", "kappa", "ds")}, chunk=256)
+    gap = CF.objective_gap("kin", z, r["z_exact"], dict(W=kin_W, L=L), {k: d[k] for k in ("x0", "ubar", "kappa", "ds")})
+    solved = st == 0
+    s = r["scale"]
+    m = 4 * 20 + 3 * 19
+    print(f"polish off: solved {int(solved.sum())}/1024, diag[0] max {dg[solved, 0].max():.2e} (tol {tol:.0e}); host "
+          f"pfeas/scale max {np.max(r['pfeas'][solved] / s[solved]):.2e}; objective gap to the exact optimum / (m scale) "
+          f"max {np.max(gap[solved] / (m * s[solved])):.2e}, min {np.min(gap[solved] / (m * s[solved])):.2e}")
+    assert solved.mean() > 0.99
+    assert dg[solved, 0].max() <= tol * (1 + 1e-12)
+    assert np.max(r["pfeas"][solved] / s[solved]) <= tol
+    assert np.max(gap[solved] / (m * s[solved])) <= 10 * tol
+    assert np.min(gap[solved] / s[solved]) >= -1e-12   # the exact optimum is the minimum

@@ -93,8 +93,11 @@ REPLAY_R4 = ["singletrack_obstacles_shoe:singletrack", "race_obstacles_shoe:sing
 # reference's barrier w ds / (dist - r - 0.1) turns negative there); replayed from those states the
 # build's barrier (finite below its 0.05 m margin floor) leaves 10-11 of 851 steps
 # non-solved, 1.2-1.3 % against the 1 % bar stated before measuring.
-XFAIL_REPLAY_R4 = {"race_obstacles_shoe:singletrack": "11 of 851 steps non-solved (bar 1 %), states inside an obstacle",
-                   "race_obstacles_shoe:cascaded": "10 of 851 steps non-solved (bar 1 %), states inside an obstacle"}
+XFAIL_REPLAY_R4 = {"race_obstacles_shoe:singletrack": "11 of 851 steps non-solved (bar 1 %), states inside an obstacle; "
+                                                      "with the reference's own barrier inside (vc_obstacles.inside, "
+                                                      "r05c): 0 non-solved, 57.8 % within 1 % (bar 60 %)",
+                   "race_obstacles_shoe:cascaded": "10 of 851 steps non-solved (bar 1 %), states inside an obstacle; "
+                                                   "with the reference's own barrier inside (r05c): passes every bar"}
 
 
 @pytest.mark.parametrize("run", [pytest.param(r, marks=pytest.mark.xfail(reason=XFAIL_REPLAY_R4[r], strict=False))
@@ -135,7 +138,12 @@ def test_replay_every_recorded_horizon_shape(data, run):
 # w ds / (dist - r - 0.1) is negative and the build's default floors the margin at 0.05 m.  With the
 # inside mode the QP model equals the reference's barrier everywhere except the band |margin| <= 0.05 m.
 # Bars: the round-4 ones above, stated before this measurement.
-@pytest.mark.parametrize("run", ["race_obstacles_shoe:singletrack", "race_obstacles_shoe:cascaded"])
+# Measured (r05c, profiles/r05/pytest_replay_r05c.log): cascaded passes every bar (0 of 851 non-solved, round 4's
+# default barrier 10); single-track 0 non-solved (default 11) and every bar but one: 57.8 % of the steps
+# within 1 % of IPOPT's command against the 60 % stated before measuring -- kept as an expected failure.
+@pytest.mark.parametrize("run", [pytest.param("race_obstacles_shoe:singletrack", marks=pytest.mark.xfail(
+    reason="0 of 851 non-solved, median |dFx| 0.5 N, but 57.8 % of the steps within 1 % (bar 60 %)", strict=False)),
+    "race_obstacles_shoe:cascaded"])
 def test_replay_race_obstacles_shoe_reference_barrier(data, run):
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(GOLDEN), "..", "scripts"))

@@ -68,3 +68,25 @@ def test_oracle_sqp_fixed_point_is_the_nlp_optimum(data):
     err = np.abs(r["u_star"] - g["u_nlp"][idx]).max(axis=(1, 2))
     print("oracle SQP (40 iterations) vs NLP optimum: max |du| %.2e" % err.max())
     assert err.max() < 1e-5
+
+
+def test_obstacle_fixture_is_a_kkt_point_of_the_reference_nlp():
+    """tests/golden/kin_nlp_obs_golden.npz (make_kin_nlp_obs_golden.py): the reference NLP with its
+    obstacle barrier (kinematic_mpc.py:130-133) at N = 20 and kinematic.yaml's N = 50.  Every
+    converged entry is a KKT point of that NLP (certificate recomputed here, < 1e-10), its stored
+    barrier margin is the one along X*, and the margin-above-floor entries the GPU test compares
+    exist at both horizons."""
+    from vcmpc.config import load_config
+    g = dict(np.load(os.path.join(GOLDEN, "kin_nlp_obs_golden.npz")))
+    W = Q.kin_weights(load_config("kinematic_mpc"))
+    W["obstacles"] = [tuple(float(v) for v in o) for o in g["obstacles"]]
+    for N in (20, 50):
+        conv, margin = g[f"n{N}_converged"], g[f"n{N}_margin"]
+        assert (conv & (margin > 0.05)).sum() >= 5, N
+        for b in np.nonzero(conv)[0][::3]:
+            P = KN.KinNLP(g[f"n{N}_x0"][b], g[f"n{N}_kappa"][b], g[f"n{N}_ds"][b], 2.5, W)
+            X, U = g[f"n{N}_x_nlp"][b], g[f"n{N}_u_nlp"][b]
+            k = P.kkt(P.pack(X, U))
+            assert k["stat"] < 1e-10 and k["pfeas"] < 1e-10, (N, b, k)
+            m = min(float(np.min(np.hypot(X[1:N, 2] - so, X[1:N, 3] - eo) - (r + 0.1))) for so, eo, r in W["obstacles"])
+            assert abs(m - margin[b]) < 1e-12

@@ -1096,7 +1096,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       for (int round = 0; round < CR_POLISH; ++round) {
         // the interior point's slacks / multipliers are dead from here: sl holds the polish's
         // iterate and la its multipliers (a later round starts from the last round's)
-        double w[NR], val[NR];
+        double w[NR], val[NR] = {};
         double* const lm = la;
         double* const vp = sl;
 #pragma unroll
@@ -1145,7 +1145,9 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
             break;
           }
         }
-        // certificate: inactive rows feasible, active multipliers nonnegative
+        // certificate: inactive rows feasible, active multipliers nonnegative (the row values
+        // recomputed here keep val out of the pass loop's live set)
+        if (stl) row_values(R, vp, val);
         uint32_t viol = 0, neg = 0;
 #pragma unroll
         for (int i = 0; i < NR; ++i) {

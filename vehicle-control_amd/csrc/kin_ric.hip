@@ -81,10 +81,6 @@ struct KrSmem {
   int flag;
 };
 
-#ifndef KR_TAPIA
-#define KR_TAPIA 0  // polish's active set from the last step's Tapia indicators where decisive (kin_ltv.hip);
-                     // off: N = 50 fell from 810 K to 370 K solves/s at equal iterations (profiles/r04/krab_r04x.txt)
-#endif
 #ifndef KR_RES_RECUR
 #define KR_RES_RECUR 1  // dual residual carried by the steps (0: adjoint sweep every iteration)
 #endif
@@ -333,7 +329,6 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
   for (int e = 0; e < NV; ++e) qmax = fmax(qmax, fabs(qc[e]));
   qmax = wmax(stl ? qmax : 0.0);
   double sl[NRW], la[NRW];
-  int tapb = 0;  // KR_TAPIA: two bits per row (1 active, 2 inactive, 0 undecided), from the last step
 #pragma unroll
   for (int i = 0; i < NRW; ++i) {
     sl[i] = m[i] > 0.0 ? fmax(d[i], 1.0) : 1.0;
@@ -604,8 +599,10 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
     bool act[NRW], elr[3];
 #pragma unroll
     for (int i = 0; i < NRW; ++i) {
-      const int t = KR_TAPIA ? (tapb >> (2 * i)) & 3 : 0;
-      act[i] = m[i] > 0.0 && (t == 1 || (t == 0 && la[i] > sl[i]));
+      // lambda > s (the Tapia-indicator guess of kin_ltv.hip was measured here in round 5: polish rounds
+      // mean 1.60 -> 1.05 but max 4 -> 11 at N = 50, B = 1024, and the launch is its slowest problem --
+      // the round-4 2.2x slowdown, with unchanged resources: profiles/r05/kr_tapia_ab_r05c.log)
+      act[i] = m[i] > 0.0 && la[i] > sl[i];
     }
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
@@ -892,14 +889,6 @@ __global__ __launch_bounds__(WTH) void kin_ric_kernel(KinLtvArgs A) {
     rd_carry = (1.0 - alpha) * rdm;
     have_rd = true;
     if (stl) {
-#if KR_TAPIA
-      tapb = 0;
-#pragma unroll
-      for (int i = 0; i < NRW; ++i) {
-        const double lr = 1.0 + alpha * dla[i] / la[i], sr = 1.0 + alpha * dsa[i] / sl[i];
-        tapb |= (m[i] > 0.0 ? (lr > 1.02 * sr ? 1 : (sr > 1.02 * lr ? 2 : 0)) : 0) << (2 * i);
-      }
-#endif
 #pragma unroll
       for (int i = 0; i < NRW; ++i) {
         if (m[i] > 0.0) {

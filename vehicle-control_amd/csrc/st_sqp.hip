@@ -1116,7 +1116,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       for (int round = 0; round < ST_POLISH; ++round) {
         // the interior point's slacks / multipliers are dead from here: sl holds the polish's
         // iterate and la its multipliers (a later round starts from the last round's)
-        double w[NR], val[NR];
+        double w[NR], val[NR] = {};
         double* const lm = la;
         double* const vp = sl;
 #pragma unroll
@@ -1164,7 +1164,9 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
             break;
           }
         }
-        // certificate: inactive rows feasible, active multipliers nonnegative
+        // certificate: inactive rows feasible, active multipliers nonnegative (the row values
+        // recomputed here keep val out of the pass loop's live set)
+        if (stl) row_values(R, vp, val);
         bool viol[NR], neg[NR], bad = false;
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
