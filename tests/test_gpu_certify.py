@@ -32,6 +32,7 @@ from oracle import certify as CF
 pytestmark = pytest.mark.gpu
 
 CERT_TOL = 1e-9     # KKT residuals, x scale
+DIST_TOL = 1e-9     # SQP QPs: or |dz - dz_exact|_inf (scaled units) to the oracle's certified optimum
 U_TOL = 1e-5        # north star: ||u* - u*_oracle||_inf (kinematic: m/s^2, rad/s; SQP: N, rad/s)
 L = 2.5
 
@@ -133,7 +134,13 @@ def test_sqp_batch_every_qp_certified(name, dyn_params):
                              {k: d[k] for k in ("x0", "kappa", "ds")}, chunk=128)
     solved = st_k[-1] == 0
     lim = CERT_TOL * r["scale"]
-    ok = (r["stat"] <= lim) & (r["pfeas"] <= lim) & (r["dfeas"] <= lim) & (r["comp"] <= lim)
+    kkt = (r["stat"] <= lim) & (r["pfeas"] <= lim) & (r["dfeas"] <= lim) & (r["comp"] <= lim)
+    # or within DIST_TOL (scaled units) of the oracle's certified exact optimum of the same QP: the
+    # condensed Hessians of the long single-track horizons reach |H| ~ 1e7 with curvature ~ 3e-2 (cond
+    # ~ 5e8, the RK4 lateral mode), where an answer 6e-11 from the optimum already reads 2e-9 x scale in
+    # condensed stationarity (N = 60 problem 2531, r05e)
+    near = (r["pfeas"] <= lim) & (r["dz_err"] <= DIST_TOL)
+    ok = kkt | near
     sc = CF.sqp_scale(kind, us.shape[2], N)
     err = np.abs(us[-1] - r["u_oracle"]).max(axis=(1, 2))
     print(f"{name}: {int(solved.sum())}/{B} solved at K = {K}; stopped early at QP k: {stop.sum(axis=1).tolist()}; "
@@ -144,7 +151,8 @@ def test_sqp_batch_every_qp_certified(name, dyn_params):
         req = (st_k[k] == 0) & ~stop[k]
         s = r["scale"][k]
         bad = np.nonzero(req & ~ok[k])[0]
-        print(f"  QP {k + 1}: required {int(req.sum())}, certified {int((ok[k] & req).sum())}; max stat "
+        print(f"  QP {k + 1}: required {int(req.sum())}, certified {int((ok[k] & req).sum())} (by distance to the "
+              f"exact optimum: {int((req & ~kkt[k] & near[k]).sum())}); max stat "
               f"{np.max(r['stat'][k][req] / s[req]):.2e} pfeas {np.max(r['pfeas'][k][req] / s[req]):.2e} comp "
               f"{np.max(r['comp'][k][req] / s[req]):.2e}; max |dz - dz_oracle| {r['dz_err'][k][req].max():.2e} "
               f"(scaled); uncertified {[(int(b), float(r['stat'][k][b] / s[b]), float(r['dz_err'][k][b])) for b in bad[:6]]}")

@@ -78,6 +78,16 @@ def test_kin_sqp_converges_to_reference_nlp_optimum(data, ms):
 # NLP with the same objective (the same local optimum, |f_SQP - f_NLP| <= 1e-9 (1 + |f|)) it must equal
 # U_NLP to the north star's 1e-5; every other compared problem is listed with both NLP objective
 # values (a different local optimum is shown, not asserted).
+# The reference NLP is nearly flat along the acceleration inputs (only the 1e-4 slew term prices them,
+# kinematic.yaml), and the barrier's curvature changes fast along the plan: the SQP converges slowly there
+# (r05d at 40 iterations: equal objectives to 9 digits with |du| up to 7e-3, KKT stat 1e-8..3e-6), so the
+# comparison runs 200 SQP iterations with the proximal weight at 1e-6 (the SQP's fixed point does not
+# depend on it; at the contract's 1e-4 each step only closes ~30 % of the gap along directions of
+# curvature ~4e-5, r05e: |du| up to 8e-2 at equal objectives after 200 iterations).
+SQP_ITERS_OBS = 200
+PROX_OBS = 1e-6
+
+
 @pytest.fixture(scope="module")
 def obs_data():
     path = os.path.join(GOLDEN, "kin_nlp_obs_golden.npz")
@@ -96,8 +106,8 @@ def test_kin_sqp_obstacles_vs_reference_nlp(obs_data, N, ms):
     obs = [tuple(float(v) for v in o) for o in obs_data["obstacles"]]
     L = 2.5
     cfg = load_config("kinematic_mpc")
-    cfg["qp"] = dict(cfg["qp"], kin_sqp=SQP_ITERS, ms=ms, trust_a=0.0, trust_w=0.0, max_iter=80,
-                     solver=1)
+    cfg["qp"] = dict(cfg["qp"], kin_sqp=SQP_ITERS_OBS, ms=ms, trust_a=0.0, trust_w=0.0, max_iter=80,
+                     solver=1, prox=PROX_OBS)
     p = make_params(kin_car=load_config("kinematic_car"), kin_mpc=cfg, obstacles=obs)
     B = len(g["x0"])
     x_ws = Q.kin_predict(g["x0"], g["ubar"], g["kappa"], g["ds"], L) if ms else None
@@ -114,7 +124,7 @@ def test_kin_sqp_obstacles_vs_reference_nlp(obs_data, N, ms):
             f_sqp[b], stat_sqp[b] = P.f(z), P.kkt(z)["stat"]
     err = np.abs(us - g["u_nlp"]).max(axis=(1, 2))
     comparable = g["converged"] & (g["margin"] > 0.05) & (st == 0)
-    same = comparable & (stat_sqp < 1e-8) & (np.abs(f_sqp - g["f"]) <= 1e-9 * (1 + np.abs(g["f"])))
+    same = comparable & (stat_sqp < 1e-10) & (np.abs(f_sqp - g["f"]) <= 1e-9 * (1 + np.abs(g["f"])))
     print(f"N={N} ms={ms}: {B} problems, NLP converged {int(g['converged'].sum())} (optimum inside an obstacle's "
           f"margin floor: {int((g['converged'] & (g['margin'] <= 0.05)).sum())}), device solved {int((st == 0).sum())}; "
           f"compared {int(comparable.sum())}, same KKT point {int(same.sum())}, "
