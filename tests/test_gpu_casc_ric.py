@@ -138,3 +138,20 @@ def test_casc_ric_batch_properties(M, dyn_params):
     assert np.isfinite(us[ok]).all() and np.isfinite(xs[ok]).all()
     assert (np.abs(us[:, :N, 1]) <= 0.4 + 1e-12).all()
     np.testing.assert_array_equal(r[2].cpu().numpy(), us)
+
+
+@pytest.mark.parametrize("M", [35, 40])
+def test_casc_ric_j_placement_bit_identical(M):
+    """Round 5: M = 35 / 40 keep the stage Jacobians in LDS while the batch fits the machine at
+    three workgroups per CU and in a global workspace beyond (four per CU; csrc/casc_ric.hip
+    cr_launch): the first 64 problems of a 4,096 batch (global J) equal the same 64 solved alone
+    (LDS J) bit for bit."""
+    from vcmpc.workload import cascaded_batch
+    B = 4096
+    d = cascaded_batch(B, M=M, seed=56)
+    with _ctx(M, B=B) as c:
+        big = c.solve(d["x0"], d["kappa"], d["ds"], d["ubar"].copy(), diag=True)
+        small = c.solve(d["x0"][:64], d["kappa"][:64], d["ds"][:64], d["ubar"][:64].copy(), diag=True)
+    print(f"M={M}: solved {(big[3] == 0).mean():.4f} of {B}")
+    for a, b in zip(big, small):
+        np.testing.assert_array_equal(a[:64], b)

@@ -238,3 +238,23 @@ def test_st_sqp_low_speed_obstacles_converge():
                 u0, xs, us, st, it, dg = ctx.solve(x0, kap, ds, np.zeros((1, 60, 2)), diag=True)
             print(f"{name} obstacles={obs}: status {int(st[0])}, iterations {int(it[0])}, diag {np.round(dg[0], 9)}")
             assert st[0] == 0
+
+
+@pytest.mark.parametrize("N,tyre", [(60, "linear"), (50, "fiala")])
+def test_st_sqp_j_placement_bit_identical(N, tyre):
+    """Round 5: for N >= 45 the launcher keeps the stage Jacobians in LDS while the batch fits the
+    machine at that kernel's occupancy (three workgroups per CU: <= 768 problems on 256 CUs) and
+    moves them to a global workspace beyond (four per CU; csrc/st_sqp.hip st_jg_pick).  The
+    placement changes where J lives, not one floating-point operation: the first 64 problems of a
+    4,096 batch (global J) must equal the same 64 solved alone (LDS J) bit for bit."""
+    from vcmpc.config import load_config
+    from vcmpc.workload import dynamic_batch
+    B = 4096
+    d = {k: v.astype(np.float64) for k, v in dynamic_batch(B, N=N, seed=55, tyre=tyre).items()}
+    cfg = load_config("singletrack_mpc")
+    with _ctx(N, cfg, tyre, max_batch=B) as ctx:
+        big = ctx.solve(d["x0"], d["kappa"], d["ds"], d["ubar"].copy(), diag=True)
+        small = ctx.solve(d["x0"][:64], d["kappa"][:64], d["ds"][:64], d["ubar"][:64].copy(), diag=True)
+    print(f"N={N} {tyre}: solved {(big[3] == 0).mean():.4f} of {B}")
+    for a, b in zip(big, small):
+        np.testing.assert_array_equal(a[:64], b)

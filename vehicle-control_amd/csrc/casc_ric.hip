@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <type_traits>
 
 #include "vc_dual.hpp"
 #include "vc_kernels.hpp"
@@ -83,13 +84,33 @@ struct CrJ {  // [A6 | B6 diag(S, 1 or S)] of one transition + 1 pad (49 doubles
   __device__ __forceinline__ double* operator[](int r) { return m[r]; }
   __device__ __forceinline__ const double* operator[](int r) const { return m[r]; }
 };
+// Round 5: where the LDS copy of J (49 doubles per stage) would cost a workgroup per CU (M = 35 / 40:
+// 48.7 / 53.1 KB, three per CU) it lives in a per-problem global workspace (CascSqpArgs.jws, 384 B
+// per stage; written once per SQP iteration, read by the Riccati passes one stage ahead of use):
+// 29.6 / 31.7 KB, four per CU -- the ceiling, the kernel holds ~480 VGPRs + AGPRs (one wave per SIMD)
+#ifndef CR_J_AHEAD
+#define CR_J_AHEAD 1  // global J: stages of lookahead in the LQ / dual sweeps (2: three operand buffers)
+#endif
+#ifndef CR_FWD_MASKED
+#define CR_FWD_MASKED 0  // global J: forward-sweep operands by exec-masked loads (0: load both, select)
+#endif
+#ifndef CR_J_GLOBAL
+#define CR_J_GLOBAL 1  // 1: where needed (N + M >= 55), 2: every shape, 0: none
+#endif
 template <int N, int M>
+constexpr bool cr_j_global_ok() { return CR_J_GLOBAL == 2 || (CR_J_GLOBAL == 1 && N + M >= 55); }  // (cr_jg_pick)
+template <bool JG>
+using CrJP = std::conditional_t<JG, double*, CrJ*>;  // workspace base (GBuf) or LDS
+struct CrNone {};  // (global: 48 doubles = 384 B per stage, [6][8] row-major)
+
+template <int N, int M, bool JG>
 struct CrSmem {
   static constexpr int H = N + M;
   StageRows8<H> xs;   // prediction: single-track states k < N, point-mass (V, s, ey, epsi, t) k >= N (rotated rows)
   double ub[H][2];    // current ubar (stride 2: the odd stride 3 cost M = 40 its third workgroup per CU)
   double kap[H], dsv[H];
-  CrJ J[H];           // J[k][row][col]: [A6 | B6 diag(S, 1 or S)] of the transition out of stage k
+  // J[k][row][col]: [A6 | B6 diag(S, 1 or S)] of the transition out of stage k (LDS unless JG)
+  std::conditional_t<JG, CrNone, CrJ[H]> J;
   union {
     struct {
       double Qt[H][NQ];  // stage Hessian + barrier, this iteration
@@ -242,14 +263,72 @@ __device__ __forceinline__ void qmul(const double* Q, const double* v, double* o
   o[8] = Q[Q88] * v[8] + Q[Q38] * v[3];
 }
 
-template <int N, int M, int TYRE>
+// Stage loop over k = first, first + step, ... (n stages) with each stage's operands loaded two
+// stages ahead of use (three rotating operand buffers, unrolled by three: no register rotation at
+// the latch).  For the sweeps whose operands come from global memory (JG): a stage of the
+// LQ sweeps is ~100-200 cycles, shorter than an L2 hit under load, so the one-stage lookahead of
+// the LDS sweeps would leave most of the latency exposed.
+template <typename Ops, typename Load, typename Stage>
+__device__ __forceinline__ void stage_loop2(int first, int step, int n, Load&& load, Stage&& stage) {
+  const int hi = n - 1;
+  auto at = [&](int i) { const int k = first + step * (i < hi ? i : hi); return k; };
+  Ops A, B, C;
+  load(at(0), A);
+  load(at(1), B);
+#pragma unroll 1
+  for (int i = 0; i < n; i += 3) {
+    load(at(i + 2), C);
+    stage(at(i), A);
+    if (i + 1 < n) {  // uniform
+      load(at(i + 3), A);
+      stage(at(i + 1), B);
+      if (i + 2 < n) {
+        load(at(i + 4), B);
+        stage(at(i + 2), C);
+      }
+    }
+  }
+}
+
+// stage-Jacobian element (k, r, c): the LDS array, or the global workspace through a buffer
+// resource (GBuf: one offset VGPR per access, bounds-checked to the problem's (N + M) stages)
+template <int N, int M, bool JG>
+__device__ __forceinline__ double cr_jld(CrJP<JG> J, int k, int r, int c) {
+  if constexpr (JG) return GBuf(J, (N + M) * 384).ld((uint32_t)(((k * 6 + r) * 8 + c) * 8));
+  else return J[k].m[r][c];
+}
+template <int N, int M, bool JG>
+__device__ __forceinline__ void cr_jst(CrJP<JG> J, int k, int r, int c, double v) {
+  if constexpr (JG) GBuf(J, (N + M) * 384).st((uint32_t)(((k * 6 + r) * 8 + c) * 8), v);
+  else J[k].m[r][c] = v;
+}
+#define JLD(k, r, c) cr_jld<N, M, JG>(J, (k), (r), (c))
+#define JST(k, r, c, v) cr_jst<N, M, JG>(J, (k), (r), (c), (v))
+
+// global J: the linearisation's stores visible to every lane of the wave before they are read
+template <bool JG>
+__device__ __forceinline__ void cr_jfence() {
+  if constexpr (JG) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+}
+template <int N, int M, bool JG>
+__device__ __forceinline__ CrJP<JG> cr_jac(CrSmem<N, M, JG>& s, int b) {
+  if constexpr (JG) return GBuf::uniform(kargs<CascSqpArgs>()->jws + (size_t)b * (N + M) * 48);
+  else return s.J;
+}
+
+template <int N, int M, int TYRE, bool JG>
 __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
   constexpr int H = N + M;
   static_assert(N >= 2 && M >= 2 && H <= WTH, "one lane per stage");
   // occupancy guard (rocprofv3 LDS_Block_Size: 53,248 B ran three one-wave workgroups per CU --
-  // r03, 201 K solves/s at M = 40 --, 54,272 B two -- r04c/d, 143-147 K); M = 40 must keep three
-  static_assert(M != 40 || sizeof(CrSmem<N, M>) <= 53248, "casc_ric<20, 40> must fit three workgroups per CU");
-  __shared__ CrSmem<N, M> s;
+  // r03, 201 K solves/s at M = 40 --, 54,272 B two -- r04c/d, 143-147 K);
+  // four (one per SIMD: the register file allows no more) need <= 40,960 B
+  static_assert(!JG || sizeof(CrSmem<N, M, JG>) <= 40960, "global-J casc_ric must fit four workgroups per CU");
+  static_assert(JG || M != 40 || sizeof(CrSmem<N, M, JG>) <= 53248, "LDS-J casc_ric<20, 40> must fit three per CU");
+  __shared__ CrSmem<N, M, JG> s;
   const int l = threadIdx.x;
   const int b = xcd_problem(blockIdx.x, A.B);
   const double S = A.w.fx_scale;
@@ -292,6 +371,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     // recomputed inside the loop instead of being hoisted out of it and spilled
     int l = l_out, k = k_out;
     asm volatile("" : "+v"(l), "+v"(k));
+    const CrJP<JG> J = cr_jac<N, M, JG>(s, b);
     const bool stl = l < H;
     const bool pm = k >= N;
     // ---------------- predict (lane 0: RK4, switch, point-mass Euler) ----------------
@@ -392,7 +472,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
           const double s0 = col == 6 ? S : 1.0;
           const int yr[6] = {0, 1, 2, 3, 5, 6};
 #pragma unroll
-          for (int r = 0; r < 6; ++r) s.J[kk][r][col] = xn[yr[r]].d[0] * s0;
+          for (int r = 0; r < 6; ++r) JST(kk, r, col, xn[yr[r]].d[0] * s0);
           s.u.l.trow[kk][tsw(kk, col)] = xn[7].d[0] * s0;
         }
       }
@@ -438,29 +518,31 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
           if (pr == 0) {
 #pragma unroll
             for (int r = 0; r < 3; ++r) {
-              s.J[j][r][0] = (r == 0 ? 1.0 : 0.0) + h * f[yi[r]].d[0];
-              s.J[j][r][1] = (r == 1 ? 1.0 : 0.0) + h * f[yi[r]].d[1];
+              JST(j, r, 0, (r == 0 ? 1.0 : 0.0) + h * f[yi[r]].d[0]);
+              JST(j, r, 1, (r == 1 ? 1.0 : 0.0) + h * f[yi[r]].d[1]);
             }
             s.u.l.trow[j][tsw(j, 0)] = h * f[4].d[0];
             s.u.l.trow[j][tsw(j, 1)] = h * f[4].d[1];
           } else if (pr == 1) {
 #pragma unroll
-            for (int r = 0; r < 3; ++r) s.J[j][r][2] = (r == 2 ? 1.0 : 0.0) + h * f[yi[r]].d[0];
+            for (int r = 0; r < 3; ++r) JST(j, r, 2, (r == 2 ? 1.0 : 0.0) + h * f[yi[r]].d[0]);
             s.u.l.trow[j][tsw(j, 2)] = h * f[4].d[0];
 #pragma unroll
             for (int cc = 3; cc < 6; ++cc) {
-              s.J[j][0][cc] = s.J[j][1][cc] = s.J[j][2][cc] = 0.0;
+              JST(j, 0, cc, 0.0);
+              JST(j, 1, cc, 0.0);
+              JST(j, 2, cc, 0.0);
               s.u.l.trow[j][tsw(j, cc)] = 0.0;
             }
 #pragma unroll
             for (int r = 3; r < 6; ++r)
 #pragma unroll
-              for (int cc = 0; cc < 8; ++cc) s.J[j][r][cc] = (r == 3 && cc == 7) ? 1.0 : 0.0;
+              for (int cc = 0; cc < 8; ++cc) JST(j, r, cc, (r == 3 && cc == 7) ? 1.0 : 0.0);
           } else {
 #pragma unroll
             for (int r = 0; r < 3; ++r) {
-              s.J[j][r][6] = h * f[yi[r]].d[0] * S;
-              s.J[j][r][7] = h * f[yi[r]].d[1] * S;
+              JST(j, r, 6, h * f[yi[r]].d[0] * S);
+              JST(j, r, 7, h * f[yi[r]].d[1] * S);
             }
             s.u.l.trow[j][tsw(j, 6)] = h * f[4].d[0] * S;
             s.u.l.trow[j][tsw(j, 7)] = h * f[4].d[1] * S;
@@ -488,23 +570,29 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     } else if (l == 5) {
       const double Ux = s.xs.at(N - 1, 0), Uy = s.xs.at(N - 1, 1);
       const double q2 = Ux * Ux + Uy * Uy, V = sqrt(q2);
+      // every element stored once (row 3's entries 0..3 and 6 by lanes 0..4 below)
 #pragma unroll
       for (int r = 0; r < 6; ++r)
 #pragma unroll
-        for (int cc = 0; cc < 8; ++cc) s.J[N - 1][r][cc] = 0.0;
-      s.J[N - 1][0][0] = Ux / V;
-      s.J[N - 1][0][1] = Uy / V;
-      s.J[N - 1][1][4] = 1.0;
-      s.J[N - 1][2][0] = -Uy / q2;
-      s.J[N - 1][2][1] = Ux / q2;
-      s.J[N - 1][2][5] = 1.0;
+        for (int cc = 0; cc < 8; ++cc) {
+          if (r == 3 && (cc < 4 || cc == 6)) continue;
+          double v = 0.0;
+          if (r == 0 && cc == 0) v = Ux / V;
+          if (r == 0 && cc == 1) v = Uy / V;
+          if (r == 1 && cc == 4) v = 1.0;
+          if (r == 2 && cc == 0) v = -Uy / q2;
+          if (r == 2 && cc == 1) v = Ux / q2;
+          if (r == 2 && cc == 5) v = 1.0;
+          JST(N - 1, r, cc, v);
+        }
 #pragma unroll
       for (int cc = 0; cc < 8; ++cc) s.u.l.trow[N - 1][tsw(N - 1, cc)] = 0.0;
     }
     WSYNC();
     // the switch's c row: the lateral-force gradient over (Ux, Uy, r, delta | dFx / S)
-    if (l < 4) s.J[N - 1][3][l] = s.u.l.gfy[1 + l];
-    if (l == 4) s.J[N - 1][3][6] = s.u.l.gfy[5] * S;
+    if (l < 4) JST(N - 1, 3, l, s.u.l.gfy[1 + l]);
+    if (l == 4) JST(N - 1, 3, 6, s.u.l.gfy[5] * S);
+    cr_jfence<JG>();
     WSYNC();
 
     // ---------------- stage QP data (lane k, registers) ----------------
@@ -714,8 +802,8 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     auto fac_load = [&](int kk, FacOps& o) {
 #pragma unroll
       for (int e = 0; e < 6; ++e) {
-        o.JT[e] = s.J[kk][e][tj];
-        o.JH[e] = s.J[kk][e][hcic];
+        o.JT[e] = JLD(kk, e, tj);
+        o.JH[e] = JLD(kk, e, hcic);
       }
       o.qv = s.u.q.Qt[kk][hsc];
     };
@@ -795,7 +883,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     };
     auto bwd_load = [&](int kk, const double (*vec)[9], BwdOps& o) {
 #pragma unroll
-      for (int e = 0; e < 6; ++e) o.J6[e] = s.J[kk][e][scol];
+      for (int e = 0; e < 6; ++e) o.J6[e] = JLD(kk, e, scol);
       o.h = vec[kk][sl9];
       const double* pa = l < 7 ? &s.u.q.K[kk][0][bl7] : &s.u.q.Hi[kk][l == 7 ? 0 : 1];
       const double* pb = l < 7 ? &s.u.q.K[kk][1][bl7] : &s.u.q.Hi[kk][l == 7 ? 1 : 2];
@@ -819,11 +907,32 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       double w[8];
     };
     auto fwd_load = [&](int kk, FwdOps& o) {
-      const double* src = fk ? &s.u.q.K[kk][fc][0] : &s.J[kk][fr][0];
-      const double* src7 = fk ? &s.u.q.kk[kk][fc] : &s.J[kk][fr][7];
+      if constexpr (JG && CR_FWD_MASKED) {
+        // no pointer select across address spaces (it would go flat), and no value select
+        // (it would wait for both loads at the load site): exec-masked loads into one buffer
+        if (fk) {
 #pragma unroll
-      for (int e = 0; e < 7; ++e) o.w[e] = src[e];
-      o.w[7] = *src7;
+          for (int e = 0; e < 7; ++e) o.w[e] = s.u.q.K[kk][fc][e];
+          o.w[7] = s.u.q.kk[kk][fc];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o.w[e] = JLD(kk, fr, e);
+        }
+      } else if constexpr (JG) {  // (no pointer select across address spaces: it would go flat)
+#pragma unroll
+        for (int e = 0; e < 7; ++e) {
+          const double kv = s.u.q.K[kk][fc][e], jv = JLD(kk, fr, e);
+          o.w[e] = fk ? kv : jv;
+        }
+        const double k7 = s.u.q.kk[kk][fc], j7 = JLD(kk, fr, 7);
+        o.w[7] = fk ? k7 : j7;
+      } else {
+        const double* src = fk ? &s.u.q.K[kk][fc][0] : &J[kk].m[fr][0];
+        const double* src7 = fk ? &s.u.q.kk[kk][fc] : &J[kk].m[fr][7];
+#pragma unroll
+        for (int e = 0; e < 7; ++e) o.w[e] = src[e];
+        o.w[7] = *src7;
+      }
     };
     auto fwd_stage = [&](int kk, const FwdOps& o, double X) -> double {
       double xb[7];
@@ -840,7 +949,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     };
     auto lq_solve = [&]() {
       BwdOps A1, B1;
-      bwd_load(H - 1, s.u.q.g, A1);
+      if constexpr (!(JG && CR_J_AHEAD == 2)) bwd_load(H - 1, s.u.q.g, A1);
       double pv = 0.0;
       auto bstage = [&](int kk, const BwdOps& o) {
         const double g = bwd_g(kk, o, pv);
@@ -849,28 +958,36 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
         pv = g + t2;
         if (fk) s.u.q.kk[kk][l - 7] = -t2;
       };
+      if constexpr (JG && CR_J_AHEAD == 2) {
+        stage_loop2<BwdOps>(H - 1, -1, H, [&](int kk, BwdOps& o) { bwd_load(kk, s.u.q.g, o); }, bstage);
+      } else {
 #pragma unroll 1
-      for (int kk = H - 1; kk >= 0; kk -= 2) {
-        const int k1 = kk >= 1 ? kk - 1 : 0, k2 = kk >= 2 ? kk - 2 : 0;
-        bwd_load(k1, s.u.q.g, B1);
-        bstage(kk, A1);
-        if (kk >= 1) {
-          bwd_load(k2, s.u.q.g, A1);
-          bstage(kk - 1, B1);
+        for (int kk = H - 1; kk >= 0; kk -= 2) {
+          const int k1 = kk >= 1 ? kk - 1 : 0, k2 = kk >= 2 ? kk - 2 : 0;
+          bwd_load(k1, s.u.q.g, B1);
+          bstage(kk, A1);
+          if (kk >= 1) {
+            bwd_load(k2, s.u.q.g, A1);
+            bstage(kk - 1, B1);
+          }
         }
       }
       WSYNC();
-      FwdOps A2, B2;
-      fwd_load(0, A2);
       double X = 0.0;
+      if constexpr (JG && CR_J_AHEAD == 2) {
+        stage_loop2<FwdOps>(0, 1, H, fwd_load, [&](int kk, const FwdOps& o) { X = fwd_stage(kk, o, X); });
+      } else {
+        FwdOps A2, B2;
+        fwd_load(0, A2);
 #pragma unroll 1
-      for (int kk = 0; kk < H; kk += 2) {
-        const int k1 = kk + 1 < H ? kk + 1 : kk, k2 = kk + 2 < H ? kk + 2 : kk;
-        fwd_load(k1, B2);
-        X = fwd_stage(kk, A2, X);
-        if (kk + 1 < H) {
-          fwd_load(k2, A2);
-          X = fwd_stage(kk + 1, B2, X);
+        for (int kk = 0; kk < H; kk += 2) {
+          const int k1 = kk + 1 < H ? kk + 1 : kk, k2 = kk + 2 < H ? kk + 2 : kk;
+          fwd_load(k1, B2);
+          X = fwd_stage(kk, A2, X);
+          if (kk + 1 < H) {
+            fwd_load(k2, A2);
+            X = fwd_stage(kk + 1, B2, X);
+          }
         }
       }
       WSYNC();
@@ -880,21 +997,25 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     // rounding through the RK4 step's unstable lateral mode at low speed)
     auto dual_residual = [&](bool cl) -> double {
       BwdOps A3, B3;
-      bwd_load(H - 1, s.u.q.g, A3);
+      if constexpr (!(JG && CR_J_AHEAD == 2)) bwd_load(H - 1, s.u.q.g, A3);
       double rho = 0.0, rmax = 0.0;
       auto rstage = [&](int kk, const BwdOps& o) {
         const double g = bwd_g(kk, o, rho);
         rmax = fk ? fmax(rmax, fabs(g)) : rmax;
         rho = cl ? g + o.a * bcast(g, 7) + o.b * bcast(g, 8) : g;  // lanes 0..6: + K' g_u
       };
+      if constexpr (JG && CR_J_AHEAD == 2) {
+        stage_loop2<BwdOps>(H - 1, -1, H, [&](int kk, BwdOps& o) { bwd_load(kk, s.u.q.g, o); }, rstage);
+      } else {
 #pragma unroll 1
-      for (int kk = H - 1; kk >= 0; kk -= 2) {
-        const int k1 = kk >= 1 ? kk - 1 : 0, k2 = kk >= 2 ? kk - 2 : 0;
-        bwd_load(k1, s.u.q.g, B3);
-        rstage(kk, A3);
-        if (kk >= 1) {
-          bwd_load(k2, s.u.q.g, A3);
-          rstage(kk - 1, B3);
+        for (int kk = H - 1; kk >= 0; kk -= 2) {
+          const int k1 = kk >= 1 ? kk - 1 : 0, k2 = kk >= 2 ? kk - 2 : 0;
+          bwd_load(k1, s.u.q.g, B3);
+          rstage(kk, A3);
+          if (kk >= 1) {
+            bwd_load(k2, s.u.q.g, A3);
+            rstage(kk - 1, B3);
+          }
         }
       }
       return wmax(rmax);
@@ -1249,14 +1370,36 @@ bool casc_ric_built(int N, int M) {
   return false;
 }
 
+size_t casc_ric_jws_doubles(int N, int M) {
+#define VC_CASE(n, m) \
+  if (N == n && M == m) return cr_j_global_ok<n, m>() ? (size_t)(n + m) * 48 : 0;
+  VC_CR_SHAPES(VC_CASE)
+#undef VC_CASE
+  return 0;
+}
+
+// J placement per launch (st_sqp.hip st_jg_pick): the LDS-J kernel while the batch fits the machine
+// at its occupancy, the four-per-CU global-J kernel beyond
+template <int N, int M, int TYRE>
+void cr_launch(const CascSqpArgs& a, hipStream_t stream) {
+  if constexpr (cr_j_global_ok<N, M>()) {
+    if (a.B > wg_per_cu(sizeof(CrSmem<N, M, false>)) * device_cus()) {
+      hipLaunchKernelGGL((casc_ric_kernel<N, M, TYRE, true>), dim3(a.B), dim3(WTH), 0, stream, a);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((casc_ric_kernel<N, M, TYRE, false>), dim3(a.B), dim3(WTH), 0, stream, a);
+}
+
 hipError_t launch_casc_ric(const CascSqpArgs& a, int N, int M, hipStream_t stream) {
   if (a.B <= 0) return hipSuccess;
+  if (casc_ric_jws_doubles(N, M) && !a.jws) return hipErrorInvalidValue;  // the workspace the kernel may need
   const bool lin = a.car.tyre == VC_TYRE_LINEAR;
-#define VC_CASE(n, m)                                                                                         \
-  if (N == n && M == m) {                                                                                    \
-    if (lin) hipLaunchKernelGGL((casc_ric_kernel<n, m, VC_TYRE_LINEAR>), dim3(a.B), dim3(WTH), 0, stream, a); \
-    else hipLaunchKernelGGL((casc_ric_kernel<n, m, VC_TYRE_FIALA>), dim3(a.B), dim3(WTH), 0, stream, a);      \
-    return hipGetLastError();                                                                                \
+#define VC_CASE(n, m)                                \
+  if (N == n && M == m) {                           \
+    if (lin) cr_launch<n, m, VC_TYRE_LINEAR>(a, stream); \
+    else cr_launch<n, m, VC_TYRE_FIALA>(a, stream);      \
+    return hipGetLastError();                       \
   }
   VC_CR_SHAPES(VC_CASE)
 #undef VC_CASE

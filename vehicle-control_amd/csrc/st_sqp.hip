@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <type_traits>
 
 #include "vc_dual.hpp"
 #include "vc_kernels.hpp"
@@ -85,17 +86,38 @@ struct StJT {
 };
 template <int N>
 using StJ = StJT<(N == 30 || N == 60) ? 8 : 9>;
+// Round 5: [A6 | B6] in LDS costs 49 doubles per stage (23.5 KB at N = 60) and kept st_sqp<60> at three
+// workgroups per CU.  Where ST_J_GLOBAL is set it lives in a per-problem global workspace instead
+// (StSqpArgs.jws, 384 B = three 128 B lines per stage; written once per SQP iteration by the
+// linearisation, read by the Riccati passes one stage ahead of use, so the L2 latency overlaps the
+// current stage's chain).
+#ifndef ST_J_AHEAD
+#define ST_J_AHEAD 1  // global J: stages of lookahead in the LQ / dual sweeps (2: three operand buffers)
+#endif
+#ifndef ST_FWD_MASKED
+#define ST_FWD_MASKED 0  // global J: forward-sweep operands by exec-masked loads (0: load both, select)
+#endif
+#ifndef ST_J_GLOBAL
+#define ST_J_GLOBAL 1  // 1: where the LDS copy would cost a workgroup per CU (N >= 50), 2: every N, 0: none
+#endif
+// whether the global-J instantiation exists for horizon N (the launcher picks it per batch: st_jg_pick)
+template <int N>
+constexpr bool st_j_global_ok() { return ST_J_GLOBAL == 2 || (ST_J_GLOBAL == 1 && N >= 45); }
+template <int N, bool JG>
+using StJP = std::conditional_t<JG, double*, StJ<N>*>;  // workspace base (GBuf) or LDS
+struct StNone {};  // (global: 48 doubles = 384 B per stage, [6][8] row-major)
 // Row stride of ub: odd (3; conflict-free lane-per-stage reads) where the LDS allows, N = 60 takes
 // 2 -- a block above 53,248 B leaves two workgroups per CU instead of three (measured: rocprofv3
 // LDS_Block_Size 53,248 ran three per CU, 54,272 two; r04).  xs: rotated rows of 8 (StageRows8)
 template <int N>
 constexpr int st_ub_w() { return N == 60 ? 2 : 3; }
-template <int N>
+template <int N, bool JG>
 struct StSmem {
   StageRows8<N> xs;   // prediction (N columns, dynamics for k < N-1), rotated rows (vc_kernels.hpp)
   double ub[N][st_ub_w<N>()];  // current ubar; [2] pad where 3
   double kap[N], dsv[N];
-  StJ<N> J[N];         // J[k][row][col], cols Ux, Uy, r, delta, ey, epsi | dFx, dw
+  // J[k][row][col], cols Ux, Uy, r, delta, ey, epsi | dFx, dw (LDS unless JG)
+  std::conditional_t<JG, StNone, StJ<N>[N]> J;
   union {
     struct {
       double Qt[N][NQ + 1];  // stage Hessian + barrier, this iteration; [NQ] pad
@@ -125,6 +147,9 @@ struct StSmem {
     } l;
   } u;
   int flag[4];
+#ifdef ST_LDS_PAD
+  double lds_pad[ST_LDS_PAD / 8];  // occupancy experiments only (scripts/st_jg_ab.sh)
+#endif
 };
 
 // Workgroup = one wavefront: LDS operations of a wave execute in order, so a sync only has to
@@ -270,13 +295,65 @@ __device__ __forceinline__ void qmul(const double* Q, const double* v, double* o
   o[8] = Q[Q88] * v[8];
 }
 
-template <int N, int TYRE>
+// Stage loop over k = first, first + step, ... (n stages) with each stage's operands loaded two
+// stages ahead of use (three rotating operand buffers, unrolled by three: no register rotation at
+// the latch).  For the sweeps whose operands come from global memory (JG): a stage of the
+// LQ sweeps is ~100-200 cycles, shorter than an L2 hit under load, so the one-stage lookahead of
+// the LDS sweeps would leave most of the latency exposed.
+template <typename Ops, typename Load, typename Stage>
+__device__ __forceinline__ void stage_loop2(int first, int step, int n, Load&& load, Stage&& stage) {
+  const int hi = n - 1;
+  auto at = [&](int i) { const int k = first + step * (i < hi ? i : hi); return k; };
+  Ops A, B, C;
+  load(at(0), A);
+  load(at(1), B);
+#pragma unroll 1
+  for (int i = 0; i < n; i += 3) {
+    load(at(i + 2), C);
+    stage(at(i), A);
+    if (i + 1 < n) {  // uniform
+      load(at(i + 3), A);
+      stage(at(i + 1), B);
+      if (i + 2 < n) {
+        load(at(i + 4), B);
+        stage(at(i + 2), C);
+      }
+    }
+  }
+}
+
+// stage-Jacobian element (k, r, c): the LDS array, or the global workspace through a buffer
+// resource (GBuf: one offset VGPR per access, bounds-checked to the problem's N stages)
+template <int N, bool JG>
+__device__ __forceinline__ double st_jld(StJP<N, JG> J, int k, int r, int c) {
+  if constexpr (JG) return GBuf(J, N * 384).ld((uint32_t)(((k * 6 + r) * 8 + c) * 8));
+  else return J[k].m[r][c];
+}
+template <int N, bool JG>
+__device__ __forceinline__ void st_jst(StJP<N, JG> J, int k, int r, int c, double v) {
+  if constexpr (JG) GBuf(J, N * 384).st((uint32_t)(((k * 6 + r) * 8 + c) * 8), v);
+  else J[k].m[r][c] = v;
+}
+#define JLD(k, r, c) st_jld<N, JG>(J, (k), (r), (c))
+#define JST(k, r, c, v) st_jst<N, JG>(J, (k), (r), (c), (v))
+
+template <int N, bool JG>
+__device__ __forceinline__ StJP<N, JG> st_jac(StSmem<N, JG>& s, const StSqpArgs& A, int b) {
+  if constexpr (JG) return GBuf::uniform(A.jws + (size_t)b * N * 48);
+  else return s.J;
+}
+
+template <int N, int TYRE, bool JG>
 __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
   static_assert(N >= 2 && N <= WTH, "one lane per stage");
   // occupancy guard (rocprofv3 LDS_Block_Size: 53,248 B ran three one-wave workgroups per CU,
-  // 54,272 B two): N = 60 keeps three
-  static_assert(N != 60 || sizeof(StSmem<N>) <= 53248, "st_sqp<60> must fit three workgroups per CU");
-  __shared__ StSmem<N> s;
+  // 54,272 B two; four need <= 40,960 B)
+  // (the kernel holds ~450 VGPRs + AGPRs: one wave per SIMD, so four workgroups per CU is the ceiling)
+#ifndef ST_LDS_PAD
+  static_assert(!JG || sizeof(StSmem<N, JG>) <= 40960, "global-J st_sqp must fit four workgroups per CU");
+  static_assert(JG || N != 60 || sizeof(StSmem<N, JG>) <= 53248, "LDS-J st_sqp<60> must fit three workgroups per CU");
+#endif
+  __shared__ StSmem<N, JG> s;
   const int l = threadIdx.x;
   const int b = xcd_problem(blockIdx.x, A.B);
   DynCoef<double> c = A.car;
@@ -344,6 +421,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     const vc_dyn_mpc& W = A.w;
     DynCoef<double> c = A.car;
     c.tyre = TYRE;
+    const StJP<N, JG> J = st_jac<N, JG>(s, A, b);
     // ---------------- predict: xs = rollout(ubar) ----------------
     // Serial: lane 0 walks the stages (RK4, algebraic tan-alpha form).  After a QP step
     // (tries == 1, ST_NEWTON_ROLLOUT, linear tyre) the new rollout is found instead by chord-Newton
@@ -457,11 +535,27 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
         {
           constexpr int yr[6] = {0, 1, 2, 3, 5, 6};
           const int r = l < 6 ? l : 0;
-          double d = 0.0;
+          // rows kk + 1 (LDS) or kk + 1, kk + 2 (global J) loaded ahead of use
+          constexpr int AH = JG ? ST_J_AHEAD : 1;
+          double d = 0.0, jn[AH][6];
+#pragma unroll
+          for (int a = 0; a < AH; ++a)
+#pragma unroll
+            for (int cc = 0; cc < 6; ++cc) jn[a][cc] = JLD(a < N - 2 ? a : N - 2, r, cc);
           for (int kk = 0; kk < N - 1; ++kk) {
+            double jc[6];
+#pragma unroll
+            for (int cc = 0; cc < 6; ++cc) jc[cc] = jn[0][cc];
+#pragma unroll
+            for (int a = 0; a + 1 < AH; ++a)
+#pragma unroll
+              for (int cc = 0; cc < 6; ++cc) jn[a][cc] = jn[a + 1][cc];
+            const int kn = kk + AH < N - 1 ? kk + AH : N - 2;
+#pragma unroll
+            for (int cc = 0; cc < 6; ++cc) jn[AH - 1][cc] = JLD(kn, r, cc);
             double acc = scr[kk * 8 + r];
 #pragma unroll
-            for (int cc = 0; cc < 6; ++cc) acc += s.J[kk][r][cc] * bcast(d, cc);
+            for (int cc = 0; cc < 6; ++cc) acc += jc[cc] * bcast(d, cc);
             d = acc;
             if (l < 6) s.xs.at(kk + 1, yr[r]) += d;
           }
@@ -526,8 +620,8 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
           const int yr[6] = {0, 1, 2, 3, 5, 6};
 #pragma unroll
           for (int r = 0; r < 6; ++r) {
-            s.J[kk][r][c0] = xn[yr[r]].d[0] * s0;
-            s.J[kk][r][c1] = xn[yr[r]].d[1];
+            JST(kk, r, c0, xn[yr[r]].d[0] * s0);
+            JST(kk, r, c1, xn[yr[r]].d[1]);
           }
           s.u.l.trow[kk][tsw(kk, c0)] = xn[7].d[0] * s0;
           s.u.l.trow[kk][tsw(kk, c1)] = xn[7].d[1];
@@ -547,6 +641,11 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
           }
         }
       }
+    }
+    if constexpr (JG) {
+      // the stage Jacobians went to global memory: visible to every lane before the passes read them
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
     WSYNC();
     ST_ACC(ST_LIN, t_l0)
@@ -696,8 +795,8 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     auto fac_load = [&](int kk, FacOps& o) {
 #pragma unroll
       for (int e = 0; e < 6; ++e) {
-        o.JT[e] = s.J[kk][e][tj];
-        o.JH[e] = s.J[kk][e][hcic];
+        o.JT[e] = JLD(kk, e, tj);
+        o.JH[e] = JLD(kk, e, hcic);
       }
       o.qv = s.u.q.Qt[kk][hsc];
     };
@@ -785,7 +884,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     // vec: s.u.q.g, the right-hand side h (solve) or the gradient gr (dual residual)
     auto bwd_load = [&](int kk, const double (*vec)[9], BwdOps& o) {
 #pragma unroll
-      for (int e = 0; e < 6; ++e) o.J6[e] = s.J[kk][e][scol];
+      for (int e = 0; e < 6; ++e) o.J6[e] = JLD(kk, e, scol);
       o.h = vec[kk][sl9];
       // lane-selected addresses, one unconditional load each (a value select would make
       // the compiler predicate the loads and wait on the whole prefetch)
@@ -812,11 +911,32 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       double w[8];
     };
     auto fwd_load = [&](int kk, FwdOps& o) {
-      const double* src = fk ? &s.u.q.K[kk][fc][0] : &s.J[kk][fr][0];
-      const double* src7 = fk ? &s.u.q.kk[kk][fc] : &s.J[kk][fr][7];
+      if constexpr (JG && ST_FWD_MASKED) {
+        // no pointer select across address spaces (it would go flat), and no value select
+        // (it would wait for both loads at the load site): exec-masked loads into one buffer
+        if (fk) {
 #pragma unroll
-      for (int e = 0; e < 7; ++e) o.w[e] = src[e];
-      o.w[7] = *src7;
+          for (int e = 0; e < 7; ++e) o.w[e] = s.u.q.K[kk][fc][e];
+          o.w[7] = s.u.q.kk[kk][fc];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o.w[e] = JLD(kk, fr, e);
+        }
+      } else if constexpr (JG) {  // (no pointer select across address spaces: it would go flat)
+#pragma unroll
+        for (int e = 0; e < 7; ++e) {
+          const double kv = s.u.q.K[kk][fc][e], jv = JLD(kk, fr, e);
+          o.w[e] = fk ? kv : jv;
+        }
+        const double k7 = s.u.q.kk[kk][fc], j7 = JLD(kk, fr, 7);
+        o.w[7] = fk ? k7 : j7;
+      } else {
+        const double* src = fk ? &s.u.q.K[kk][fc][0] : &J[kk].m[fr][0];
+        const double* src7 = fk ? &s.u.q.kk[kk][fc] : &J[kk].m[fr][7];
+#pragma unroll
+        for (int e = 0; e < 7; ++e) o.w[e] = src[e];
+        o.w[7] = *src7;
+      }
     };
     // one forward stage: writes dv[kk], returns xt_{k+1} (lanes 0..6)
     auto fwd_stage = [&](int kk, const FwdOps& o, double X) -> double {
@@ -838,7 +958,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     // once the backward pass is done with it
     auto lq_solve = [&]() {
       BwdOps A1, B1;
-      bwd_load(N - 1, s.u.q.g, A1);
+      if constexpr (!(JG && ST_J_AHEAD == 2)) bwd_load(N - 1, s.u.q.g, A1);
       double pv = 0.0;  // lanes 0..6: p_{k+1}
       auto bstage = [&](int kk, const BwdOps& o) {
         const double g = bwd_g(kk, o, pv);
@@ -847,28 +967,36 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
         pv = g + t2;
         if (fk) s.u.q.kk[kk][l - 7] = -t2;
       };
+      if constexpr (JG && ST_J_AHEAD == 2) {
+        stage_loop2<BwdOps>(N - 1, -1, N, [&](int kk, BwdOps& o) { bwd_load(kk, s.u.q.g, o); }, bstage);
+      } else {
 #pragma unroll 1
-      for (int kk = N - 1; kk >= 0; kk -= 2) {
-        const int k1 = kk >= 1 ? kk - 1 : 0, k2 = kk >= 2 ? kk - 2 : 0;
-        bwd_load(k1, s.u.q.g, B1);
-        bstage(kk, A1);
-        if (kk >= 1) {
-          bwd_load(k2, s.u.q.g, A1);
-          bstage(kk - 1, B1);
+        for (int kk = N - 1; kk >= 0; kk -= 2) {
+          const int k1 = kk >= 1 ? kk - 1 : 0, k2 = kk >= 2 ? kk - 2 : 0;
+          bwd_load(k1, s.u.q.g, B1);
+          bstage(kk, A1);
+          if (kk >= 1) {
+            bwd_load(k2, s.u.q.g, A1);
+            bstage(kk - 1, B1);
+          }
         }
       }
       WSYNC();
-      FwdOps A2, B2;
-      fwd_load(0, A2);
       double X = 0.0;  // lanes 0..6: xt_k
+      if constexpr (JG && ST_J_AHEAD == 2) {
+        stage_loop2<FwdOps>(0, 1, N, fwd_load, [&](int kk, const FwdOps& o) { X = fwd_stage(kk, o, X); });
+      } else {
+        FwdOps A2, B2;
+        fwd_load(0, A2);
 #pragma unroll 1
-      for (int kk = 0; kk < N; kk += 2) {
-        const int k1 = kk + 1 < N ? kk + 1 : kk, k2 = kk + 2 < N ? kk + 2 : kk;
-        fwd_load(k1, B2);
-        X = fwd_stage(kk, A2, X);
-        if (kk + 1 < N) {
-          fwd_load(k2, A2);
-          X = fwd_stage(kk + 1, B2, X);
+        for (int kk = 0; kk < N; kk += 2) {
+          const int k1 = kk + 1 < N ? kk + 1 : kk, k2 = kk + 2 < N ? kk + 2 : kk;
+          fwd_load(k1, B2);
+          X = fwd_stage(kk, A2, X);
+          if (kk + 1 < N) {
+            fwd_load(k2, A2);
+            X = fwd_stage(kk + 1, B2, X);
+          }
         }
       }
       WSYNC();
@@ -884,7 +1012,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     // barrier gradient: scripts/st_obs_shoe_diag.py, the N = 60 obstacle runs of test_gpu_bands).
     auto dual_residual = [&](bool cl) -> double {
       BwdOps A3, B3;
-      bwd_load(N - 1, s.u.q.g, A3);
+      if constexpr (!(JG && ST_J_AHEAD == 2)) bwd_load(N - 1, s.u.q.g, A3);
       double rho = 0.0, rmax = 0.0;
       auto rstage = [&](int kk, const BwdOps& o) {
         const double g = bwd_g(kk, o, rho);
@@ -892,14 +1020,18 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
         // lanes 0..6: + K' g_u (the lq_solve backward pass's pv); lanes 7, 8 are not read on
         rho = cl ? g + o.a * bcast(g, 7) + o.b * bcast(g, 8) : g;
       };
+      if constexpr (JG && ST_J_AHEAD == 2) {
+        stage_loop2<BwdOps>(N - 1, -1, N, [&](int kk, BwdOps& o) { bwd_load(kk, s.u.q.g, o); }, rstage);
+      } else {
 #pragma unroll 1
-      for (int kk = N - 1; kk >= 0; kk -= 2) {
-        const int k1 = kk >= 1 ? kk - 1 : 0, k2 = kk >= 2 ? kk - 2 : 0;
-        bwd_load(k1, s.u.q.g, B3);
-        rstage(kk, A3);
-        if (kk >= 1) {
-          bwd_load(k2, s.u.q.g, A3);
-          rstage(kk - 1, B3);
+        for (int kk = N - 1; kk >= 0; kk -= 2) {
+          const int k1 = kk >= 1 ? kk - 1 : 0, k2 = kk >= 2 ? kk - 2 : 0;
+          bwd_load(k1, s.u.q.g, B3);
+          rstage(kk, A3);
+          if (kk >= 1) {
+            bwd_load(k2, s.u.q.g, A3);
+            rstage(kk - 1, B3);
+          }
         }
       }
       return wmax(rmax);
@@ -1287,14 +1419,48 @@ bool st_sqp_built(int N) {
   }
 }
 
+size_t st_sqp_jws_doubles(int N) {
+  switch (N) {
+#define VC_CASE(n) \
+  case n:          \
+    return st_j_global_ok<n>() ? (size_t)n * 48 : 0;
+    VC_ST_HORIZONS(VC_CASE)
+#undef VC_CASE
+    default:
+      return 0;
+  }
+}
+
+// J placement per launch (round 5): the LDS-J kernel runs its waves ~10 % faster (no L2 latency in
+// the LQ sweeps), the global-J kernel fits more workgroups per CU (N = 50 / 60: four instead of
+// three).  A batch the LDS-J kernel holds resident at once (wg_per_cu x CUs problems) takes it; a
+// larger one the global-J kernel, which then needs fewer rounds of the machine
+// (scripts/st_jg_ab.sh).
+template <int N>
+bool st_jg_pick(int B) {
+  if constexpr (!st_j_global_ok<N>()) return false;
+  else return B > wg_per_cu(sizeof(StSmem<N, false>)) * device_cus();
+}
+template <int N, int TYRE>
+void st_launch(const StSqpArgs& a, hipStream_t stream) {
+  if constexpr (st_j_global_ok<N>()) {
+    if (st_jg_pick<N>(a.B)) {
+      hipLaunchKernelGGL((st_sqp_kernel<N, TYRE, true>), dim3(a.B), dim3(WTH), 0, stream, a);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((st_sqp_kernel<N, TYRE, false>), dim3(a.B), dim3(WTH), 0, stream, a);
+}
+
 hipError_t launch_st_sqp(const StSqpArgs& a, int N, hipStream_t stream) {
   if (a.B <= 0) return hipSuccess;
+  if (st_sqp_jws_doubles(N) && !a.jws) return hipErrorInvalidValue;  // the workspace the kernel may need
   const bool lin = a.car.tyre == VC_TYRE_LINEAR;
   switch (N) {
-#define VC_CASE(n)                                                                                          \
-  case n:                                                                                                  \
-    if (lin) hipLaunchKernelGGL((st_sqp_kernel<n, VC_TYRE_LINEAR>), dim3(a.B), dim3(WTH), 0, stream, a);  \
-    else hipLaunchKernelGGL((st_sqp_kernel<n, VC_TYRE_FIALA>), dim3(a.B), dim3(WTH), 0, stream, a);       \
+#define VC_CASE(n)                                        \
+  case n:                                                \
+    if (lin) st_launch<n, VC_TYRE_LINEAR>(a, stream);    \
+    else st_launch<n, VC_TYRE_FIALA>(a, stream);         \
     return hipGetLastError();
     VC_ST_HORIZONS(VC_CASE)
 #undef VC_CASE

@@ -39,6 +39,48 @@ __device__ __forceinline__ int xcd_problem(int g, int B) {
   return g < 8 * q ? (g & 7) * q + (g >> 3) : g;
 }
 
+// Compute units of the current device (host side; the occupancy-driven kernel choices).
+inline int device_cus() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 256;
+  return n > 0 ? n : 256;
+}
+// One-wave workgroups of an lds-byte block resident per CU (160 KB of LDS allocated in 512 B
+// granules -- rocprofv3 LDS_Block_Size --, and at most one per SIMD: the solve kernels hold more
+// than 256 VGPRs + AGPRs per lane).
+constexpr int wg_per_cu(size_t lds) {
+  const size_t g = (lds + 511) / 512 * 512, n = 163840 / (g ? g : 1);
+  return n < 4 ? (int)n : 4;
+}
+
+// fp64 array in global memory addressed through a buffer resource: SGPR base + 32-bit VGPR byte
+// offset (one VGPR per access instead of a 64-bit address pair -- the Riccati kernels have no
+// registers to spare), and an offset at or past `bytes` reads 0 / drops the store instead of
+// faulting.  (A pointer read out of the kernel-argument block has no known address space: plain
+// loads through it become flat loads, which count against lgkmcnt too, so every LDS wait after
+// them would also wait for global memory.)
+struct GBuf {
+  __amdgpu_buffer_rsrc_t r;
+  // a base the compiler cannot prove uniform (read through a laundered kernel-argument pointer)
+  // would put the descriptor in VGPRs and wrap every access in a readfirstlane loop: callers
+  // pass it through uniform() first
+  static __device__ __forceinline__ double* uniform(double* p) {
+    const uint64_t u = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u), hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+    return (double*)(((uint64_t)hi << 32) | lo);
+  }
+  __device__ __forceinline__ GBuf(double* base, uint32_t bytes)
+      : r(__builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)bytes, 0x00020000)) {}  // gfx9 raw buffer
+  __device__ __forceinline__ double ld(uint32_t off) const {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+  }
+  __device__ __forceinline__ void st(uint32_t off, double v) const {
+    typedef __attribute__((ext_vector_type(2))) unsigned u2;
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), r, off, 0, 0);
+  }
+};
+
 // 1/x to full fp64 accuracy: hardware v_rcp_f64 + two Newton steps (five VALU ops against
 // the ~11-op div_scale / div_fmas / div_fixup sequence of an IEEE divide).  x = +-inf or 0
 // (an unbounded row's slack, a zero step component) makes the Newton residual NaN; the
@@ -203,6 +245,7 @@ struct StSqpArgs {
   int32_t* status;      // [B]
   int32_t* iters;       // [B]
   double* diag;         // [B][4] optional diagnostics, may be null
+  double* jws;          // [B][st_sqp_jws_doubles(N)] stage Jacobians kept out of LDS (null: none needed)
   int B;
   DynCoef<double> car;
   vc_dyn_mpc w;
@@ -222,6 +265,7 @@ struct CascSqpArgs {
   int32_t* status;      // [B]
   int32_t* iters;       // [B]
   double* diag;         // [B][4] optional diagnostics, may be null
+  double* jws;          // [B][casc_ric_jws_doubles(N, M)] stage Jacobians kept out of LDS (null: none needed)
   double* H_out;        // [B][2H][2H]  (mode 1 only)
   double* g_out;        // [B][2H]      (mode 1 only)
   int mode;             // 0 = full solve, 1 = first QP's H, g only
@@ -283,8 +327,12 @@ hipError_t launch_casc_sqp(const CascSqpArgs& a, int N, int M, hipStream_t strea
 // H_out / g_out are not read), N + M <= 64.
 hipError_t launch_casc_ric(const CascSqpArgs& a, int N, int M, hipStream_t stream);
 bool casc_ric_built(int N, int M);
+// doubles per problem of CascSqpArgs.jws for shape (N, M) (0: the kernel keeps its Jacobians in LDS)
+size_t casc_ric_jws_doubles(int N, int M);
 hipError_t launch_st_sqp(const StSqpArgs& a, int N, hipStream_t stream);
 bool st_sqp_built(int N);
+// doubles per problem of StSqpArgs.jws for horizon N (0: the kernel keeps its Jacobians in LDS)
+size_t st_sqp_jws_doubles(int N);
 bool casc_sqp_built(int N, int M);
 size_t dyn_sqp_smem_bytes(int N);
 int dyn_sqp_debug_stride();

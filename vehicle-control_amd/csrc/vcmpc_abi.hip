@@ -30,6 +30,8 @@ struct vc_ctx {
   size_t sim_bytes = 0;
   void* ls = nullptr;     // kinematic SQP scratch (vc_qp.kin_sqp > 0): u_prev, status / iteration sums
   size_t ls_bytes = 0;
+  void* jw = nullptr;     // single-track / cascaded SQP: stage Jacobians of the kernels that keep them out of LDS
+  size_t jw_bytes = 0;
   int fault_iter = -1, fault_problem = -1;  // vc_debug_qp_fault (tests only)
   std::string err;
 };
@@ -55,6 +57,18 @@ int fail(vc_ctx* c, int code, const char* fmt, ...) {
   } while (0)
 
 size_t esize(const vc_ctx* c) { return c->dtype == VC_F32 ? 4 : 8; }
+
+// Grow-only device scratch owned by the context (freed once the stream has drained).
+int ensure_scratch(vc_ctx* c, void** p, size_t* have, size_t need) {
+  if (need <= *have) return 0;
+  VC_HIP(c, hipStreamSynchronize(c->stream));
+  if (*p) VC_HIP(c, hipFree(*p));
+  *p = nullptr;
+  *have = 0;
+  VC_HIP(c, hipMalloc(p, need));
+  *have = need;
+  return 0;
+}
 int nx_of(const vc_ctx* c) { return c->model == VC_MODEL_KINEMATIC ? 6 : 8; }
 
 int ensure_arena(vc_ctx* c, size_t bytes) {
@@ -224,7 +238,13 @@ int casc_solve(vc_ctx* c, int B, const void* x0, const void* kappa, const void* 
     a.H_out = (double*)H_out;
     a.g_out = (double*)g_out;
   }
-  if (mode == 0 && casc_stagewise(c)) VC_HIP(c, vc::launch_casc_ric(a, c->N, c->p.casc.horizon_pm, c->stream));
+  if (mode == 0 && casc_stagewise(c)) {
+    if (const size_t jd = vc::casc_ric_jws_doubles(c->N, c->p.casc.horizon_pm)) {
+      if (int r = ensure_scratch(c, &c->jw, &c->jw_bytes, (size_t)B * jd * 8)) return r;
+      a.jws = (double*)c->jw;
+    }
+    VC_HIP(c, vc::launch_casc_ric(a, c->N, c->p.casc.horizon_pm, c->stream));
+  }
   else VC_HIP(c, vc::launch_casc_sqp(a, c->N, c->p.casc.horizon_pm, c->stream));
   if (flags == VC_HOST_PTRS) return unstage(c, slots);
   return 0;
@@ -275,6 +295,10 @@ int st_solve(vc_ctx* c, int B, const void* x0, const void* kappa, const void* ds
     a.status = status;
     a.iters = iters;
     a.diag = (double*)diag;
+  }
+  if (const size_t jd = vc::st_sqp_jws_doubles(N)) {
+    if (int r = ensure_scratch(c, &c->jw, &c->jw_bytes, (size_t)B * jd * 8)) return r;
+    a.jws = (double*)c->jw;
   }
   VC_HIP(c, vc::launch_st_sqp(a, N, c->stream));
   if (flags == VC_HOST_PTRS) return unstage(c, slots);
@@ -413,6 +437,7 @@ void vc_destroy(vc_ctx* c) {
   if (c->track) (void)hipFree(c->track);
   if (c->sim) (void)hipFree(c->sim);
   if (c->ls) (void)hipFree(c->ls);
+  if (c->jw) (void)hipFree(c->jw);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
 }
