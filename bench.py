@@ -145,7 +145,10 @@ def pmc_traffic(batch, kernel="kin_ltv_kernel<20>"):
     try:
         with open(PMC_SUMMARY) as f:
             p = json.load(f)
-        return p[f"{kernel} grid={64 * batch}"]["derived"]["traffic_bytes_per_launch"]
+        # FETCH_SIZE counts half the bytes of a read on gfx950 (MI355X guide; calibrated for this
+        # kernel's 8 B-per-lane loads too: scripts/pmc_calibrate.sh, profiles/r05/pmc_calibration_r05y.txt,
+        # FETCH_SIZE = 0.500 and WRITE_SIZE = 1.000 of a known byte count), so reads count twice
+        return p[f"{kernel} grid={64 * batch}"]["derived"]["traffic_bytes_per_launch_fetch_x2"]
     except (OSError, ValueError, KeyError):
         return None
 
@@ -994,7 +997,7 @@ def main():
             "roofline": {"bound": "fp64", "achieved": flops_F * B / (kern_ms / 1e3) / 1e12, "peak": FP64_VALU_PEAK,
                          "unit": "TFLOP/s", "frac": flops_F * B / (kern_ms / 1e3) / 1e12 / FP64_VALU_PEAK,
                          "traffic": pmc_traffic(B),
-                         "traffic_unit": f"HBM bytes/launch (rocprofv3 FETCH_SIZE+WRITE_SIZE, {os.path.relpath(PMC_SUMMARY, ROOT)})",
+                         "traffic_unit": f"HBM bytes/launch (rocprofv3 2 x FETCH_SIZE + WRITE_SIZE: the gfx950 read correction, calibrated for 8 B/lane in profiles/r05/pmc_calibration_r05y.txt; {os.path.relpath(PMC_SUMMARY, ROOT)})",
                          "kernel": "kin_ltv_kernel<20>", "kernel_ms": kern_ms, "flops_per_solve": flops_F,
                          "flops_note": "SURVEY 8(d) F: 0.42 MFLOP sweep + (IPM iterations + polish rounds) x 0.28 MFLOP; a polish round (normal-matrix build + factorisation + solves) is priced as one iteration",
                          "polish_rounds_mean": polish_rounds,
