@@ -11,9 +11,10 @@ The same line carries, under "c3", BASELINE config 3 -- B = 4096 dynamic-bicycle
 (linear tyre) single-track NMPC problems per GPU, N = 40, 3 SQP iterations, solved in fp64
 (vc_solve on a dynamic context, csrc/st_sqp.hip: the kernel that meets the 1e-5 parity bar,
 and the faster one) -- measured the same way; it is a secondary workload, not `value`.
-The fp32 condensed kernel BASELINE config 3 names (csrc/dyn_sqp.hip) is retired from the
-default line: it misses the 1e-5 bar (fp32 QP-data floor) and is slower than the fp64
-kernel; `--c3-f32` still measures it under "c3_f32".  Under "c5": BASELINE config 5 -- the closed-loop
+The fp32 condensed kernel BASELINE config 3 names (csrc/dyn_sqp.hip) is measured beside it under
+"c3_f32" (it misses the 1e-5 bar -- fp32 QP-data floor, DESIGN 2b -- and is slower than the fp64
+kernel; --no-c3-f32 skips it), and "c3_survey" runs the fp64 C3 leg on SURVEY 8(d)'s full sampler
+ranges (Ux down to 5 m/s, ey to +-3 m, Fx warm starts to +-6000 N).  Under "c5": BASELINE config 5 -- the closed-loop
 Monte-Carlo, 8192 vehicles x 500 steps on ippodromo (horizon -> NMPC solve -> fp64
 plant, all on the device, vc_simulate), vehicles sharded over the ranks.  Under
 "cascaded": the reference's cascaded NMPC (20 single-track + 40 point-mass stages,
@@ -55,7 +56,7 @@ FLOP_ITER = (2 * N_DEC * sum(2 * (1 + r % (N_HORIZON - 1)) for r in range(NC_ROW
              + 4 * (2 * NC_ROWS * N_DEC) + 2 * 2 * N_DEC * N_DEC)                       # mat-vecs
 FP64_VALU_PEAK = 78.6  # TFLOP/s
 # newest committed PMC summary first (scripts/pmc_profile.sh -> scripts/pmc_summary.py)
-PMC_SUMMARIES = [os.path.join(ROOT, "profiles", r, "pmc_summary.json") for r in ("r05", "r04")]
+PMC_SUMMARIES = [os.path.join(ROOT, "profiles", r, "pmc_summary.json") for r in ("r06", "r05", "r04")]
 PMC_SUMMARY = next((p for p in PMC_SUMMARIES if os.path.exists(p)), PMC_SUMMARIES[0])
 
 # ---- C3: dynamic single-track SQP (fp32, N = 40) ------------------------------------
@@ -153,6 +154,47 @@ def pmc_traffic(batch, kernel="kin_ltv_kernel<20>"):
         return None
 
 
+def pmc_mfma(batch, kernel="kin_ltv_kernel<20>"):
+    """The matrix-core share of one launch, from the committed PMC pass at this batch
+    (profiles/<round>/pmc_summary.json, scripts/pmc_summary.py):
+      flops_per_launch = SQ_INSTS_VALU_MFMA_MOPS_F64 x 512 (v_mfma_f64_16x16x4_f64 = 2,048 FLOP,
+                         counted as 4 MOPS of 512), equal to SQ_INSTS_MFMA x 2,048 here (the only
+                         MFMA the kernel issues);
+      busy_frac        = SQ_VALU_MFMA_BUSY_CYCLES / (SIMDs x cycles of the launch), SIMDs = 256 CUs x 4,
+                         cycles = GRBM_GUI_ACTIVE / 8 (rocprofv3 sums GRBM over the 8 XCDs; MI355X guide,
+                         DVFS note) -- BUSY_CYCLES counts SIMD cycles, 64 per v_mfma_f64_16x16x4_f64
+                         (463,596 MFMAs, 29.67 M busy cycles at C2, r05);
+      peak             = the dense fp64 matrix rate, 78.6 TFLOP/s (16x16x4 f64 = 2,048 FLOP per 64 cycles
+                         per SIMD x 1,024 SIMDs x 2.4 GHz), the same number as the fp64 vector peak."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            p = json.load(f)
+        e = p[f"{kernel} grid={64 * batch}"]
+    except (OSError, ValueError, KeyError):
+        return None
+    c = e["counters_per_dispatch"]
+    flops = float(c.get("SQ_INSTS_VALU_MFMA_MOPS_F64", 0.0)) * 512.0 + float(c.get("SQ_INSTS_VALU_MFMA_MOPS_F32", 0.0)) * 512.0
+    cyc = float(c["GRBM_GUI_ACTIVE"]) / 8.0
+    busy = float(c["SQ_VALU_MFMA_BUSY_CYCLES"])
+    return {"flops_per_launch": flops, "flops_per_solve": flops / batch, "mfma_insts_per_launch": float(c["SQ_INSTS_MFMA"]),
+            "busy_cycles_per_launch": busy, "launch_cycles": cyc, "simds": 1024,
+            "busy_frac": busy / (1024.0 * cyc), "peak": FP64_VALU_PEAK, "unit": "TFLOP/s",
+            "source": os.path.relpath(PMC_SUMMARY, ROOT),
+            "valu_insts_per_launch": float(c["SQ_INSTS_VALU"])}
+
+
+def _mfma_live(m, kern_ms):
+    """pmc_mfma's counters priced on this run's live kernel time (the rocprof pass's own
+    duration gives busy_frac; achieved / frac use the timed launches)."""
+    if m is None:
+        return None
+    a = m["flops_per_launch"] / (kern_ms / 1e3) / 1e12
+    return dict(m, achieved=a, frac=a / m["peak"],
+                note="matrix-core FLOP per launch from SQ_INSTS_VALU_MFMA_MOPS_F64 x 512 (= SQ_INSTS_MFMA x 2048); "
+                     "busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8) of the PMC pass; "
+                     "achieved / frac on the live kernel_ms")
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -164,7 +206,10 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=1024, help="problems in the CPU-baseline sample")
     ap.add_argument("--c3-batch", type=int, default=4096, help="C3 problems per GPU (config 3: 4096)")
     ap.add_argument("--no-c3", action="store_true", help="skip the secondary C3 measurement")
-    ap.add_argument("--c3-f32", action="store_true", help="also time C3 through the fp32 condensed kernel")
+    ap.add_argument("--no-c3-f32", action="store_true",
+                    help="skip C3 through the fp32 condensed kernel (BASELINE config 3's named dtype)")
+    ap.add_argument("--no-c3-survey", action="store_true",
+                    help="skip C3 on SURVEY 8(d)'s full sampler ranges (Ux ~ U(5, 22), ey ~ U(-3, 3), Fx ~ U(-6000, 6000))")
     ap.add_argument("--c5-vehicles", type=int, default=C5_VEHICLES, help="C5 vehicles in total (config 5: 8192)")
     ap.add_argument("--c5-steps", type=int, default=C5_STEPS, help="C5 closed-loop steps (config 5: 500)")
     ap.add_argument("--no-c5", action="store_true", help="skip the secondary C5 closed-loop measurement")
@@ -315,10 +360,12 @@ def cpu_baseline_c3(data, sample):
                       f"complex-step linearisation + exact QP, numpy fp64, 1 thread) in {dt:.2f} s"}
 
 
-def run_c3(args, dev, stream, rank, dist, steps, f64=False, N=C3_N, cfg_name="dynamic_mpc", qp=None, leg="c3"):
+def run_c3(args, dev, stream, rank, dist, steps, f64=False, N=C3_N, cfg_name="dynamic_mpc", qp=None, leg="c3",
+           ranges="traces"):
     """Secondary measurement: BASELINE config 3 on this rank (weak scaling).  f64=True runs
     the same workload through the fp64 stagewise-Riccati kernel (csrc/st_sqp.hip); with
-    N = 60 / cfg_name = "singletrack_mpc" it is the reference's own single-track horizon."""
+    N = 60 / cfg_name = "singletrack_mpc" it is the reference's own single-track horizon.
+    ranges="survey": SURVEY 8(d)'s C3 sampler ranges as written (vcmpc/workload.py dynamic_batch)."""
     import numpy as np
     import torch
 
@@ -327,7 +374,8 @@ def run_c3(args, dev, stream, rank, dist, steps, f64=False, N=C3_N, cfg_name="dy
     from vcmpc.workload import dynamic_batch
 
     B = args.c3_batch
-    data = dynamic_batch(B, N=N, seed=args.seed + 104729 * rank)
+    draw = {}
+    data = dynamic_batch(B, N=N, seed=args.seed + 104729 * rank, ranges=ranges, stats=draw)
     tdt = torch.float64 if f64 else torch.float32
     t = {k: torch.from_numpy(v).to(dev, tdt) for k, v in data.items()}
     ubar0 = t["ubar"].clone()
@@ -390,7 +438,12 @@ def run_c3(args, dev, stream, rank, dist, steps, f64=False, N=C3_N, cfg_name="dy
                                 "achieved": bpsolve * B / (kern_ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
                                 "unit": "GB/s"}},
            "solver": {"solved_frac": float((st == 0).mean()), "pdip_iters_mean": float(it.mean()),
-                      "pdip_iters_max": int(it.max())}}
+                      "pdip_iters_max": int(it.max()),
+                      "status_counts": {str(int(k)): int(v) for k, v in zip(*np.unique(st, return_counts=True))}}}
+    if ranges == "survey":
+        out["config"]["workload"] += (" -- SURVEY 8(d) sampler ranges: Ux ~ U(5, 22), ey ~ U(-3, 3), Fx warm start "
+                                      "~ U(-6000, 6000) N per stage; warm starts outside the spatial model's domain "
+                                      f"re-drawn ({draw.get('redrawn', 0)} of {draw.get('drawn', 0)} drawn)")
     return out, data
 
 
@@ -786,7 +839,8 @@ def run_latency(args, dev):
 
     legs = {"kinematic_n20": lambda: kin(20), "kinematic_n50": lambda: kin(50),
             "singletrack_n50": lambda: dyn("singletrack_mpc", 50), "singletrack_n60": lambda: dyn("singletrack_mpc", 60),
-            "cascaded_n20_m15": lambda: dyn("cascaded_mpc", 20, 15), "cascaded_n20_m40": lambda: dyn("cascaded_mpc", 20, 40)}
+            "cascaded_n20_m15": lambda: dyn("cascaded_mpc", 20, 15), "cascaded_n20_m35": lambda: dyn("cascaded_mpc", 20, 35),
+            "cascaded_n20_m40": lambda: dyn("cascaded_mpc", 20, 40)}
     out = {}
     for name, make in legs.items():
         try:
@@ -813,7 +867,8 @@ def run_latency(args, dev):
                    "(host numpy in/out, H2D + one solve launch + D2H per command; drive = the device plant "
                    "step), closed loop on ippodromo from s = 1 m; recorded_ipopt_median_ms = the reference's "
                    "recorded CasADi/IPOPT medians (experiments/data, unrecorded CPU) -- historical context, "
-                   "not a same-host comparison")
+                   "not a same-host comparison; cascaded_n20_m40 (cascaded.yaml's shape) has no recorded "
+                   "counterpart among the recorded runs' horizons")
     return out
 
 
@@ -911,7 +966,7 @@ def main():
                 kin_legs[name] = run_kin_leg(args, dev, stream, rank, dist, max(3, args.steps // 4), N, solver, B, leg=name)
             except Exception as e:
                 kin_legs[name] = {"error": f"{type(e).__name__}: {e}"}
-    c3 = c3_data = c3f = st60 = st60c = None
+    c3 = c3_data = c3f = c3s = st60 = st60c = None
     if not args.no_c3:
         # C3 on its parity path: the fp64 stagewise-Riccati kernel meets the 1e-5 bar and is the
         # faster one; the fp32 condensed kernel BASELINE names is reported beside it (c3_f32, a
@@ -926,12 +981,18 @@ def main():
                                 "1e-5 bar -- its QP data, linearised over 40 RK4 stages in fp32, already "
                                 "carries errors that condition numbers of 1e4-1e6 amplify past 1e-5 (DESIGN "
                                 "2b: 1.4e-5 .. 2.5e-3 measured) -- and it is slower (196 K vs 377 K solves/s, "
-                                "r03); measured with --c3-f32 only")
-        if args.c3_f32:
+                                "r03); measured beside it under c3_f32")
+        if not args.no_c3_f32:
             try:
                 c3f, _ = run_c3(args, dev, stream, rank, dist, max(3, args.steps // 4), leg="c3_f32")
             except Exception as e:
                 c3f = {"error": f"{type(e).__name__}: {e}"}
+        if not args.no_c3_survey:
+            try:
+                c3s, _ = run_c3(args, dev, stream, rank, dist, max(3, args.steps // 4), f64=True, leg="c3_survey",
+                                ranges="survey")
+            except Exception as e:
+                c3s = {"error": f"{type(e).__name__}: {e}"}
         try:
             st60, _ = run_c3(args, dev, stream, rank, dist, max(3, args.steps // 4), f64=True, N=60,
                              cfg_name="singletrack_mpc", leg="singletrack_n60_f64")
@@ -989,11 +1050,14 @@ def main():
             "config": {"workload": f"C2 kinematic-bicycle LTV-MPC, B={B} per GPU, N={N_HORIZON}, fp64",
                        "batch_per_gpu": B, "global_batch": B * world, "horizon": N_HORIZON,
                        "parallelism": f"dp{world} (independent shards)"},
-            # the binding roofline is fp64 compute ("not HBM"); almost all of the
-            # kernel's fp64 work issues on the VALU (the v_mfma_f64 normal-matrix build is ~1 %
-            # of it), so the peak is the fp64 vector rate, 78.6 TFLOP/s on MI355X.  `frac` prices
-            # SURVEY 8(d)'s dense count F = 0.42 M + (iterations + 1 polish) x 0.28 M FLOP per
-            # solve; the build's structure-exploiting count is reported beside it
+            # the binding roofline is fp64 compute ("not HBM").  The kernel's fp64 work
+            # splits between the VALU and the matrix cores: the v_mfma_f64_16x16x4_f64 tiles (the
+            # normal-matrix build C'DC and the blocked factorisation's trailing updates) execute
+            # 0.93 MFLOP per solve -- as much as the whole structure-exploiting count (r05 PMC,
+            # `mfma` below; a tile pads its triangle, so part of that is padding).  Both units peak
+            # at 78.6 TFLOP/s in fp64 on MI355X, so that is the peak.  `frac` prices SURVEY 8(d)'s
+            # dense count F = 0.42 M + (iterations + polish rounds) x 0.28 M FLOP per solve; the
+            # structure-exploiting count and the matrix-core share are reported beside it
             "roofline": {"bound": "fp64", "achieved": flops_F * B / (kern_ms / 1e3) / 1e12, "peak": FP64_VALU_PEAK,
                          "unit": "TFLOP/s", "frac": flops_F * B / (kern_ms / 1e3) / 1e12 / FP64_VALU_PEAK,
                          "traffic": pmc_traffic(B),
@@ -1009,6 +1073,7 @@ def main():
                                         "frac": flops * B / (kern_ms / 1e3) / 1e12 / FP64_VALU_PEAK,
                                         "note": "the build's structure-exploiting count (triangular rows, "
                                                 "n^3/3 Cholesky): sweep + (IPM iterations + 1) x iteration"},
+                         "mfma": _mfma_live(pmc_mfma(B), kern_ms),
                          "hbm": {"achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                  "frac": achieved / HBM_PEAK_GBS, "algorithmic_bytes": BYTES_PER_SOLVE * B,
                                  "bytes_per_solve": BYTES_PER_SOLVE}},
@@ -1041,6 +1106,8 @@ def main():
             out["c3"] = c3
         if c3f is not None:
             out["c3_f32"] = c3f
+        if c3s is not None:
+            out["c3_survey"] = c3s
         if st60 is not None:
             out["singletrack_n60_f64"] = st60
         if st60c is not None:

@@ -46,7 +46,7 @@
  *     returns immediately; call vc_synchronize() before reading results.
  *   - Return value: 0 on success, a negative VC_E* code on an API or HIP error
  *     (message via vc_last_error).  Per-problem outcomes are reported in status[b]
- *     (VC_SOLVED, VC_MAX_ITER, VC_NONFINITE); no exception-style failure, unlike the
+ *     (VC_SOLVED, VC_MAX_ITER, VC_NONFINITE, VC_OUT_OF_DOMAIN); no exception-style failure, unlike the
  *     reference simulator's catch-all (simulation/racing.py:416-423).
  *   - Threading: one context per device per host thread; calls on one context
  *     are serialised on its stream.
@@ -60,7 +60,7 @@
 extern "C" {
 #endif
 
-#define VCMPC_ABI_VERSION 11
+#define VCMPC_ABI_VERSION 12
 #define VC_MAX_OBSTACLES 16
 
 typedef struct vc_ctx vc_ctx;
@@ -69,7 +69,11 @@ enum vc_model { VC_MODEL_KINEMATIC = 0, VC_MODEL_DYNAMIC = 1, VC_MODEL_CASCADED 
 enum vc_dtype { VC_F64 = 0, VC_F32 = 1 };
 enum vc_flags { VC_HOST_PTRS = 0, VC_DEVICE_PTRS = 1 };
 enum vc_tyre { VC_TYRE_FIALA = 0, VC_TYRE_LINEAR = 1 };
-enum vc_status { VC_SOLVED = 0, VC_MAX_ITER = 1, VC_NONFINITE = 2 };
+/* VC_OUT_OF_DOMAIN (ABI 12, SQP contexts): the returned x* = rollout(u*) leaves the spatial
+ * model's domain (Ux > 0 and s' = (Ux cos epsi - Uy sin epsi) / (1 - kappa ey) > 0 at every
+ * stage, dynamic_car.py:169-191 divides by s') although every QP converged: the SQP started
+ * from a warm start outside the domain and never got back in.  Not a solution of the NLP. */
+enum vc_status { VC_SOLVED = 0, VC_MAX_ITER = 1, VC_NONFINITE = 2, VC_OUT_OF_DOMAIN = 3 };
 enum vc_error {
   VC_OK = 0,
   VC_E_ARG = -1,      /* bad argument / dimension */
@@ -173,7 +177,9 @@ typedef struct vc_obstacles {
                          1: inside an obstacle beyond the floor band (dist - (r + 0.1) < -margin_min)
                          the QP model takes the reference's own barrier w ds / (dist - r - 0.1),
                          negative there; the floor then acts only in |dist - (r + 0.1)| <= margin_min
-                         (ABI 11; the kinematic merit keeps its C1 extension) */
+                         (ABI 11).  Dynamic / cascaded contexts only: vc_create rejects 1 for
+                         the kinematic model (its merit keeps the C1 extension) and any value
+                         other than 0 and 1 (ABI 12) */
   double margin_min;  /* floor of dist - (r + 0.1) in the barrier's derivatives [m] */
   double s[VC_MAX_OBSTACLES], ey[VC_MAX_OBSTACLES], radius[VC_MAX_OBSTACLES];
 } vc_obstacles;
@@ -242,7 +248,7 @@ int vc_solve(vc_ctx* ctx, int B, const void* x0, const void* kappa, const void* 
  *   [3] polish rounds used.  diag follows the pointer convention of `flags`.
  * Kinematic (kin_ltv) [0] is the true residual of the interior point's last iterate.
  * Single-track / cascaded SQP contexts: [2] = 1 any QP failed, 2 every QP converged,
- * 16 the SQP stopped early (a QP after the first had no solution: its step was refused and
+ * 4 every converged QP's answer certified by the active-set polish, 16 the SQP stopped early (a QP after the first had no solution: its step was refused and
  * the earlier iterate returned, so `status` reflects the QPs before it only); [3] the largest
  * interior-point iteration count of one QP. */
 int vc_solve_diag(vc_ctx* ctx, int B, const void* x0, const void* kappa, const void* ds,

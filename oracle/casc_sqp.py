@@ -320,7 +320,9 @@ def casc_sqp_solve(x0, ubar, kappa, ds, p, W, tyre="fiala", keep_qps=False, **qp
         u = np.where(((alpha > 0) & ~stopped)[:, None, None], u + alpha[:, None, None] * du, u)
     xs, xp = casc_predict(np.asarray(x0, np.float64), u, np.asarray(kappa, np.float64),
                           np.asarray(ds, np.float64), p, W, tyre)
-    return dict(u_star=u, x_star=pack_states(xs, xp), u0=u[:, 0].copy(), hist=hist)
+    # status VC_OUT_OF_DOMAIN where x* leaves the models' domain (csrc/casc_ric.hip, ABI 12)
+    return dict(u_star=u, x_star=pack_states(xs, xp), u0=u[:, 0].copy(), hist=hist,
+                in_domain=casc_in_domain(xs, xp, np.asarray(kappa, np.float64)))
 
 
 def casc_horizon_params(state, state_prediction, mpc_dt, N, Mh, ds_pm, k_of_s):

@@ -26,7 +26,8 @@ here once and implemented identically by ``csrc/dyn_sqp.hip``:
                   outside the domain, and wherever the full step stays inside
   A QP after the first without a solution (infeasible linearisation) refuses its step and ends
   the SQP at the current iterate.
-  output u* = ubar, x* = predict(u*), u0 = u*_0.
+  output u* = ubar, x* = predict(u*), u0 = u*_0; an x* outside the domain is not a solution
+  (status VC_OUT_OF_DOMAIN: the SQP started outside and never got back in).
 
 QP cost = the reference NLP cost in Gauss-Newton form about (xbar, ubar), with every
 ``if_else`` branch frozen at the prediction, plus prox * ||dz||^2:
@@ -318,7 +319,9 @@ def dyn_sqp_solve(x0, ubar, kappa, ds, p, W, tyre="linear", keep_qps=False, **qp
         u = np.where(((alpha > 0) & ~stopped)[:, None, None], u + alpha[:, None, None] * du, u)
     x_star = dyn_predict(np.asarray(x0, np.float64), u, np.asarray(kappa, np.float64),
                          np.asarray(ds, np.float64), p, tyre)
-    return dict(u_star=u, x_star=x_star, u0=u[:, 0].copy(), hist=hist)
+    # status VC_OUT_OF_DOMAIN where x* leaves the model's domain (csrc/st_sqp.hip, ABI 12)
+    return dict(u_star=u, x_star=x_star, u0=u[:, 0].copy(), hist=hist,
+                in_domain=in_domain(x_star, np.asarray(kappa, np.float64)))
 
 
 def dyn_horizon_params(state, state_prediction, mpc_dt, N, k_of_s):

@@ -63,7 +63,8 @@ def replay(run, g, rec, sqp, skip=5, qp=None, dump=None, segments=1, cfg_extra=N
     N = int(cfg["horizon"])
     du, dplan, rel_u, nfail, dbg = [], [], [], 0, None
     us = np.full((T, 2), np.nan)
-    rec_nan = own_nan = 0
+    rec_nan = own_nan = nonfinite = 0
+    st_counts = {}
     for j in range(int(np.max(np.diff(bounds)))):
         idx = np.minimum(bounds[:-1] + j, bounds[1:] - 1)          # a finished window repeats its last row
         live = bounds[:-1] + j < bounds[1:]
@@ -72,6 +73,10 @@ def replay(run, g, rec, sqp, skip=5, qp=None, dump=None, segments=1, cfg_extra=N
             n = int(idx[k])
             us[n] = u[k]
             nfail += int(ctl.status[k] != 0)
+            st_counts[int(ctl.status[k])] = st_counts.get(int(ctl.status[k]), 0) + 1
+            # the controller's output and its next warm start are finite at every step
+            nonfinite += int(not (np.isfinite(u[k]).all() and np.isfinite(ctl.state_prediction[k]).all()
+                                  and np.isfinite(ctl.action_prediction[k]).all()))
             if j < skip:
                 continue
             if n + 1 < len(U):   # racing.py:230-241: action_traj[n + 1] is the command at state_traj[n]
@@ -94,6 +99,7 @@ def replay(run, g, rec, sqp, skip=5, qp=None, dump=None, segments=1, cfg_extra=N
         np.savez(dump, u=us, U=U, X=X, du=du, dplan=dplan, skip=skip, bounds=bounds)
     rel = du / np.maximum(np.abs(np.array(rel_u)), [100.0, 0.01])
     return dict(run=run, sqp=sqp, qp=cfg["qp"], steps=len(du), segments=K, nonsolved=nfail,
+                nonfinite_steps=nonfinite, status_counts={str(k): v for k, v in sorted(st_counts.items())},
                 obstacles=bool(cfg.get("obstacles")), track=track_of(run),
                 dFx_median=float(np.median(du[:, 0])), dFx_p90=float(np.percentile(du[:, 0], 90)),
                 dFx_max=float(du[:, 0].max()), dw_median=float(np.median(du[:, 1])),

@@ -18,7 +18,7 @@ static int fails = 0;
   } while (0)
 
 int main() {
-  CHECK(vc_abi_version() == 11);
+  CHECK(vc_abi_version() == 12);
   CHECK(vc_params_sizeof() == (int)sizeof(vc_params));
   vc_params p;
   std::memset(&p, 0, sizeof(p));
@@ -28,6 +28,11 @@ int main() {
   CHECK(vc_create(0, VC_MODEL_KINEMATIC, 0, 64, VC_F64, &p) == nullptr);
   CHECK(vc_create(0, VC_MODEL_KINEMATIC, 20, 0, VC_F64, &p) == nullptr);
   CHECK(vc_create(0, VC_MODEL_KINEMATIC, 20, 64, VC_F64, nullptr) == nullptr);
+  p.obs.inside = 1;   // the inside-mode barrier is an SQP-model feature (ABI 12)
+  CHECK(vc_create(0, VC_MODEL_KINEMATIC, 20, 64, VC_F64, &p) == nullptr);
+  p.obs.inside = 2;   // a switch: 0 or 1
+  CHECK(vc_create(0, VC_MODEL_DYNAMIC, 40, 64, VC_F64, &p) == nullptr);
+  p.obs.inside = 0;
   vc_destroy(nullptr);
   vc_ctx* c = vc_create(0, VC_MODEL_KINEMATIC, 20, 64, VC_F64, &p);
   if (!c) {

@@ -159,7 +159,8 @@ XFAIL_R4 = {
 }
 
 
-@pytest.mark.parametrize("key", [pytest.param(k, marks=pytest.mark.xfail(reason=XFAIL_R4[k], strict=False))
+@pytest.mark.parametrize("key", [pytest.param(k, marks=pytest.mark.xfail(reason=XFAIL_R4[k], strict=True,
+                                                                                raises=AssertionError))
                                  if k in XFAIL_R4 else k for k in sorted(RUNS_R4)])
 def test_recorded_obstacle_and_shoe_runs_within_bands(key):
     import sys

@@ -144,14 +144,16 @@ def test_casc_ric_batch_properties(M, dyn_params):
 def test_casc_ric_j_placement_bit_identical(M):
     """Round 5: M = 35 / 40 keep the stage Jacobians in LDS while the batch fits the machine at
     three workgroups per CU and in a global workspace beyond (four per CU; csrc/casc_ric.hip
-    cr_launch): the first 64 problems of a 4,096 batch (global J) equal the same 64 solved alone
-    (LDS J) bit for bit."""
+    cr_launch): every problem of a 4,096 batch (global J) equals the same problem solved in LDS-J
+    chunks of 512 bit for bit (the whole batch: ADVICE r05)."""
     from vcmpc.workload import cascaded_batch
-    B = 4096
+    B, CH = 4096, 512
     d = cascaded_batch(B, M=M, seed=56)
     with _ctx(M, B=B) as c:
         big = c.solve(d["x0"], d["kappa"], d["ds"], d["ubar"].copy(), diag=True)
-        small = c.solve(d["x0"][:64], d["kappa"][:64], d["ds"][:64], d["ubar"][:64].copy(), diag=True)
+        parts = [c.solve(d["x0"][i:i + CH], d["kappa"][i:i + CH], d["ds"][i:i + CH], d["ubar"][i:i + CH].copy(),
+                         diag=True) for i in range(0, B, CH)]
+    small = [np.concatenate([p[j] for p in parts]) for j in range(len(big))]
     print(f"M={M}: solved {(big[3] == 0).mean():.4f} of {B}")
     for a, b in zip(big, small):
-        np.testing.assert_array_equal(a[:64], b)
+        np.testing.assert_array_equal(a, b)

@@ -245,16 +245,20 @@ def test_st_sqp_j_placement_bit_identical(N, tyre):
     """Round 5: for N >= 45 the launcher keeps the stage Jacobians in LDS while the batch fits the
     machine at that kernel's occupancy (three workgroups per CU: <= 768 problems on 256 CUs) and
     moves them to a global workspace beyond (four per CU; csrc/st_sqp.hip st_jg_pick).  The
-    placement changes where J lives, not one floating-point operation: the first 64 problems of a
-    4,096 batch (global J) must equal the same 64 solved alone (LDS J) bit for bit."""
+    placement changes where J lives, not one floating-point operation: every problem of a 4,096
+    batch (global J) must equal the same problem solved in LDS-J chunks of 512 bit for bit (ADVICE
+    r05: the whole batch, so an addressing error in the per-problem workspace at any problem
+    index -- the bounds-checked loads would return zeros, not fault -- shows as a mismatch)."""
     from vcmpc.config import load_config
     from vcmpc.workload import dynamic_batch
-    B = 4096
+    B, CH = 4096, 512   # CH <= 768: LDS J at three workgroups per CU on 256 CUs
     d = {k: v.astype(np.float64) for k, v in dynamic_batch(B, N=N, seed=55, tyre=tyre).items()}
     cfg = load_config("singletrack_mpc")
     with _ctx(N, cfg, tyre, max_batch=B) as ctx:
         big = ctx.solve(d["x0"], d["kappa"], d["ds"], d["ubar"].copy(), diag=True)
-        small = ctx.solve(d["x0"][:64], d["kappa"][:64], d["ds"][:64], d["ubar"][:64].copy(), diag=True)
+        parts = [ctx.solve(d["x0"][i:i + CH], d["kappa"][i:i + CH], d["ds"][i:i + CH], d["ubar"][i:i + CH].copy(),
+                           diag=True) for i in range(0, B, CH)]
+    small = [np.concatenate([p[j] for p in parts]) for j in range(len(big))]
     print(f"N={N} {tyre}: solved {(big[3] == 0).mean():.4f} of {B}")
     for a, b in zip(big, small):
-        np.testing.assert_array_equal(a[:64], b)
+        np.testing.assert_array_equal(a, b)

@@ -88,17 +88,8 @@ struct CrJ {  // [A6 | B6 diag(S, 1 or S)] of one transition + 1 pad (49 doubles
 // 48.7 / 53.1 KB, three per CU) it lives in a per-problem global workspace (CascSqpArgs.jws, 384 B
 // per stage; written once per SQP iteration, read by the Riccati passes one stage ahead of use):
 // 29.6 / 31.7 KB, four per CU -- the ceiling, the kernel holds ~480 VGPRs + AGPRs (one wave per SIMD)
-#ifndef CR_J_AHEAD
-#define CR_J_AHEAD 1  // global J: stages of lookahead in the LQ / dual sweeps (2: three operand buffers)
-#endif
-#ifndef CR_FWD_MASKED
-#define CR_FWD_MASKED 0  // global J: forward-sweep operands by exec-masked loads (0: load both, select)
-#endif
-#ifndef CR_J_GLOBAL
-#define CR_J_GLOBAL 1  // 1: where needed (N + M >= 55), 2: every shape, 0: none
-#endif
 template <int N, int M>
-constexpr bool cr_j_global_ok() { return CR_J_GLOBAL == 2 || (CR_J_GLOBAL == 1 && N + M >= 55); }  // (cr_jg_pick)
+constexpr bool cr_j_global_ok() { return N + M >= 55; }  // (cr_jg_pick)
 template <bool JG>
 using CrJP = std::conditional_t<JG, double*, CrJ*>;  // workspace base (GBuf) or LDS
 struct CrNone {};  // (global: 48 doubles = 384 B per stage, [6][8] row-major)
@@ -149,29 +140,13 @@ struct CrSmem {
   int flag[4];
 };
 
-#ifndef CR_RES_RECUR
-#define CR_RES_RECUR 1  // dual residual carried by the steps (0: adjoint sweep every iteration)
-#endif
 
-#ifndef CR_POLISH
-#define CR_POLISH 3  // active-set polish rounds after each converged QP (0: off, the round-4 kernel)
-#endif
-#ifndef CR_AL_RHO
-#define CR_AL_RHO 1e2  // polish: augmented-Lagrangian weight of an active row, x (1 + max diag Q) / |c|^2
-#endif
-#ifndef CR_AL_PASSES
-#define CR_AL_PASSES 16
-#endif
-#ifndef CR_CERT_PTOL
-#define CR_CERT_PTOL 1e-11  // polish certificate: inactive-row violation, x (1 + max |q|)
-#endif
-#ifndef CR_CERT_DTOL
-#define CR_CERT_DTOL 1e-12  // polish certificate: wrong-signed multiplier, x (1 + max |q|)
-#endif
+constexpr int kCrPolish = 3;  // active-set polish rounds after each converged QP (0: off, the round-4 kernel)
+constexpr double kCrAlRho = 1e2;  // polish: augmented-Lagrangian weight of an active row, x (1 + max diag Q) / |c|^2
+constexpr int kCrAlPasses = 16;
+constexpr double kCrCertPtol = 1e-11;  // polish certificate: inactive-row violation, x (1 + max |q|)
+constexpr double kCrCertDtol = 1e-12;  // polish certificate: wrong-signed multiplier, x (1 + max |q|)
 
-#ifndef CR_KEEP_ITERATE
-#define CR_KEEP_ITERATE 1  // a later QP without a solution keeps the iterate (0: applies it, step non-solved)
-#endif
 
 #define WSYNC()                          \
   do {                                   \
@@ -261,33 +236,6 @@ __device__ __forceinline__ void qmul(const double* Q, const double* v, double* o
   o[6] = Q[Q66] * v[6] + Q[Q67] * v[7];
   o[7] = Q[Q07] * v[0] + Q[Q17] * v[1] + Q[Q27] * v[2] + Q[Q37] * v[3] + Q[Q67] * v[6] + Q[Q77] * v[7];
   o[8] = Q[Q88] * v[8] + Q[Q38] * v[3];
-}
-
-// Stage loop over k = first, first + step, ... (n stages) with each stage's operands loaded two
-// stages ahead of use (three rotating operand buffers, unrolled by three: no register rotation at
-// the latch).  For the sweeps whose operands come from global memory (JG): a stage of the
-// LQ sweeps is ~100-200 cycles, shorter than an L2 hit under load, so the one-stage lookahead of
-// the LDS sweeps would leave most of the latency exposed.
-template <typename Ops, typename Load, typename Stage>
-__device__ __forceinline__ void stage_loop2(int first, int step, int n, Load&& load, Stage&& stage) {
-  const int hi = n - 1;
-  auto at = [&](int i) { const int k = first + step * (i < hi ? i : hi); return k; };
-  Ops A, B, C;
-  load(at(0), A);
-  load(at(1), B);
-#pragma unroll 1
-  for (int i = 0; i < n; i += 3) {
-    load(at(i + 2), C);
-    stage(at(i), A);
-    if (i + 1 < n) {  // uniform
-      load(at(i + 3), A);
-      stage(at(i + 1), B);
-      if (i + 2 < n) {
-        load(at(i + 4), B);
-        stage(at(i + 2), C);
-      }
-    }
-  }
 }
 
 // stage-Jacobian element (k, r, c): the LDS array, or the global workspace through a buffer
@@ -907,18 +855,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       double w[8];
     };
     auto fwd_load = [&](int kk, FwdOps& o) {
-      if constexpr (JG && CR_FWD_MASKED) {
-        // no pointer select across address spaces (it would go flat), and no value select
-        // (it would wait for both loads at the load site): exec-masked loads into one buffer
-        if (fk) {
-#pragma unroll
-          for (int e = 0; e < 7; ++e) o.w[e] = s.u.q.K[kk][fc][e];
-          o.w[7] = s.u.q.kk[kk][fc];
-        } else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) o.w[e] = JLD(kk, fr, e);
-        }
-      } else if constexpr (JG) {  // (no pointer select across address spaces: it would go flat)
+      if constexpr (JG) {  // (no pointer select across address spaces: it would go flat)
 #pragma unroll
         for (int e = 0; e < 7; ++e) {
           const double kv = s.u.q.K[kk][fc][e], jv = JLD(kk, fr, e);
@@ -949,7 +886,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     };
     auto lq_solve = [&]() {
       BwdOps A1, B1;
-      if constexpr (!(JG && CR_J_AHEAD == 2)) bwd_load(H - 1, s.u.q.g, A1);
+      bwd_load(H - 1, s.u.q.g, A1);
       double pv = 0.0;
       auto bstage = [&](int kk, const BwdOps& o) {
         const double g = bwd_g(kk, o, pv);
@@ -958,36 +895,28 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
         pv = g + t2;
         if (fk) s.u.q.kk[kk][l - 7] = -t2;
       };
-      if constexpr (JG && CR_J_AHEAD == 2) {
-        stage_loop2<BwdOps>(H - 1, -1, H, [&](int kk, BwdOps& o) { bwd_load(kk, s.u.q.g, o); }, bstage);
-      } else {
 #pragma unroll 1
-        for (int kk = H - 1; kk >= 0; kk -= 2) {
-          const int k1 = kk >= 1 ? kk - 1 : 0, k2 = kk >= 2 ? kk - 2 : 0;
-          bwd_load(k1, s.u.q.g, B1);
-          bstage(kk, A1);
-          if (kk >= 1) {
-            bwd_load(k2, s.u.q.g, A1);
-            bstage(kk - 1, B1);
-          }
+      for (int kk = H - 1; kk >= 0; kk -= 2) {
+        const int k1 = kk >= 1 ? kk - 1 : 0, k2 = kk >= 2 ? kk - 2 : 0;
+        bwd_load(k1, s.u.q.g, B1);
+        bstage(kk, A1);
+        if (kk >= 1) {
+          bwd_load(k2, s.u.q.g, A1);
+          bstage(kk - 1, B1);
         }
       }
       WSYNC();
       double X = 0.0;
-      if constexpr (JG && CR_J_AHEAD == 2) {
-        stage_loop2<FwdOps>(0, 1, H, fwd_load, [&](int kk, const FwdOps& o) { X = fwd_stage(kk, o, X); });
-      } else {
-        FwdOps A2, B2;
-        fwd_load(0, A2);
+      FwdOps A2, B2;
+      fwd_load(0, A2);
 #pragma unroll 1
-        for (int kk = 0; kk < H; kk += 2) {
-          const int k1 = kk + 1 < H ? kk + 1 : kk, k2 = kk + 2 < H ? kk + 2 : kk;
-          fwd_load(k1, B2);
-          X = fwd_stage(kk, A2, X);
-          if (kk + 1 < H) {
-            fwd_load(k2, A2);
-            X = fwd_stage(kk + 1, B2, X);
-          }
+      for (int kk = 0; kk < H; kk += 2) {
+        const int k1 = kk + 1 < H ? kk + 1 : kk, k2 = kk + 2 < H ? kk + 2 : kk;
+        fwd_load(k1, B2);
+        X = fwd_stage(kk, A2, X);
+        if (kk + 1 < H) {
+          fwd_load(k2, A2);
+          X = fwd_stage(kk + 1, B2, X);
         }
       }
       WSYNC();
@@ -997,25 +926,21 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     // rounding through the RK4 step's unstable lateral mode at low speed)
     auto dual_residual = [&](bool cl) -> double {
       BwdOps A3, B3;
-      if constexpr (!(JG && CR_J_AHEAD == 2)) bwd_load(H - 1, s.u.q.g, A3);
+      bwd_load(H - 1, s.u.q.g, A3);
       double rho = 0.0, rmax = 0.0;
       auto rstage = [&](int kk, const BwdOps& o) {
         const double g = bwd_g(kk, o, rho);
         rmax = fk ? fmax(rmax, fabs(g)) : rmax;
         rho = cl ? g + o.a * bcast(g, 7) + o.b * bcast(g, 8) : g;  // lanes 0..6: + K' g_u
       };
-      if constexpr (JG && CR_J_AHEAD == 2) {
-        stage_loop2<BwdOps>(H - 1, -1, H, [&](int kk, BwdOps& o) { bwd_load(kk, s.u.q.g, o); }, rstage);
-      } else {
 #pragma unroll 1
-        for (int kk = H - 1; kk >= 0; kk -= 2) {
-          const int k1 = kk >= 1 ? kk - 1 : 0, k2 = kk >= 2 ? kk - 2 : 0;
-          bwd_load(k1, s.u.q.g, B3);
-          rstage(kk, A3);
-          if (kk >= 1) {
-            bwd_load(k2, s.u.q.g, A3);
-            rstage(kk - 1, B3);
-          }
+      for (int kk = H - 1; kk >= 0; kk -= 2) {
+        const int k1 = kk >= 1 ? kk - 1 : 0, k2 = kk >= 2 ? kk - 2 : 0;
+        bwd_load(k1, s.u.q.g, B3);
+        rstage(kk, A3);
+        if (kk >= 1) {
+          bwd_load(k2, s.u.q.g, A3);
+          rstage(kk - 1, B3);
         }
       }
       return wmax(rmax);
@@ -1045,7 +970,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     // ---------------- interior point (Mehrotra predictor-corrector) ----------------
     int it = 0;
     bool conv = false, fail = false;
-    // dual residual carried by the steps (CR_RES_RECUR): the LQ direction solves the linearised
+    // dual residual carried by the steps: the LQ direction solves the linearised
     // stationarity exactly, so a step of length alpha scales the condensed gradient by
     // (1 - alpha); the adjoint sweep runs at the first iteration and wherever the carried value
     // would end the loop (convergence, or acceptance at a factorisation failure)
@@ -1084,13 +1009,13 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       WSYNC();
       rpm = wmax(rpm);
       const double mu = wsum(mus) / mcount;
-      const bool carried = CR_RES_RECUR && have_rd;
+      const bool carried = have_rd;
       double rdm = carried ? rd_carry : dual_residual(kvalid);
       bool rd_cl = carried || kvalid;
       last_res = fmax(rdm, rpm);
       last_mu = mu;
       if (!(last_res == last_res) || !(mu == mu) || last_res > 1e300) { fail = true; break; }
-      if (CR_RES_RECUR && have_rd && mu <= 1e2 * tol_mu && fmax(rdm, rpm) <= 1e3 * rtol) {
+      if (have_rd && mu <= 1e2 * tol_mu && fmax(rdm, rpm) <= 1e3 * rtol) {
         // the carried value would end the loop here or below: take the sweep's
         rdm = dual_residual(kvalid);
         rd_cl = kvalid;
@@ -1189,7 +1114,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     // is refined away) with multiplier updates, then certified (inactive rows feasible, active
     // multipliers nonnegative); otherwise the violated rows join and the negative ones leave.
     bool pol_qp = false;
-    if (CR_POLISH > 0 && conv) {
+    if (kCrPolish > 0 && conv) {
       double hs = 0.0, qs = 0.0;
       if (stl) {
         hs = fmax(fmax(fmax(Qc[Q00], Qc[Q11]), fmax(Qc[Q22], Qc[Q33])),
@@ -1200,7 +1125,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
       hs = 1.0 + wmax(hs);
       qs = 1.0 + wmax(qs);
       // row i's weight (recomputed where used: an array of 12 would stay live across the polish)
-      const double rho_h = CR_AL_RHO * hs;
+      const double rho_h = kCrAlRho * hs;
       auto rho = [&](int i) -> double {
         double cn2 = 1.0;
         if (i >= 3 && i < 8) {
@@ -1214,7 +1139,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
 #pragma unroll
       for (int i = 0; i < NR; ++i) act |= (stl && R.m(i) > 0.0 && la[i] > sl[i]) ? (1u << i) : 0u;
 #pragma unroll 1
-      for (int round = 0; round < CR_POLISH; ++round) {
+      for (int round = 0; round < kCrPolish; ++round) {
         // the interior point's slacks / multipliers are dead from here: sl holds the polish's
         // iterate and la its multipliers (a later round starts from the last round's)
         double w[NR], val[NR] = {};
@@ -1234,7 +1159,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
         bool al_conv = false;
         int held = 0;
 #pragma unroll 1
-        for (int p = 0; p < CR_AL_PASSES; ++p) {
+        for (int p = 0; p < kCrAlPasses; ++p) {
           if (stl) {
             double g9[9], y[NR];
             row_values(R, vp, val);
@@ -1278,8 +1203,8 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
           const bool ai = (act >> i) & 1u;
-          viol |= (stl && R.m(i) > 0.0 && !ai && val[i] - R.d[i] > CR_CERT_PTOL * qs) ? (1u << i) : 0u;
-          neg |= (ai && lm[i] < -CR_CERT_DTOL * qs) ? (1u << i) : 0u;
+          viol |= (stl && R.m(i) > 0.0 && !ai && val[i] - R.d[i] > kCrCertPtol * qs) ? (1u << i) : 0u;
+          neg |= (ai && lm[i] < -kCrCertDtol * qs) ? (1u << i) : 0u;
         }
         if (al_conv && __all((viol | neg) ? 0 : 1) != 0) {
           if (stl) {
@@ -1300,7 +1225,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
     // (kin_merit.hip) and oracle/dyn_sqp.py alike.  (Applying the unconverged iterate and
     // reporting the whole step non-solved threw away a plan from converged QPs: the
     // single-track N = 60 obstacle run on the shoe track lost the car, scripts/band_trace.py.)
-    if (CR_KEEP_ITERATE && sq > 0 && !conv) {
+    if (sq > 0 && !conv) {
       stopped = true;
       break;
     }
@@ -1341,6 +1266,7 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
   if (l == 0) {
     int32_t st;
     if (!finite || s.flag[0] == VC_NONFINITE) st = VC_NONFINITE;
+    else if (s.flag[2] == 0) st = VC_OUT_OF_DOMAIN;  // x* (the last rollout) outside the models' domain
     else if (all_conv) st = VC_SOLVED;
     else st = VC_MAX_ITER;
     A.status[b] = st;
@@ -1370,20 +1296,28 @@ bool casc_ric_built(int N, int M) {
   return false;
 }
 
-size_t casc_ric_jws_doubles(int N, int M) {
+// J placement per launch (st_sqp.hip st_jg_pick): the LDS-J kernel while the batch fits the machine
+// at its occupancy, the four-per-CU global-J kernel beyond
+template <int N, int M>
+bool cr_jg_pick(int B) {
+  if constexpr (!cr_j_global_ok<N, M>()) return false;
+  else return B > wg_per_cu(sizeof(CrSmem<N, M, false>)) * device_cus();
+}
+
+// doubles of J workspace per problem a launch of B problems needs (nonzero only where cr_jg_pick
+// takes the global-J kernel)
+size_t casc_ric_jws_doubles(int N, int M, int B) {
 #define VC_CASE(n, m) \
-  if (N == n && M == m) return cr_j_global_ok<n, m>() ? (size_t)(n + m) * 48 : 0;
+  if (N == n && M == m) return cr_jg_pick<n, m>(B) ? (size_t)(n + m) * 48 : 0;
   VC_CR_SHAPES(VC_CASE)
 #undef VC_CASE
   return 0;
 }
 
-// J placement per launch (st_sqp.hip st_jg_pick): the LDS-J kernel while the batch fits the machine
-// at its occupancy, the four-per-CU global-J kernel beyond
 template <int N, int M, int TYRE>
 void cr_launch(const CascSqpArgs& a, hipStream_t stream) {
   if constexpr (cr_j_global_ok<N, M>()) {
-    if (a.B > wg_per_cu(sizeof(CrSmem<N, M, false>)) * device_cus()) {
+    if (cr_jg_pick<N, M>(a.B)) {
       hipLaunchKernelGGL((casc_ric_kernel<N, M, TYRE, true>), dim3(a.B), dim3(WTH), 0, stream, a);
       return;
     }
@@ -1393,7 +1327,7 @@ void cr_launch(const CascSqpArgs& a, hipStream_t stream) {
 
 hipError_t launch_casc_ric(const CascSqpArgs& a, int N, int M, hipStream_t stream) {
   if (a.B <= 0) return hipSuccess;
-  if (casc_ric_jws_doubles(N, M) && !a.jws) return hipErrorInvalidValue;  // the workspace the kernel may need
+  if (casc_ric_jws_doubles(N, M, a.B) && !a.jws) return hipErrorInvalidValue;  // the workspace the kernel needs
   const bool lin = a.car.tyre == VC_TYRE_LINEAR;
 #define VC_CASE(n, m)                                \
   if (N == n && M == m) {                           \

@@ -1268,7 +1268,8 @@ __global__ __launch_bounds__(CTH, 1) void casc_sqp_kernel(CascSqpArgs A) {
   if (t == 0) {
     A.u0[(size_t)b * 2] = s.ub[0][0];
     A.u0[(size_t)b * 2 + 1] = s.ub[0][1];
-    A.status[b] = s.flag[0];
+    // x* (the last rollout) outside the models' domain: not a solution (VC_OUT_OF_DOMAIN)
+    A.status[b] = (s.flag[0] == VC_NONFINITE || s.dom != 0) ? s.flag[0] : VC_OUT_OF_DOMAIN;
     A.iters[b] = s.flag[1];
     if (A.diag) {
 #ifdef VC_TIMING

@@ -1246,6 +1246,7 @@ __global__ __launch_bounds__(NTH, 1) void dyn_sqp_kernel(DynSqpArgs A) {
   if (t == 0) {
     int32_t st;
     if (!all_finite) st = VC_NONFINITE;
+    else if (s.flag[2] == 0) st = VC_OUT_OF_DOMAIN;  // x* (the last rollout) outside the model's domain
     else if (all_conv) st = VC_SOLVED;
     else st = VC_MAX_ITER;
     A.status[b] = st;

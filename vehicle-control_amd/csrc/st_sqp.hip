@@ -87,22 +87,13 @@ struct StJT {
 template <int N>
 using StJ = StJT<(N == 30 || N == 60) ? 8 : 9>;
 // Round 5: [A6 | B6] in LDS costs 49 doubles per stage (23.5 KB at N = 60) and kept st_sqp<60> at three
-// workgroups per CU.  Where ST_J_GLOBAL is set it lives in a per-problem global workspace instead
+// workgroups per CU.  From N = 45 on it lives in a per-problem global workspace instead
 // (StSqpArgs.jws, 384 B = three 128 B lines per stage; written once per SQP iteration by the
 // linearisation, read by the Riccati passes one stage ahead of use, so the L2 latency overlaps the
 // current stage's chain).
-#ifndef ST_J_AHEAD
-#define ST_J_AHEAD 1  // global J: stages of lookahead in the LQ / dual sweeps (2: three operand buffers)
-#endif
-#ifndef ST_FWD_MASKED
-#define ST_FWD_MASKED 0  // global J: forward-sweep operands by exec-masked loads (0: load both, select)
-#endif
-#ifndef ST_J_GLOBAL
-#define ST_J_GLOBAL 1  // 1: where the LDS copy would cost a workgroup per CU (N >= 50), 2: every N, 0: none
-#endif
 // whether the global-J instantiation exists for horizon N (the launcher picks it per batch: st_jg_pick)
 template <int N>
-constexpr bool st_j_global_ok() { return ST_J_GLOBAL == 2 || (ST_J_GLOBAL == 1 && N >= 45); }
+constexpr bool st_j_global_ok() { return N >= 45; }
 template <int N, bool JG>
 using StJP = std::conditional_t<JG, double*, StJ<N>*>;  // workspace base (GBuf) or LDS
 struct StNone {};  // (global: 48 doubles = 384 B per stage, [6][8] row-major)
@@ -147,55 +138,24 @@ struct StSmem {
     } l;
   } u;
   int flag[4];
-#ifdef ST_LDS_PAD
-  double lds_pad[ST_LDS_PAD / 8];  // occupancy experiments only (scripts/st_jg_ab.sh)
-#endif
 };
 
 // Workgroup = one wavefront: LDS operations of a wave execute in order, so a sync only has to
 // stop the compiler from moving memory operations across it (no s_barrier, and no wait for
 // outstanding loads other than the ones actually used).
-#ifndef ST_NEWTON_ROLLOUT
-#define ST_NEWTON_ROLLOUT 1  // after a QP step: chord-Newton rollout from the pre-step trajectory (0: serial)
-#endif
-#ifndef ST_NEWTON_FROM_SQ
-#define ST_NEWTON_FROM_SQ 1  // from the second QP step on (the first, from the warm start, is the largest)
-#endif
-#ifndef ST_NEWTON_TOL
-#define ST_NEWTON_TOL 1e-14  // accepted defect, relative to 1 + |y|
-#endif
-#ifndef ST_NEWTON_MAX
-#define ST_NEWTON_MAX 12
-#endif
-#ifndef ST_NEWTON_UX_MIN
+constexpr double kStNewtonTol = 1e-14;  // accepted defect, relative to 1 + |y|
+constexpr int kStNewtonMax = 12;
 // below ~6 m/s the reference's RK4 step (mpc_dt 0.03 s) is expansive in the lateral mode (|eig A_k| 3-5
 // at 4 m/s), so a stage defect the chord iteration accepts at 1e-14 grows through the stages
 // and x* drifts from rollout(u*): there the serial rollout runs
-#define ST_NEWTON_UX_MIN 8.0
-#endif
-#ifndef ST_RES_RECUR
-#define ST_RES_RECUR 1  // dual residual carried by the steps (0: adjoint sweep every iteration)
-#endif
+constexpr double kStNewtonUxMin = 8.0;
 
-#ifndef ST_POLISH
-#define ST_POLISH 3  // active-set polish rounds after each converged QP (0: off, the round-4 kernel)
-#endif
-#ifndef ST_AL_RHO
-#define ST_AL_RHO 1e2  // polish: augmented-Lagrangian weight of an active row, x (1 + max diag Q) / |c|^2
-#endif
-#ifndef ST_AL_PASSES
-#define ST_AL_PASSES 16
-#endif
-#ifndef ST_CERT_PTOL
-#define ST_CERT_PTOL 1e-11  // polish certificate: inactive-row violation, x (1 + max |q|)
-#endif
-#ifndef ST_CERT_DTOL
-#define ST_CERT_DTOL 1e-12  // polish certificate: wrong-signed multiplier, x (1 + max |q|)
-#endif
+constexpr int kStPolish = 3;  // active-set polish rounds after each converged QP (0: off, the round-4 kernel)
+constexpr double kStAlRho = 1e2;  // polish: augmented-Lagrangian weight of an active row, x (1 + max diag Q) / |c|^2
+constexpr int kStAlPasses = 16;
+constexpr double kStCertPtol = 1e-11;  // polish certificate: inactive-row violation, x (1 + max |q|)
+constexpr double kStCertDtol = 1e-12;  // polish certificate: wrong-signed multiplier, x (1 + max |q|)
 
-#ifndef ST_KEEP_ITERATE
-#define ST_KEEP_ITERATE 1  // a later QP without a solution keeps the iterate (0: applies it, step non-solved)
-#endif
 
 #define WSYNC()                          \
   do {                                   \
@@ -295,33 +255,6 @@ __device__ __forceinline__ void qmul(const double* Q, const double* v, double* o
   o[8] = Q[Q88] * v[8];
 }
 
-// Stage loop over k = first, first + step, ... (n stages) with each stage's operands loaded two
-// stages ahead of use (three rotating operand buffers, unrolled by three: no register rotation at
-// the latch).  For the sweeps whose operands come from global memory (JG): a stage of the
-// LQ sweeps is ~100-200 cycles, shorter than an L2 hit under load, so the one-stage lookahead of
-// the LDS sweeps would leave most of the latency exposed.
-template <typename Ops, typename Load, typename Stage>
-__device__ __forceinline__ void stage_loop2(int first, int step, int n, Load&& load, Stage&& stage) {
-  const int hi = n - 1;
-  auto at = [&](int i) { const int k = first + step * (i < hi ? i : hi); return k; };
-  Ops A, B, C;
-  load(at(0), A);
-  load(at(1), B);
-#pragma unroll 1
-  for (int i = 0; i < n; i += 3) {
-    load(at(i + 2), C);
-    stage(at(i), A);
-    if (i + 1 < n) {  // uniform
-      load(at(i + 3), A);
-      stage(at(i + 1), B);
-      if (i + 2 < n) {
-        load(at(i + 4), B);
-        stage(at(i + 2), C);
-      }
-    }
-  }
-}
-
 // stage-Jacobian element (k, r, c): the LDS array, or the global workspace through a buffer
 // resource (GBuf: one offset VGPR per access, bounds-checked to the problem's N stages)
 template <int N, bool JG>
@@ -349,10 +282,8 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
   // occupancy guard (rocprofv3 LDS_Block_Size: 53,248 B ran three one-wave workgroups per CU,
   // 54,272 B two; four need <= 40,960 B)
   // (the kernel holds ~450 VGPRs + AGPRs: one wave per SIMD, so four workgroups per CU is the ceiling)
-#ifndef ST_LDS_PAD
   static_assert(!JG || sizeof(StSmem<N, JG>) <= 40960, "global-J st_sqp must fit four workgroups per CU");
   static_assert(JG || N != 60 || sizeof(StSmem<N, JG>) <= 53248, "LDS-J st_sqp<60> must fit three workgroups per CU");
-#endif
   __shared__ StSmem<N, JG> s;
   const int l = threadIdx.x;
   const int b = xcd_problem(blockIdx.x, A.B);
@@ -424,14 +355,14 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     const StJP<N, JG> J = st_jac<N, JG>(s, A, b);
     // ---------------- predict: xs = rollout(ubar) ----------------
     // Serial: lane 0 walks the stages (RK4, algebraic tan-alpha form).  After a QP step
-    // (tries == 1, ST_NEWTON_ROLLOUT, linear tyre) the new rollout is found instead by chord-Newton
+    // (tries == 1, from the second QP step, linear tyre) the new rollout is found instead by chord-Newton
     // sweeps from the pre-step trajectory, whose Jacobians A_k are still in s.J: every lane
     // evaluates its own stage, F(x_k, u_k) -> defect c_k = F_y - y_{k+1} (6 lateral/longitudinal
     // states; s and t do not enter F and are prefix sums of their increments), then lanes 0..5
     // sweep delta_{k+1} = c_k + A_k delta_k, y_{k+1} += delta_{k+1}.  Accepted when every defect is
-    // below ST_NEWTON_TOL (1 + |y|): the serial rollout's trajectory up to those defects carried
+    // below kStNewtonTol (1 + |y|): the serial rollout's trajectory up to those defects carried
     // through the dynamics (measured <= 3e-10 relative at 1e-13, tests/test_gpu_st_sqp.py), at the
-    // cost of one RK4 step per sweep instead of N - 1; otherwise (not converged in ST_NEWTON_MAX sweeps,
+    // cost of one RK4 step per sweep instead of N - 1; otherwise (not converged in kStNewtonMax sweeps,
     // non-finite) the serial rollout runs.  The chord iteration converges linearly at a rate set by
     // the step's size (scripts/newton_rollout_study.py: 3-10 sweeps for the linear tyre's SQP
     // steps; the Fiala tyre's saturation often needs more, so it keeps the serial rollout).
@@ -439,10 +370,10 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     // flag[1]: finite, flag[2]: inside the spatial model's domain (Ux > 0, s' > 0)
     ST_STAMP(t_p0)
     {
-      bool newton = ST_NEWTON_ROLLOUT && TYRE == VC_TYRE_LINEAR && tries == 1 && sq >= ST_NEWTON_FROM_SQ;
+      bool newton = TYRE == VC_TYRE_LINEAR && tries == 1 && sq >= 1;  // from the second QP step on
       if (newton) {  // uniform: only where the RK4 step's lateral mode is stable along the pre-step plan
         const double ux = stl ? s.xs.at(k, 0) : 1e300;
-        newton = wmin(ux) >= ST_NEWTON_UX_MIN;
+        newton = wmin(ux) >= kStNewtonUxMin;
       }
       double* scr = &s.u.l.trow[0][0];  // defects / increments [N-1][8]: dead between the IPM and the linearisation
       for (int nit = 0;; ++nit) {
@@ -498,7 +429,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
         WSYNC();
         const bool allfin = __all(fin ? 1 : 0) != 0;
         err = wmax(err);
-        if (allfin && err <= ST_NEWTON_TOL) {
+        if (allfin && err <= kStNewtonTol) {
           // converged: s and t as prefix sums of the stage increments, domain test in parallel
           if (l == 0) {
             double sv = s.xs.at(0, 4), tv = s.xs.at(0, 7);
@@ -527,7 +458,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
           }
           break;
         }
-        if (!allfin || nit + 1 >= ST_NEWTON_MAX) {
+        if (!allfin || nit + 1 >= kStNewtonMax) {
           newton = false;  // the serial rollout (from state 0, which the sweeps never change)
           continue;
         }
@@ -536,7 +467,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
           constexpr int yr[6] = {0, 1, 2, 3, 5, 6};
           const int r = l < 6 ? l : 0;
           // rows kk + 1 (LDS) or kk + 1, kk + 2 (global J) loaded ahead of use
-          constexpr int AH = JG ? ST_J_AHEAD : 1;
+          constexpr int AH = 1;
           double d = 0.0, jn[AH][6];
 #pragma unroll
           for (int a = 0; a < AH; ++a)
@@ -911,18 +842,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       double w[8];
     };
     auto fwd_load = [&](int kk, FwdOps& o) {
-      if constexpr (JG && ST_FWD_MASKED) {
-        // no pointer select across address spaces (it would go flat), and no value select
-        // (it would wait for both loads at the load site): exec-masked loads into one buffer
-        if (fk) {
-#pragma unroll
-          for (int e = 0; e < 7; ++e) o.w[e] = s.u.q.K[kk][fc][e];
-          o.w[7] = s.u.q.kk[kk][fc];
-        } else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) o.w[e] = JLD(kk, fr, e);
-        }
-      } else if constexpr (JG) {  // (no pointer select across address spaces: it would go flat)
+      if constexpr (JG) {  // (no pointer select across address spaces: it would go flat)
 #pragma unroll
         for (int e = 0; e < 7; ++e) {
           const double kv = s.u.q.K[kk][fc][e], jv = JLD(kk, fr, e);
@@ -958,7 +878,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     // once the backward pass is done with it
     auto lq_solve = [&]() {
       BwdOps A1, B1;
-      if constexpr (!(JG && ST_J_AHEAD == 2)) bwd_load(N - 1, s.u.q.g, A1);
+      bwd_load(N - 1, s.u.q.g, A1);
       double pv = 0.0;  // lanes 0..6: p_{k+1}
       auto bstage = [&](int kk, const BwdOps& o) {
         const double g = bwd_g(kk, o, pv);
@@ -967,36 +887,28 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
         pv = g + t2;
         if (fk) s.u.q.kk[kk][l - 7] = -t2;
       };
-      if constexpr (JG && ST_J_AHEAD == 2) {
-        stage_loop2<BwdOps>(N - 1, -1, N, [&](int kk, BwdOps& o) { bwd_load(kk, s.u.q.g, o); }, bstage);
-      } else {
 #pragma unroll 1
-        for (int kk = N - 1; kk >= 0; kk -= 2) {
-          const int k1 = kk >= 1 ? kk - 1 : 0, k2 = kk >= 2 ? kk - 2 : 0;
-          bwd_load(k1, s.u.q.g, B1);
-          bstage(kk, A1);
-          if (kk >= 1) {
-            bwd_load(k2, s.u.q.g, A1);
-            bstage(kk - 1, B1);
-          }
+      for (int kk = N - 1; kk >= 0; kk -= 2) {
+        const int k1 = kk >= 1 ? kk - 1 : 0, k2 = kk >= 2 ? kk - 2 : 0;
+        bwd_load(k1, s.u.q.g, B1);
+        bstage(kk, A1);
+        if (kk >= 1) {
+          bwd_load(k2, s.u.q.g, A1);
+          bstage(kk - 1, B1);
         }
       }
       WSYNC();
       double X = 0.0;  // lanes 0..6: xt_k
-      if constexpr (JG && ST_J_AHEAD == 2) {
-        stage_loop2<FwdOps>(0, 1, N, fwd_load, [&](int kk, const FwdOps& o) { X = fwd_stage(kk, o, X); });
-      } else {
-        FwdOps A2, B2;
-        fwd_load(0, A2);
+      FwdOps A2, B2;
+      fwd_load(0, A2);
 #pragma unroll 1
-        for (int kk = 0; kk < N; kk += 2) {
-          const int k1 = kk + 1 < N ? kk + 1 : kk, k2 = kk + 2 < N ? kk + 2 : kk;
-          fwd_load(k1, B2);
-          X = fwd_stage(kk, A2, X);
-          if (kk + 1 < N) {
-            fwd_load(k2, A2);
-            X = fwd_stage(kk + 1, B2, X);
-          }
+      for (int kk = 0; kk < N; kk += 2) {
+        const int k1 = kk + 1 < N ? kk + 1 : kk, k2 = kk + 2 < N ? kk + 2 : kk;
+        fwd_load(k1, B2);
+        X = fwd_stage(kk, A2, X);
+        if (kk + 1 < N) {
+          fwd_load(k2, A2);
+          X = fwd_stage(kk + 1, B2, X);
         }
       }
       WSYNC();
@@ -1012,7 +924,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     // barrier gradient: scripts/st_obs_shoe_diag.py, the N = 60 obstacle runs of test_gpu_bands).
     auto dual_residual = [&](bool cl) -> double {
       BwdOps A3, B3;
-      if constexpr (!(JG && ST_J_AHEAD == 2)) bwd_load(N - 1, s.u.q.g, A3);
+      bwd_load(N - 1, s.u.q.g, A3);
       double rho = 0.0, rmax = 0.0;
       auto rstage = [&](int kk, const BwdOps& o) {
         const double g = bwd_g(kk, o, rho);
@@ -1020,18 +932,14 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
         // lanes 0..6: + K' g_u (the lq_solve backward pass's pv); lanes 7, 8 are not read on
         rho = cl ? g + o.a * bcast(g, 7) + o.b * bcast(g, 8) : g;
       };
-      if constexpr (JG && ST_J_AHEAD == 2) {
-        stage_loop2<BwdOps>(N - 1, -1, N, [&](int kk, BwdOps& o) { bwd_load(kk, s.u.q.g, o); }, rstage);
-      } else {
 #pragma unroll 1
-        for (int kk = N - 1; kk >= 0; kk -= 2) {
-          const int k1 = kk >= 1 ? kk - 1 : 0, k2 = kk >= 2 ? kk - 2 : 0;
-          bwd_load(k1, s.u.q.g, B3);
-          rstage(kk, A3);
-          if (kk >= 1) {
-            bwd_load(k2, s.u.q.g, A3);
-            rstage(kk - 1, B3);
-          }
+      for (int kk = N - 1; kk >= 0; kk -= 2) {
+        const int k1 = kk >= 1 ? kk - 1 : 0, k2 = kk >= 2 ? kk - 2 : 0;
+        bwd_load(k1, s.u.q.g, B3);
+        rstage(kk, A3);
+        if (kk >= 1) {
+          bwd_load(k2, s.u.q.g, A3);
+          rstage(kk - 1, B3);
         }
       }
       return wmax(rmax);
@@ -1061,7 +969,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     // ---------------- interior point (Mehrotra predictor-corrector) ----------------
     int it = 0;
     bool conv = false, fail = false;
-    // dual residual carried by the steps (ST_RES_RECUR): the LQ direction solves the linearised
+    // dual residual carried by the steps: the LQ direction solves the linearised
     // stationarity exactly, so a step of length alpha scales the condensed gradient by
     // (1 - alpha); the adjoint sweep runs at the first iteration and wherever the carried value
     // would end the loop (convergence, or acceptance at a factorisation failure)
@@ -1104,14 +1012,14 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       const double mu = wsum(mus) / mcount;
       ST_ACC(ST_RESID, t_r0)
       ST_STAMP(t_d0)
-      const bool carried = ST_RES_RECUR && have_rd;
+      const bool carried = have_rd;
       double rdm = carried ? rd_carry : dual_residual(kvalid);
       bool rd_cl = carried || kvalid;
       ST_ACC(ST_DUAL, t_d0)
       last_res = fmax(rdm, rpm);
       last_mu = mu;
       if (!(last_res == last_res) || !(mu == mu) || last_res > 1e300) { fail = true; break; }
-      if (ST_RES_RECUR && have_rd && mu <= 1e2 * tol_mu && fmax(rdm, rpm) <= 1e3 * rtol) {
+      if (have_rd && mu <= 1e2 * tol_mu && fmax(rdm, rpm) <= 1e3 * rtol) {
         // the carried value would end the loop here or below: take the sweep's
         rdm = dual_residual(kvalid);
         rd_cl = kvalid;
@@ -1227,10 +1135,10 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     // stage-locally each pass, so the factor's rounding is refined away instead of entering the
     // answer -- with multiplier updates lm_i += rho_i (c_i v - d_i) until the active rows hold.
     // Certified when the inactive rows are feasible and the active multipliers nonnegative;
-    // otherwise the violated rows join and the negative ones leave (ST_POLISH rounds), and an
+    // otherwise the violated rows join and the negative ones leave (kStPolish rounds), and an
     // uncertified polish keeps the interior point's iterate.
     bool pol_qp = false;
-    if (ST_POLISH > 0 && conv) {
+    if (kStPolish > 0 && conv) {
       double hs = 0.0, qs = 0.0;
       if (stl) {
         hs = fmax(fmax(fmax(Qc[Q00], Qc[Q11]), fmax(Qc[Q22], Qc[Q33])),
@@ -1241,7 +1149,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       hs = 1.0 + wmax(hs);
       qs = 1.0 + wmax(qs);
       // row i's weight (recomputed where used: an array of 12 would stay live across the polish)
-      const double rho_h = ST_AL_RHO * hs;
+      const double rho_h = kStAlRho * hs;
       auto rho = [&](int i) -> double {
         double cn2 = 1.0;
         if (i >= 3 && i < 8) {
@@ -1255,7 +1163,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
 #pragma unroll
       for (int i = 0; i < NR; ++i) act[i] = stl && R.m[i] > 0.0 && la[i] > sl[i];
 #pragma unroll 1
-      for (int round = 0; round < ST_POLISH; ++round) {
+      for (int round = 0; round < kStPolish; ++round) {
         // the interior point's slacks / multipliers are dead from here: sl holds the polish's
         // iterate and la its multipliers (a later round starts from the last round's)
         double w[NR], val[NR] = {};
@@ -1274,7 +1182,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
         bool al_conv = false;
         int held = 0;
 #pragma unroll 1
-        for (int p = 0; p < ST_AL_PASSES; ++p) {
+        for (int p = 0; p < kStAlPasses; ++p) {
           if (stl) {
             double g9[9], y[NR];
             row_values(R, vp, val);
@@ -1317,8 +1225,8 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
         bool viol[NR], neg[NR], bad = false;
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
-          viol[i] = stl && R.m[i] > 0.0 && !act[i] && val[i] - R.d[i] > ST_CERT_PTOL * qs;
-          neg[i] = act[i] && lm[i] < -ST_CERT_DTOL * qs;
+          viol[i] = stl && R.m[i] > 0.0 && !act[i] && val[i] - R.d[i] > kStCertPtol * qs;
+          neg[i] = act[i] && lm[i] < -kStCertDtol * qs;
           bad = bad || viol[i] || neg[i];
         }
         if (al_conv && __all(bad ? 0 : 1) != 0) {
@@ -1341,7 +1249,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     // (kin_merit.hip) and oracle/dyn_sqp.py alike.  (Applying the unconverged iterate and
     // reporting the whole step non-solved threw away a plan from converged QPs: the
     // single-track N = 60 obstacle run on the shoe track lost the car, scripts/band_trace.py.)
-    if (ST_KEEP_ITERATE && sq > 0 && !conv) {
+    if (sq > 0 && !conv) {
       stopped = true;
       break;
     }
@@ -1382,6 +1290,7 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
   if (l == 0) {
     int32_t st;
     if (!finite || s.flag[0] == VC_NONFINITE) st = VC_NONFINITE;
+    else if (s.flag[2] == 0) st = VC_OUT_OF_DOMAIN;  // x* (the last rollout) outside the model's domain
     else if (all_conv) st = VC_SOLVED;
     else st = VC_MAX_ITER;
     A.status[b] = st;
@@ -1419,18 +1328,6 @@ bool st_sqp_built(int N) {
   }
 }
 
-size_t st_sqp_jws_doubles(int N) {
-  switch (N) {
-#define VC_CASE(n) \
-  case n:          \
-    return st_j_global_ok<n>() ? (size_t)n * 48 : 0;
-    VC_ST_HORIZONS(VC_CASE)
-#undef VC_CASE
-    default:
-      return 0;
-  }
-}
-
 // J placement per launch (round 5): the LDS-J kernel runs its waves ~10 % faster (no L2 latency in
 // the LQ sweeps), the global-J kernel fits more workgroups per CU (N = 50 / 60: four instead of
 // three).  A batch the LDS-J kernel holds resident at once (wg_per_cu x CUs problems) takes it; a
@@ -1440,6 +1337,19 @@ template <int N>
 bool st_jg_pick(int B) {
   if constexpr (!st_j_global_ok<N>()) return false;
   else return B > wg_per_cu(sizeof(StSmem<N, false>)) * device_cus();
+}
+// doubles of J workspace per problem a launch of B problems needs: nonzero only where st_jg_pick
+// takes the global-J kernel (a large max_batch no longer allocates it for LDS-J launches)
+size_t st_sqp_jws_doubles(int N, int B) {
+  switch (N) {
+#define VC_CASE(n) \
+  case n:          \
+    return st_jg_pick<n>(B) ? (size_t)n * 48 : 0;
+    VC_ST_HORIZONS(VC_CASE)
+#undef VC_CASE
+    default:
+      return 0;
+  }
 }
 template <int N, int TYRE>
 void st_launch(const StSqpArgs& a, hipStream_t stream) {
@@ -1454,7 +1364,7 @@ void st_launch(const StSqpArgs& a, hipStream_t stream) {
 
 hipError_t launch_st_sqp(const StSqpArgs& a, int N, hipStream_t stream) {
   if (a.B <= 0) return hipSuccess;
-  if (st_sqp_jws_doubles(N) && !a.jws) return hipErrorInvalidValue;  // the workspace the kernel may need
+  if (st_sqp_jws_doubles(N, a.B) && !a.jws) return hipErrorInvalidValue;  // the workspace the kernel needs
   const bool lin = a.car.tyre == VC_TYRE_LINEAR;
   switch (N) {
 #define VC_CASE(n)                                        \

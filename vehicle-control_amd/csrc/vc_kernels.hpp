@@ -245,7 +245,7 @@ struct StSqpArgs {
   int32_t* status;      // [B]
   int32_t* iters;       // [B]
   double* diag;         // [B][4] optional diagnostics, may be null
-  double* jws;          // [B][st_sqp_jws_doubles(N)] stage Jacobians kept out of LDS (null: none needed)
+  double* jws;          // [B][st_sqp_jws_doubles(N, B)] stage Jacobians kept out of LDS (null: none needed)
   int B;
   DynCoef<double> car;
   vc_dyn_mpc w;
@@ -265,7 +265,7 @@ struct CascSqpArgs {
   int32_t* status;      // [B]
   int32_t* iters;       // [B]
   double* diag;         // [B][4] optional diagnostics, may be null
-  double* jws;          // [B][casc_ric_jws_doubles(N, M)] stage Jacobians kept out of LDS (null: none needed)
+  double* jws;          // [B][casc_ric_jws_doubles(N, M, B)] stage Jacobians kept out of LDS (null: none needed)
   double* H_out;        // [B][2H][2H]  (mode 1 only)
   double* g_out;        // [B][2H]      (mode 1 only)
   int mode;             // 0 = full solve, 1 = first QP's H, g only
@@ -328,11 +328,11 @@ hipError_t launch_casc_sqp(const CascSqpArgs& a, int N, int M, hipStream_t strea
 hipError_t launch_casc_ric(const CascSqpArgs& a, int N, int M, hipStream_t stream);
 bool casc_ric_built(int N, int M);
 // doubles per problem of CascSqpArgs.jws for shape (N, M) (0: the kernel keeps its Jacobians in LDS)
-size_t casc_ric_jws_doubles(int N, int M);
+size_t casc_ric_jws_doubles(int N, int M, int B);  // 0: the launch of B problems keeps J in LDS
 hipError_t launch_st_sqp(const StSqpArgs& a, int N, hipStream_t stream);
 bool st_sqp_built(int N);
 // doubles per problem of StSqpArgs.jws for horizon N (0: the kernel keeps its Jacobians in LDS)
-size_t st_sqp_jws_doubles(int N);
+size_t st_sqp_jws_doubles(int N, int B);  // 0: the launch of B problems keeps J in LDS
 bool casc_sqp_built(int N, int M);
 size_t dyn_sqp_smem_bytes(int N);
 int dyn_sqp_debug_stride();

@@ -239,7 +239,7 @@ int casc_solve(vc_ctx* c, int B, const void* x0, const void* kappa, const void* 
     a.g_out = (double*)g_out;
   }
   if (mode == 0 && casc_stagewise(c)) {
-    if (const size_t jd = vc::casc_ric_jws_doubles(c->N, c->p.casc.horizon_pm)) {
+    if (const size_t jd = vc::casc_ric_jws_doubles(c->N, c->p.casc.horizon_pm, B)) {
       if (int r = ensure_scratch(c, &c->jw, &c->jw_bytes, (size_t)B * jd * 8)) return r;
       a.jws = (double*)c->jw;
     }
@@ -296,7 +296,7 @@ int st_solve(vc_ctx* c, int B, const void* x0, const void* kappa, const void* ds
     a.iters = iters;
     a.diag = (double*)diag;
   }
-  if (const size_t jd = vc::st_sqp_jws_doubles(N)) {
+  if (const size_t jd = vc::st_sqp_jws_doubles(N, B)) {
     if (int r = ensure_scratch(c, &c->jw, &c->jw_bytes, (size_t)B * jd * 8)) return r;
     a.jws = (double*)c->jw;
   }
@@ -397,6 +397,17 @@ vc_ctx* vc_create(int device, int model, int N, int max_batch, int dtype, const 
   if (dtype != VC_F64 && dtype != VC_F32) { fail(nullptr, VC_E_ARG, "bad dtype %d", dtype); return nullptr; }
   if (N < 1 || N > 4096) { fail(nullptr, VC_E_ARG, "bad horizon N=%d", N); return nullptr; }
   if (max_batch < 1) { fail(nullptr, VC_E_ARG, "bad max_batch %d", max_batch); return nullptr; }
+  // obs.inside (ABI 11) is a switch, and only the SQP models' QP and merit use it: the kinematic
+  // merit keeps its C1 extension inside the margin floor, so an inside-mode kinematic QP would
+  // disagree with its own line search
+  if (params->obs.inside != 0 && params->obs.inside != 1) {
+    fail(nullptr, VC_E_ARG, "obs.inside=%d must be 0 or 1", params->obs.inside);
+    return nullptr;
+  }
+  if (model == VC_MODEL_KINEMATIC && params->obs.inside) {
+    fail(nullptr, VC_E_ARG, "obs.inside=1 is not supported by the kinematic model (dynamic / cascaded only)");
+    return nullptr;
+  }
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
   if (e != hipSuccess || ndev == 0) {

@@ -12,7 +12,7 @@ import os
 
 LIB_NAME = "libvcmpc.so"
 LIB_PATH = os.environ.get("VCMPC_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME))
-ABI_VERSION = 11
+ABI_VERSION = 12
 VC_MAX_OBSTACLES = 16
 OBS_MARGIN_MIN = 0.05  # VC_OBS_MARGIN_MIN (csrc/vc_kernels.hpp)
 
@@ -20,10 +20,11 @@ VC_MODEL_KINEMATIC, VC_MODEL_DYNAMIC, VC_MODEL_CASCADED = 0, 1, 2
 VC_F64, VC_F32 = 0, 1
 VC_HOST_PTRS, VC_DEVICE_PTRS = 0, 1
 VC_TYRE_FIALA, VC_TYRE_LINEAR = 0, 1
-VC_SOLVED, VC_MAX_ITER, VC_NONFINITE = 0, 1, 2
+VC_SOLVED, VC_MAX_ITER, VC_NONFINITE, VC_OUT_OF_DOMAIN = 0, 1, 2, 3
 VC_OK, VC_E_ARG, VC_E_HIP, VC_E_UNSUPPORTED = 0, -1, -2, -3
 
-STATUS_NAMES = {VC_SOLVED: "solved", VC_MAX_ITER: "max_iter", VC_NONFINITE: "nonfinite"}
+STATUS_NAMES = {VC_SOLVED: "solved", VC_MAX_ITER: "max_iter", VC_NONFINITE: "nonfinite",
+                VC_OUT_OF_DOMAIN: "out_of_domain"}
 
 
 class vc_kin_car(C.Structure):

@@ -27,7 +27,7 @@ import numpy as np
 from .. import _abi
 from ..config import make_params, obstacle_list
 from ..solver import Context
-from .controller import Controller
+from .controller import Controller, neutral_restart
 
 IUX, IS = 0, 4
 IFX, IW = 0, 1
@@ -131,14 +131,20 @@ class BatchedSingleTrackMPC(Controller):
         u0, xbar, ustar, status, iters = self.ctx.solve(x0f, kf, dsf, ubar)
         bad = status != 0
         if bad.any():
+            # the retry is neutral in its horizon too: ds, kappa from the state prediction x0 at
+            # every stage (vc_simulate's restart), not from the previous plan the failed solve used
             idx = np.nonzero(bad)[0]
-            r = self.ctx.solve(cast(x0f[idx]), cast(kf[idx]), cast(dsf[idx]),
+            ds_n, kap_n = dyn_horizon_params(x0[idx, IS], np.repeat(x0[idx, IUX, None], self.N, axis=1), self.dt,
+                                             self.car.track.k)
+            r = self.ctx.solve(cast(x0f[idx]), cast(kap_n), cast(ds_n),
                                np.zeros((len(idx), self.N, self.na), self.np_dtype))
             u0[idx], xbar[idx], ustar[idx], status[idx], iters[idx] = r
         self.action_prediction = np.swapaxes(ustar, 1, 2).astype(np.float64)
         self.state_prediction = np.swapaxes(xbar, 1, 2).astype(np.float64)
+        u0 = u0.astype(np.float64)
+        neutral_restart(status, x0, u0, self.state_prediction, self.action_prediction, None)
         self.status, self.iters = status, iters
-        return u0.astype(np.float64)
+        return u0
 
 
 def casc_horizon_params(s0, ux_pred, mpc_dt, N, M, ds_pm, k_of_s):
@@ -219,12 +225,18 @@ class BatchedCascadedMPC(Controller):
         bad = status != 0
         if bad.any():
             idx = np.nonzero(bad)[0]
-            r = self.ctx.solve(np.ascontiguousarray(x0[idx]), np.ascontiguousarray(kappa[idx]),
-                               np.ascontiguousarray(ds[idx]), np.ascontiguousarray(self._neutral(x0, kappa)[idx]))
+            ux_n = np.repeat(x0[idx, IUX, None], self.H, axis=1)   # neutral horizon (see BatchedSingleTrackMPC)
+            ds_n, kap_n = casc_horizon_params(x0[idx, IS], ux_n, self.dt, self.N, self.M, self.ds_pm,
+                                              self.car.track.k)
+            r = self.ctx.solve(np.ascontiguousarray(x0[idx]), kap_n, ds_n,
+                               np.ascontiguousarray(self._neutral(x0[idx], kap_n)))
             u0[idx], xbar[idx], ustar[idx], status[idx], iters[idx] = r
+            kappa[idx] = kap_n
         self._fresh = status != 0
         self.action_prediction = np.swapaxes(ustar, 1, 2).copy()
         self.state_prediction = np.swapaxes(xbar, 1, 2).copy()
+        neutral_restart(status, x0, u0, self.state_prediction, self.action_prediction,
+                         lambda rows: np.swapaxes(self._neutral(x0[rows], kappa[rows]), 1, 2), self.N)
         self.status, self.iters = status, iters
         return u0
 

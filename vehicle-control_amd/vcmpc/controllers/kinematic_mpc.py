@@ -19,7 +19,7 @@ import numpy as np
 from .. import _abi
 from ..config import make_params, obstacle_list
 from ..solver import Context
-from .controller import Controller
+from .controller import Controller, neutral_restart
 
 IV, IS = 0, 2
 # Real-time-iteration globalisation of the closed-loop controller: a trust region
@@ -161,6 +161,10 @@ class BatchedKinematicMPC(Controller):
             u0[idx], xbar[idx], ustar[idx], status[idx], iters[idx] = r
         self.action_prediction = np.swapaxes(ustar, 1, 2).copy()
         self.state_prediction = np.swapaxes(xbar, 1, 2).copy()
+        # a retry without a finite plan restarts from the neutral warm start (u = 0, the state at
+        # every stage), as vc_simulate does: a non-finite plan must not become the next ds
+        nonfin = (status == _abi.VC_NONFINITE) | ~np.isfinite(ustar).all(axis=(1, 2)) | ~np.isfinite(xbar).all(axis=(1, 2))
+        neutral_restart(nonfin, x0, u0, self.state_prediction, self.action_prediction, None)
         if self.shift:  # vc_qp.shift, as vc_simulate does: a solved vehicle's next warm start one stage on
             ok = status == 0
             self.action_prediction[ok, :, :-1] = self.action_prediction[ok, :, 1:].copy()

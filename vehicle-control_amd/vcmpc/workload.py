@@ -100,19 +100,25 @@ def c4_shard(total: int, rank: int, world: int, seed: int = 31, N: int = 20):
 # ----------------------------------------------------------------------------
 # C3 / C5: dynamic single-track SQP-MPC, N = 40, fp32
 # ----------------------------------------------------------------------------
-def _dyn_screen(x0, ubar, kappa, ds, p, tyre):
-    """Warm-start rollout inside the model's domain (host-side screen only)."""
+def _dyn_screen(x0, ubar, kappa, ds, p, tyre, domain_only=False):
+    """Warm-start rollout inside the model's domain (host-side screen only).  domain_only: just
+    the spatial model's own domain -- finite, Ux > 0 and s' = (Ux cos epsi - Uy sin epsi) /
+    (1 - kappa ey) > 0 at every stage (dynamic_car.py:169-191 divides by s')."""
     from .host_models import dyn_rollout_np  # local numpy RK4 used only for screening
     X = dyn_rollout_np(x0, ubar, kappa, ds, p, tyre)
     ok = np.isfinite(X).all(axis=(1, 2))
-    with np.errstate(invalid="ignore"):
+    with np.errstate(invalid="ignore", over="ignore"):
+        if domain_only:
+            k = kappa[:, :X.shape[1]]
+            sdot = (X[..., 0] * np.cos(X[..., 6]) - X[..., 1] * np.sin(X[..., 6])) / (1.0 - k * X[..., 5])
+            return ok & (X[..., 0] > 0).all(1) & (sdot > 0).all(1)
         ok &= (X[..., 0] > 5.0).all(1) & (np.abs(X[..., 1]) < 3.0).all(1) & (np.abs(X[..., 2]) < 1.5).all(1)
         ok &= (np.abs(X[..., 3]) < 0.45).all(1) & (np.abs(X[..., 6]) < 0.8).all(1)
     return ok
 
 
 def dynamic_batch(B: int, N: int = 40, seed: int = 31, mpc_dt: float = 0.03, tyre: str = "linear",
-                  car_cfg=None):
+                  car_cfg=None, ranges: str = "traces", stats: dict | None = None):
     """BASELINE config 3 workload, float32, seeded:
       x0:    Ux ~ U(8, 22), Uy ~ U(-0.3, 0.3), r ~ U(-0.2, 0.6), delta ~ U(-0.07, 0.24),
              s ~ U(0, 300), ey ~ U(-2.5, 2.5), epsi ~ U(-0.3, 0.3), t = 0
@@ -122,7 +128,13 @@ def dynamic_batch(B: int, N: int = 40, seed: int = 31, mpc_dt: float = 0.03, tyr
       kappa: piecewise constant over 4 segments, each ~ U(0, 0.047)
       ds:    mpc_dt * Ux0 for every stage (cascaded_mpc.py:323-327, constant-speed prediction)
       ubar:  Fx = F0 + U(-300, 300) with F0 ~ U(-2000, 2000) per problem; w ~ U(-0.1, 0.1)
-    Problems whose warm-start rollout leaves the model's domain are re-drawn."""
+    Problems whose warm-start rollout leaves the model's domain are re-drawn.
+
+    ranges="survey": SURVEY 8(d)'s C3 sampler as written -- Ux ~ U(5, 22), ey ~ U(-3, 3) and the
+    Fx warm start ~ U(-6000, 6000) N per stage (the other ranges as above); only warm starts
+    whose rollout leaves the spatial model's own domain (Ux <= 0, s' <= 0, non-finite) are
+    re-drawn, so low-speed problems and hard-braking warm starts stay in the set.  ``stats``
+    (a dict) receives the number drawn and the number re-drawn."""
     from .config import load_config
     from .host_models import dyn_params
     p = dyn_params(car_cfg if car_cfg is not None else load_config("dynamic_car"))
@@ -132,19 +144,26 @@ def dynamic_batch(B: int, N: int = 40, seed: int = 31, mpc_dt: float = 0.03, tyr
     while have < B:
         m = max(2 * (B - have), 16)
         x0 = np.zeros((m, 8))
-        x0[:, 0] = rng.uniform(8, 22, m)
+        survey = ranges == "survey"
+        x0[:, 0] = rng.uniform(5 if survey else 8, 22, m)
         x0[:, 1] = rng.uniform(-0.3, 0.3, m)
         x0[:, 2] = rng.uniform(-0.2, 0.6, m)
         x0[:, 3] = rng.uniform(-0.07, 0.24, m)
         x0[:, 4] = rng.uniform(0, 300, m)
-        x0[:, 5] = rng.uniform(-2.5, 2.5, m)
+        x0[:, 5] = rng.uniform(-3, 3, m) if survey else rng.uniform(-2.5, 2.5, m)
         x0[:, 6] = rng.uniform(-0.3, 0.3, m)
         seg = rng.uniform(0, 0.047, (m, 4))
         kappa = np.repeat(seg, -(-N // 4), axis=1)[:, :N]
         ds = np.repeat(mpc_dt * x0[:, :1], N, axis=1)
-        F0 = rng.uniform(-2000, 2000, (m, 1))
-        ubar = np.stack([F0 + rng.uniform(-300, 300, (m, N)), rng.uniform(-0.1, 0.1, (m, N))], -1)
-        ok = _dyn_screen(x0, ubar, kappa, ds, p, tyre)
+        if survey:
+            fx = rng.uniform(-6000, 6000, (m, N))
+        else:
+            fx = rng.uniform(-2000, 2000, (m, 1)) + rng.uniform(-300, 300, (m, N))
+        ubar = np.stack([fx, rng.uniform(-0.1, 0.1, (m, N))], -1)
+        ok = _dyn_screen(x0, ubar, kappa, ds, p, tyre, domain_only=survey)
+        if stats is not None:
+            stats["drawn"] = stats.get("drawn", 0) + m
+            stats["redrawn"] = stats.get("redrawn", 0) + int((~ok).sum())
         for k, v in (("x0", x0), ("kappa", kappa), ("ds", ds), ("ubar", ubar)):
             out[k].append(v[ok])
         have += int(ok.sum())
