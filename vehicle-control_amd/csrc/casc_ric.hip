@@ -250,8 +250,18 @@ __device__ __forceinline__ void cr_jst(CrJP<JG> J, int k, int r, int c, double v
   if constexpr (JG) GBuf(J, (N + M) * 384).st((uint32_t)(((k * 6 + r) * 8 + c) * 8), v);
   else J[k].m[r][c] = v;
 }
+// columns c, c + 1 (c even) of one row: global J as one 16-byte store (GBuf::st2)
+template <int N, int M, bool JG>
+__device__ __forceinline__ void cr_jst2(CrJP<JG> J, int k, int r, int c, double v0, double v1) {
+  if constexpr (JG) GBuf(J, (N + M) * 384).st2((uint32_t)(((k * 6 + r) * 8 + c) * 8), v0, v1);
+  else {
+    J[k].m[r][c] = v0;
+    J[k].m[r][c + 1] = v1;
+  }
+}
 #define JLD(k, r, c) cr_jld<N, M, JG>(J, (k), (r), (c))
 #define JST(k, r, c, v) cr_jst<N, M, JG>(J, (k), (r), (c), (v))
+#define JST2(k, r, c, v0, v1) cr_jst2<N, M, JG>(J, (k), (r), (c), (v0), (v1))
 
 // global J: the linearisation's stores visible to every lane of the wave before they are read
 template <bool JG>
@@ -461,40 +471,50 @@ __global__ __launch_bounds__(WTH) void casc_ric_kernel(CascSqpArgs A) {
           pm_spatial_ode<D2, double>(x, u2, D2(s.kap[j]), c, f);
           const double h = s.dsv[j];
           // rows (V, ey, epsi) of I + h df/dx at y slots (0, 1, 2); inputs scaled by S; the
-          // Fy slew's c row (3) = e_u1; t-row over (V, ey, epsi)
+          // Fy slew's c row (3) = e_u1; t-row over (V, ey, epsi).  Each task owns one column pair
+          // of rows 0..2 -- (0, 1), (2, 3) with column 3 zero, (6, 7) -- stored by one 16-byte store
+          // per row after the seed branches (the three tasks of a stage are adjacent lanes: one
+          // store instruction per row); the constant entries (columns 4, 5 of rows 0..2, rows 3..5)
+          // are written by the first linearisation of the launch only
           const int yi[3] = {0, 2, 3};
+          double cv0[3], cv1[3];
           if (pr == 0) {
 #pragma unroll
             for (int r = 0; r < 3; ++r) {
-              JST(j, r, 0, (r == 0 ? 1.0 : 0.0) + h * f[yi[r]].d[0]);
-              JST(j, r, 1, (r == 1 ? 1.0 : 0.0) + h * f[yi[r]].d[1]);
+              cv0[r] = (r == 0 ? 1.0 : 0.0) + h * f[yi[r]].d[0];
+              cv1[r] = (r == 1 ? 1.0 : 0.0) + h * f[yi[r]].d[1];
             }
             s.u.l.trow[j][tsw(j, 0)] = h * f[4].d[0];
             s.u.l.trow[j][tsw(j, 1)] = h * f[4].d[1];
           } else if (pr == 1) {
 #pragma unroll
-            for (int r = 0; r < 3; ++r) JST(j, r, 2, (r == 2 ? 1.0 : 0.0) + h * f[yi[r]].d[0]);
+            for (int r = 0; r < 3; ++r) {
+              cv0[r] = (r == 2 ? 1.0 : 0.0) + h * f[yi[r]].d[0];
+              cv1[r] = 0.0;
+            }
             s.u.l.trow[j][tsw(j, 2)] = h * f[4].d[0];
 #pragma unroll
-            for (int cc = 3; cc < 6; ++cc) {
-              JST(j, 0, cc, 0.0);
-              JST(j, 1, cc, 0.0);
-              JST(j, 2, cc, 0.0);
-              s.u.l.trow[j][tsw(j, cc)] = 0.0;
+            for (int cc = 3; cc < 6; ++cc) s.u.l.trow[j][tsw(j, cc)] = 0.0;
+            if (sq == 0) {
+#pragma unroll
+              for (int r = 0; r < 3; ++r) JST2(j, r, 4, 0.0, 0.0);
+#pragma unroll
+              for (int r = 3; r < 6; ++r)
+#pragma unroll
+                for (int cc = 0; cc < 8; cc += 2) JST2(j, r, cc, 0.0, (r == 3 && cc == 6) ? 1.0 : 0.0);
             }
-#pragma unroll
-            for (int r = 3; r < 6; ++r)
-#pragma unroll
-              for (int cc = 0; cc < 8; ++cc) JST(j, r, cc, (r == 3 && cc == 7) ? 1.0 : 0.0);
           } else {
 #pragma unroll
             for (int r = 0; r < 3; ++r) {
-              JST(j, r, 6, h * f[yi[r]].d[0] * S);
-              JST(j, r, 7, h * f[yi[r]].d[1] * S);
+              cv0[r] = h * f[yi[r]].d[0] * S;
+              cv1[r] = h * f[yi[r]].d[1] * S;
             }
             s.u.l.trow[j][tsw(j, 6)] = h * f[4].d[0] * S;
             s.u.l.trow[j][tsw(j, 7)] = h * f[4].d[1] * S;
           }
+          const int cp = pr == 0 ? 0 : (pr == 1 ? 2 : 6);
+#pragma unroll
+          for (int r = 0; r < 3; ++r) JST2(j, r, cp, cv0[r], cv1[r]);
         }
       }
     }

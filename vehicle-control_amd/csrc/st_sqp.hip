@@ -267,8 +267,18 @@ __device__ __forceinline__ void st_jst(StJP<N, JG> J, int k, int r, int c, doubl
   if constexpr (JG) GBuf(J, N * 384).st((uint32_t)(((k * 6 + r) * 8 + c) * 8), v);
   else J[k].m[r][c] = v;
 }
+// columns c, c + 1 (c even) of one row: global J as one 16-byte store
+template <int N, bool JG>
+__device__ __forceinline__ void st_jst2(StJP<N, JG> J, int k, int r, int c, double v0, double v1) {
+  if constexpr (JG) GBuf(J, N * 384).st2((uint32_t)(((k * 6 + r) * 8 + c) * 8), v0, v1);
+  else {
+    J[k].m[r][c] = v0;
+    J[k].m[r][c + 1] = v1;
+  }
+}
 #define JLD(k, r, c) st_jld<N, JG>(J, (k), (r), (c))
 #define JST(k, r, c, v) st_jst<N, JG>(J, (k), (r), (c), (v))
+#define JST2(k, r, c, v0, v1) st_jst2<N, JG>(J, (k), (r), (c), (v0), (v1))
 
 template <int N, bool JG>
 __device__ __forceinline__ StJP<N, JG> st_jac(StSmem<N, JG>& s, const StSqpArgs& A, int b) {
@@ -545,15 +555,13 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
           const D2 kp(s.kap[kk]);
           const D2 th = dyn_fx_split(u2[0]);
           rk4_apply<D2, 8>(x, D2(s.dsv[kk]), [&](const D2* xx, D2* f) { dyn_spatial_ode_alg_th<D2, double>(xx, u2, th, kp, c, f); }, xn);
-          // columns of [A6 | B6] (y index of the seeds) and the t-row
+          // columns of [A6 | B6] (y index of the seeds) and the t-row; the four tasks of a stage
+          // are adjacent lanes, so each row store covers the stage's whole 64-byte row (global J)
           const int c0 = pr < 3 ? 2 * pr : 6, c1 = c0 + 1;
           const double s0 = pr == 3 ? S : 1.0;
           const int yr[6] = {0, 1, 2, 3, 5, 6};
 #pragma unroll
-          for (int r = 0; r < 6; ++r) {
-            JST(kk, r, c0, xn[yr[r]].d[0] * s0);
-            JST(kk, r, c1, xn[yr[r]].d[1]);
-          }
+          for (int r = 0; r < 6; ++r) JST2(kk, r, c0, xn[yr[r]].d[0] * s0, xn[yr[r]].d[1]);
           s.u.l.trow[kk][tsw(kk, c0)] = xn[7].d[0] * s0;
           s.u.l.trow[kk][tsw(kk, c1)] = xn[7].d[1];
         } else {

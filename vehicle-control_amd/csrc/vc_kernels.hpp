@@ -79,6 +79,16 @@ struct GBuf {
     typedef __attribute__((ext_vector_type(2))) unsigned u2;
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), r, off, 0, 0);
   }
+  // two adjacent doubles as one 16-byte store (off 16-byte aligned): where the lanes of one store
+  // instruction cover whole 64-byte rows this way, each row leaves the CU as one full write instead
+  // of several partial ones (the memory side counts a request per partial write: st_sqp's J went out
+  // ~4x its size as 8-byte column stores, r05 PMC)
+  __device__ __forceinline__ void st2(uint32_t off, double v0, double v1) const {
+    typedef __attribute__((ext_vector_type(4))) unsigned u4;
+    typedef __attribute__((ext_vector_type(2))) double d2v;
+    const d2v v = {v0, v1};
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), r, off, 0, 0);
+  }
 };
 
 // 1/x to full fp64 accuracy: hardware v_rcp_f64 + two Newton steps (five VALU ops against
