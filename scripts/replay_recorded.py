@@ -119,6 +119,8 @@ def main():
     ap.add_argument("--prox", type=float, nargs="+", default=[None], help="override qp.prox (sweep)")
     ap.add_argument("--dump", default=None, help="npz prefix for per-step arrays")
     ap.add_argument("--segments", type=int, default=1, help="replay windows side by side (see replay())")
+    ap.add_argument("--inside", action="store_true", help="the reference's barrier inside obstacles (vc_obstacles.inside)")
+    ap.add_argument("--table", action="store_true", help="print a markdown table of the results at the end")
     args = ap.parse_args()
     g = dict(np.load(os.path.join(ROOT, "tests", "golden", "replay_kat.npz"), allow_pickle=False))
     recs = json.loads(str(g["configs"]))
@@ -128,12 +130,18 @@ def main():
             for sqp in args.sqp:
                 r = replay(run, g, recs[run], sqp, qp=None if prox is None else {"prox": prox},
                            dump=None if args.dump is None else f"{args.dump}_{run}_p{prox}_s{sqp}.npz",
-                           segments=args.segments)
+                           segments=args.segments, cfg_extra={"obstacle_inside": True} if args.inside else None)
                 res.append(r)
                 print(json.dumps({k: v for k, v in r.items() if k != "example_plan"}), flush=True)
     if args.out:
         with open(args.out, "w") as f:
             json.dump(res, f, indent=1)
+    if args.table:
+        print("| run | steps | non-solved | median \\|ΔFx\\| [N] | median \\|Δw\\| [rad/s] | within 1 % | plan dev median [m] |")
+        print("|---|---|---|---|---|---|---|")
+        for r in res:
+            print(f"| {r['run']} | {r['steps']} | {r['nonsolved']} | {r['dFx_median']:.3g} | {r['dw_median']:.2g} | "
+                  f"{100 * r['frac_within_1pct']:.1f} % | {r['plan_dev_median_m']:.2g} |")
 
 
 if __name__ == "__main__":
