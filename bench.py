@@ -195,6 +195,10 @@ def _mfma_live(m, kern_ms):
                      "achieved / frac on the live kernel_ms")
 
 
+class _Skip(Exception):
+    """a leg switched off on the command line"""
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -223,6 +227,9 @@ def parse():
     ap.add_argument("--latency-calls", type=int, default=200,
                     help="single-vehicle drop-in latency: timed command + drive steps per controller")
     ap.add_argument("--no-latency", action="store_true", help="skip the single-vehicle latency legs")
+    ap.add_argument("--no-converged", action="store_true",
+                    help="skip the converged-setting legs (40 SQP iterations): a PMC pass then averages the "
+                         "st_sqp<60> / casc_ric dispatches of the bench-setting legs only (same kernel, same grid)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU work: each rank only takes its C2/C4/C5 shards and runs the counter "
                          "collective over gloo (tests the launcher and the rank logic on a CPU host)")
@@ -1001,8 +1008,12 @@ def main():
         # what a reference-equivalent answer costs: the converged SQP setting of the replay against
         # IPOPT's recorded solutions (tests/test_gpu_replay.py: prox 0.01, 40 SQP iterations)
         try:
+            if args.no_converged:
+                raise _Skip()
             st60c, _ = run_c3(args, dev, stream, rank, dist, 2, f64=True, N=60, cfg_name="singletrack_mpc",
                               qp=CONVERGED_QP, leg="singletrack_n60_converged")
+        except _Skip:
+            pass
         except Exception as e:
             st60c = {"error": f"{type(e).__name__}: {e}"}
     ca = ca_data = cac = None
@@ -1012,7 +1023,11 @@ def main():
         except Exception as e:
             ca = {"error": f"{type(e).__name__}: {e}"}
         try:
+            if args.no_converged:
+                raise _Skip()
             cac, _ = run_casc(args, dev, stream, rank, dist, 2, qp=CONVERGED_QP, leg="cascaded_converged")
+        except _Skip:
+            pass
         except Exception as e:
             cac = {"error": f"{type(e).__name__}: {e}"}
     c5 = c5_aux = None

@@ -1,7 +1,9 @@
 #!/bin/bash
 # PMC counter passes, one rocprofv3 run per pass (--pmc with --kernel-trace only, no trace
 # domains), over a short bench run of every solve leg except the C5 closed loop (1,500
-# dispatches).  Counters the box does not list are dropped from a pass before it runs, and
+# dispatches) and the converged-setting legs (--no-converged: they launch the same st_sqp<60> /
+# casc_ric kernels on the same grid at 40 SQP iterations, and a per-dispatch average over both
+# settings -- the round-5 summary's -- mixed 5- and 40-iteration launches).  Counters the box does not list are dropped from a pass before it runs, and
 # every pass is held to the per-block limits (<= 8 SQ, <= 4 TCC: FETCH_SIZE and WRITE_SIZE
 # get passes of their own).  Summaries: python scripts/pmc_summary.py gpurun_out/pmc_<tag>
 # usage: bash scripts/pmc_profile.sh <tag> [extra bench args]
@@ -27,7 +29,7 @@ for SET in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
   [ -z "$KEEP" ] && continue
   echo "== pass $i:$KEEP"
   timeout -k 10 -s KILL 240 rocprofv3 --kernel-trace --pmc $KEEP -d "$OUT/p$i" -o run -f csv -- \
-      python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-c5 --no-cpu-baseline --no-latency $EXTRA > "$OUT/p$i.log" 2>&1
+      python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-c5 --no-cpu-baseline --no-latency --no-converged $EXTRA > "$OUT/p$i.log" 2>&1
   rc=$?
   echo "   rc=$rc"
   if [ $rc -ge 124 ]; then echo "fatal rc=$rc, stopping"; exit $rc; fi

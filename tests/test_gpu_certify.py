@@ -21,7 +21,8 @@ So here every returned answer of each bench batch is checked independently of th
 
 Sets: the C2 batch (1,024), the bench's C4 problem set (65,536, vcmpc.workload.c4_shard), the
 C4-style kinematic_batch(65536, seed = 31) where 23921 lives, kinematic N = 50 (8,192), C3
-(4,096, N = 40, 3 SQP iterations), single-track N = 60 (4,096) and cascaded 20 + 40 (4,096).
+(4,096, N = 40, 3 SQP iterations), C3 on SURVEY 8(d)'s full sampler ranges (4,096; round 6),
+single-track N = 60 (4,096) and cascaded 20 + 40 (4,096).
 These are the bench legs' own seeds (bench.py, rank 0).  A failure here is a kernel bug to fix.
 """
 import numpy as np
@@ -105,6 +106,9 @@ def _sqp_set(name):
     if name == "c3":          # bench.py run_c3, rank 0
         d = {k: v.astype(np.float64) for k, v in dynamic_batch(4096, N=40, seed=31).items()}
         return "dyn", 40, d, load_config("dynamic_mpc"), "linear"
+    if name == "c3_survey":   # bench.py c3_survey: SURVEY 8(d)'s sampler ranges as written
+        d = {k: v.astype(np.float64) for k, v in dynamic_batch(4096, N=40, seed=31, ranges="survey").items()}
+        return "dyn", 40, d, load_config("dynamic_mpc"), "linear"
     if name == "st_n60":      # bench.py singletrack_n60_f64
         d = {k: v.astype(np.float64) for k, v in dynamic_batch(4096, N=60, seed=31).items()}
         return "dyn", 60, d, load_config("singletrack_mpc"), "linear"
@@ -113,7 +117,7 @@ def _sqp_set(name):
     raise ValueError(name)
 
 
-@pytest.mark.parametrize("name", ["c3", "st_n60", "cascaded"])
+@pytest.mark.parametrize("name", ["c3", "st_n60", "cascaded", "c3_survey"])
 def test_sqp_batch_every_qp_certified(name, dyn_params):
     from oracle import casc_sqp as CS
     from oracle import dyn_sqp as D
@@ -163,8 +167,28 @@ def test_sqp_batch_every_qp_certified(name, dyn_params):
           f"in QP units {np.abs((us[-1] - r['u_oracle']) / sc).max(axis=(1, 2))[solved].max():.3e}; "
           f"> 1e-5: {int((err[solved] > U_TOL).sum())}; worst {[(int(b), float(err[b])) for b in worst]}")
     assert not fails, fails[:20]
-    assert (solved.mean() >= 0.997), np.bincount(st_k[-1])
     assert err[solved].max() < U_TOL
+    if name != "c3_survey":
+        assert (solved.mean() >= 0.997), np.bincount(st_k[-1])
+        return
+    # SURVEY 8(d)'s full ranges (round 6, VERDICT r05 missing 3: Ux down to 5 m/s, ey to +-3 m, Fx warm
+    # starts to +-6000 N per stage): the solved fraction is reported, and every problem the kernel does
+    # not solve is one the contract cannot solve either -- the oracle's own SQP ends outside the spatial
+    # model's domain (the kernel's VC_OUT_OF_DOMAIN), or one of its QPs has no feasible point (phase-1 LP
+    # with a checked Farkas certificate, oracle/feasibility.py)
+    from oracle import feasibility as F
+    bad = np.nonzero(~solved)[0]
+    print(f"  c3_survey: solved {solved.mean():.4f} ({int(solved.sum())}/{B}); status counts "
+          f"{np.bincount(st_k[-1], minlength=4).tolist()} (solved, max_iter, nonfinite, out_of_domain)")
+    if len(bad):
+        sub = {k: v[bad] for k, v in d.items()}
+        ref = D.dyn_sqp_solve(sub["x0"], sub["ubar"], sub["kappa"], sub["ds"], dyn_params, W, tyre, keep_qps=True)
+        first, farkas = F.first_infeasible_iteration(ref["hist"])
+        explained = ~ref["in_domain"] | ((first >= 0) & farkas)
+        print(f"  non-solved: oracle x* outside the domain {int((~ref['in_domain']).sum())}, infeasible QP with a "
+              f"Farkas certificate {int(((first >= 0) & farkas).sum())}, unexplained "
+              f"{[(int(b), int(st_k[-1][b])) for b in bad[~explained][:10]]}")
+        assert explained.all()
 
 
 def test_kin_ltv_interior_point_status_rests_on_the_true_residual(kin_W):
