@@ -217,7 +217,9 @@ def _sqp_worker(job):
         predict, in_dom = _predictor(job)
         x0, kap, ds = (np.asarray(job[k], np.float64) for k in ("x0", "kappa", "ds"))
         p, tyre = job["p"], job["tyre"]
-        out = {k: np.zeros((K, B)) for k in ("stat", "pfeas", "dfeas", "comp", "scale", "alpha", "dz_err")}
+        out = {k: np.zeros((K, B)) for k in ("stat", "pfeas", "dfeas", "comp", "scale", "alpha", "dz_err", "f_k", "f_o",
+                                             "f_mag")}
+        out["refused_both"] = np.zeros((K, B), bool)
         out["exact_ok"] = np.zeros((K, B), bool)
         uo = np.array(us[0], np.float64, copy=True)
         stopped_o = np.zeros(B, bool)
@@ -239,6 +241,16 @@ def _sqp_worker(job):
             out["alpha"][k - 1] = alpha
             out["exact_ok"][k - 1] = ok_o
             out["dz_err"][k - 1] = np.abs(zk - dz_o).max(axis=1)
+            # the QP objective 1/2 z'Hz + g'z at the kernel's step and at the oracle's optimum, and the
+            # magnitude of its terms at the optimum (what fp64 rounding of f is relative to)
+            hz = np.einsum("bij,bj->bi", H, dz_o)
+            out["f_k"][k - 1] = 0.5 * np.einsum("bi,bij,bj->b", zk, H, zk) + np.einsum("bi,bi->b", g, zk)
+            out["f_o"][k - 1] = 0.5 * np.einsum("bi,bi->b", dz_o, hz) + np.einsum("bi,bi->b", g, dz_o)
+            out["f_mag"][k - 1] = 0.5 * np.einsum("bi,bij,bj->b", np.abs(dz_o), np.abs(H), np.abs(dz_o)) + \
+                np.einsum("bi,bi->b", np.abs(g), np.abs(dz_o))
+            # no step length keeps the rollout in the domain for the oracle's step (alpha = 0) and the
+            # kernel took none either: that QP's answer is not applied by the contract
+            out["refused_both"][k - 1] = (alpha == 0) & (np.abs(z1).max(axis=1) == 0)
             # (b) the oracle's own SQP iterate
             if k == 1:
                 zo, oko = dz_o, ok_o

@@ -62,9 +62,6 @@
 #ifndef KIN_DOT_CH
 #define KIN_DOT_CH 8  // terms per chunk of the residual dot products
 #endif
-#ifndef KIN_CHOL_RL
-#define KIN_CHOL_RL 1  // pivot-chain operands L[k+2..k+3][k..k+1] by v_readlane from their lanes (0: from LDS)
-#endif
 #ifndef KIN_CHOL_CH
 #define KIN_CHOL_CH 8  // rows per trailing-update chunk, loaded one chunk ahead (4: +5 % factorisation time)
 #endif
@@ -692,17 +689,6 @@ __device__ bool factor_blocked(double (&Mr)[Dims<N>::n], d4 (&acc)[Tiles<N>::NT]
       const double x = Mr[k], y = Mr[k + 1];
       Mr[k] = lane > k ? x : 0.0;
       Mr[k + 1] = lane > k + 1 ? y : 0.0;
-      // the next pivot pair's operands L[k+2][k], L[k+3][k], L[k+2][k+1], L[k+3][k+1] are this
-      // step's x, y in lanes k+2, k+3: read them from those lanes (v_readlane) instead of through the
-      // LDS store -> load round trip, which sat on the pivot chain once per two columns (the other
-      // columns of the update still read the stored factor).  Same values, same FMA order.
-      double rl[2][2];
-      if (KIN_CHOL_RL) {
-        rl[0][0] = lane_bcast(x, k + 2);
-        rl[0][1] = lane_bcast(x, k + 3);
-        rl[1][0] = lane_bcast(y, k + 2);
-        rl[1][1] = lane_bcast(y, k + 3);
-      }
       const double* cA = &s.Lc[lc_base<n>(k)];
       const double* cB = &s.Lc[lc_base<n>(k + 1)];
       constexpr int CH = 4;
@@ -724,9 +710,7 @@ __device__ bool factor_blocked(double (&Mr)[Dims<N>::n], d4 (&acc)[Tiles<N>::NT]
 #pragma unroll
         for (int q = 0; q < CH; ++q) {
           const int j = J0 + ch * CH + q;
-          const bool lk = KIN_CHOL_RL && ch == 0 && q < 2;  // compile-time: a lookahead column
-          const double la = lk ? rl[0][q & 1] : u0[ch & 1][q], lb = lk ? rl[1][q & 1] : u1[ch & 1][q];
-          if (j < c1) Mr[j] = fma(-y, lb, fma(-x, la, Mr[j]));
+          if (j < c1) Mr[j] = fma(-y, u1[ch & 1][q], fma(-x, u0[ch & 1][q], Mr[j]));
         }
         if (ch >= 1 && ch <= 3) part(ch - 1, k + 2);
         fence();
