@@ -220,6 +220,7 @@ def _sqp_worker(job):
         out = {k: np.zeros((K, B)) for k in ("stat", "pfeas", "dfeas", "comp", "scale", "alpha", "dz_err", "f_k", "f_o",
                                              "f_mag")}
         out["refused_both"] = np.zeros((K, B), bool)
+        out["step_ratio"] = np.zeros((K, B))
         out["exact_ok"] = np.zeros((K, B), bool)
         uo = np.array(us[0], np.float64, copy=True)
         stopped_o = np.zeros(B, bool)
@@ -251,6 +252,10 @@ def _sqp_worker(job):
             # no step length keeps the rollout in the domain for the oracle's step (alpha = 0) and the
             # kernel took none either: that QP's answer is not applied by the contract
             out["refused_both"][k - 1] = (alpha == 0) & (np.abs(z1).max(axis=1) == 0)
+            # the kernel's applied step against the oracle's optimum of the same QP, as a step length:
+            # |z1|_inf / |dz_o|_inf (1 = full step, 1/2^j a cut-back; compared with alpha, the domain test's)
+            with np.errstate(divide="ignore", invalid="ignore"):
+                out["step_ratio"][k - 1] = np.abs(z1).max(axis=1) / np.abs(dz_o).max(axis=1)
             # (b) the oracle's own SQP iterate
             if k == 1:
                 zo, oko = dz_o, ok_o

@@ -257,18 +257,12 @@ __device__ __forceinline__ void qmul(const double* Q, const double* v, double* o
 
 // stage-Jacobian element (k, r, c): the LDS array, or the global workspace through a buffer
 // resource (GBuf: one offset VGPR per access, bounds-checked to the problem's N stages)
-#ifndef ST_JSOFF
-#define ST_JSOFF 1  // global J loads: stage offset k * 384 as the buffer load's SGPR soffset (0: one VGPR offset)
-#endif
+// (round 6: the stage offset k * 384 as the loads' SGPR soffset instead, per-lane offsets loop-invariant,
+// was 2.8 % slower at N = 60 -- profiles/r06/kin_ab/sqp_ab_soffset_r06j.log)
 template <int N, bool JG>
 __device__ __forceinline__ double st_jld(StJP<N, JG> J, int k, int r, int c) {
-  if constexpr (JG) {
-    if (ST_JSOFF)  // k is wave-uniform at every call site (stage loops, or a clamped uniform index)
-      return GBuf(J, N * 384).ld((uint32_t)((r * 8 + c) * 8), (uint32_t)__builtin_amdgcn_readfirstlane(k * 384));
-    return GBuf(J, N * 384).ld((uint32_t)(((k * 6 + r) * 8 + c) * 8));
-  } else {
-    return J[k].m[r][c];
-  }
+  if constexpr (JG) return GBuf(J, N * 384).ld((uint32_t)(((k * 6 + r) * 8 + c) * 8));
+  else return J[k].m[r][c];
 }
 template <int N, bool JG>
 __device__ __forceinline__ void st_jst(StJP<N, JG> J, int k, int r, int c, double v) {

@@ -75,11 +75,7 @@ struct GBuf {
   __device__ __forceinline__ double ld(uint32_t off) const {
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
   }
-  // voff: the per-lane part of the byte offset (VGPR), soff: a wave-uniform part (SGPR soffset operand),
-  // so a loop over uniform blocks (stages) needs no per-load VALU address arithmetic
-  __device__ __forceinline__ double ld(uint32_t voff, uint32_t soff) const {
-    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
-  }
+
   __device__ __forceinline__ void st(uint32_t off, double v) const {
     typedef __attribute__((ext_vector_type(2))) unsigned u2;
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), r, off, 0, 0);
