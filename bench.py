@@ -227,8 +227,6 @@ def parse():
     ap.add_argument("--latency-calls", type=int, default=200,
                     help="single-vehicle drop-in latency: timed command + drive steps per controller")
     ap.add_argument("--no-latency", action="store_true", help="skip the single-vehicle latency legs")
-    ap.add_argument("--no-graph", action="store_true",
-                    help="C2: time eager launches instead of replaying the captured HIP graph of one step")
     ap.add_argument("--no-converged", action="store_true",
                     help="skip the converged-setting legs (40 SQP iterations): a PMC pass then averages the "
                          "st_sqp<60> / casc_ric dispatches of the bench-setting legs only (same kernel, same grid)")
@@ -931,22 +929,6 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    # One step = restore the warm start (device copy) + vc_solve, captured once into a HIP graph
-    # (torch.cuda.CUDAGraph over the context stream: vc_solve with device pointers only enqueues the
-    # kernel) and replayed: the two launches' host dispatch leaves the step (--no-graph: eager).
-    graph, graph_note = None, "eager (--no-graph)"
-    if not args.no_graph:
-        try:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=stream):
-                step()
-            torch.cuda.synchronize(dev)
-            g.replay()
-            torch.cuda.synchronize(dev)
-            graph, graph_note = g, "hipGraph replay (warm-start restore + vc_solve captured on the context stream)"
-        except Exception as e:  # capture unsupported: time the eager launches
-            graph_note = f"eager (graph capture failed: {type(e).__name__}: {e})"
-            torch.cuda.synchronize(dev)
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(args.steps)]
     dist.barrier()
@@ -954,19 +936,11 @@ def main():
     leg_push("c2")
     t0 = time.perf_counter()
     for i in range(args.steps):
-        if graph is not None:
-            graph.replay()
-        else:
-            step(events[i])
+        step(events[i])
     torch.cuda.synchronize(dev)
     leg_pop()
     dist.barrier()
     elapsed = time.perf_counter() - t0
-    if graph is not None:
-        # the kernel's own time: the same K launches eager, HIP events around vc_solve on its stream
-        for i in range(args.steps):
-            step(events[i])
-        torch.cuda.synchronize(dev)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
     st = status.cpu().numpy()
     it = iters.cpu().numpy()
@@ -1090,7 +1064,7 @@ def main():
                      "v <= 1 m/s or reaches |epsi| >= 1.2 rad are re-drawn)"),
             "config": {"workload": f"C2 kinematic-bicycle LTV-MPC, B={B} per GPU, N={N_HORIZON}, fp64",
                        "batch_per_gpu": B, "global_batch": B * world, "horizon": N_HORIZON,
-                       "parallelism": f"dp{world} (independent shards)", "launch": graph_note},
+                       "parallelism": f"dp{world} (independent shards)"},
             # the binding roofline is fp64 compute ("not HBM").  The kernel's fp64 work
             # splits between the VALU and the matrix cores: the v_mfma_f64_16x16x4_f64 tiles (the
             # normal-matrix build C'DC and the blocked factorisation's trailing updates) execute
