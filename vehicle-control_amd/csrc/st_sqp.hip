@@ -94,19 +94,9 @@ using StJ = StJT<(N == 30 || N == 60) ? 8 : 9>;
 // whether the global-J instantiation exists for horizon N (the launcher picks it per batch: st_jg_pick)
 template <int N>
 constexpr bool st_j_global_ok() { return N >= 45; }
-// Round 6: the Riccati passes no longer read the global workspace element by element (6-12 buffer
-// loads per lane and stage, each with its own offset, which the compiler kept in AGPRs and waited on one
-// pair at a time).  A four-slot LDS ring of whole stages sits between them: lanes 0..47 load one double
-// each of a stage two stages ahead of its use (one coalesced 384 B load per stage), store it into the
-// ring one stage ahead, and the passes read the ring with the LDS version's addressing (st_jring_*).
-template <int N>
-struct StJG {
-  double* g;       // the problem's global workspace (48 doubles per stage, [6][8] row-major)
-  StJ<N>* ring;    // LDS ring, stage k in slot k & 3
-};
 template <int N, bool JG>
-using StJP = std::conditional_t<JG, StJG<N>, StJ<N>*>;  // workspace + LDS ring, or LDS
-constexpr int ST_JRING = 4;
+using StJP = std::conditional_t<JG, double*, StJ<N>*>;  // workspace base (GBuf) or LDS
+struct StNone {};  // (global: 48 doubles = 384 B per stage, [6][8] row-major)
 // Row stride of ub: odd (3; conflict-free lane-per-stage reads) where the LDS allows, N = 60 takes
 // 2 -- a block above 53,248 B leaves two workgroups per CU instead of three (measured: rocprofv3
 // LDS_Block_Size 53,248 ran three per CU, 54,272 two; r04).  xs: rotated rows of 8 (StageRows8)
@@ -117,8 +107,8 @@ struct StSmem {
   StageRows8<N> xs;   // prediction (N columns, dynamics for k < N-1), rotated rows (vc_kernels.hpp)
   double ub[N][st_ub_w<N>()];  // current ubar; [2] pad where 3
   double kap[N], dsv[N];
-  // J[k][row][col], cols Ux, Uy, r, delta, ey, epsi | dFx, dw (LDS; JG: the four-slot ring of StJG)
-  std::conditional_t<JG, StJ<N>[ST_JRING], StJ<N>[N]> J;
+  // J[k][row][col], cols Ux, Uy, r, delta, ey, epsi | dFx, dw (LDS unless JG)
+  std::conditional_t<JG, StNone, StJ<N>[N]> J;
   union {
     struct {
       double Qt[N][NQ + 1];  // stage Hessian + barrier, this iteration; [NQ] pad
@@ -271,18 +261,18 @@ __device__ __forceinline__ void qmul(const double* Q, const double* v, double* o
 // was 2.8 % slower at N = 60 -- profiles/r06/kin_ab/sqp_ab_soffset_r06j.log)
 template <int N, bool JG>
 __device__ __forceinline__ double st_jld(StJP<N, JG> J, int k, int r, int c) {
-  if constexpr (JG) return J.ring[k & (ST_JRING - 1)].m[r][c];  // stage k must be in the ring (st_jring_step)
+  if constexpr (JG) return GBuf(J, N * 384).ld((uint32_t)(((k * 6 + r) * 8 + c) * 8));
   else return J[k].m[r][c];
 }
 template <int N, bool JG>
 __device__ __forceinline__ void st_jst(StJP<N, JG> J, int k, int r, int c, double v) {
-  if constexpr (JG) GBuf(J.g, N * 384).st((uint32_t)(((k * 6 + r) * 8 + c) * 8), v);
+  if constexpr (JG) GBuf(J, N * 384).st((uint32_t)(((k * 6 + r) * 8 + c) * 8), v);
   else J[k].m[r][c] = v;
 }
 // columns c, c + 1 (c even) of one row: global J as one 16-byte store
 template <int N, bool JG>
 __device__ __forceinline__ void st_jst2(StJP<N, JG> J, int k, int r, int c, double v0, double v1) {
-  if constexpr (JG) GBuf(J.g, N * 384).st2((uint32_t)(((k * 6 + r) * 8 + c) * 8), v0, v1);
+  if constexpr (JG) GBuf(J, N * 384).st2((uint32_t)(((k * 6 + r) * 8 + c) * 8), v0, v1);
   else {
     J[k].m[r][c] = v0;
     J[k].m[r][c + 1] = v1;
@@ -294,47 +284,9 @@ __device__ __forceinline__ void st_jst2(StJP<N, JG> J, int k, int r, int c, doub
 
 template <int N, bool JG>
 __device__ __forceinline__ StJP<N, JG> st_jac(StSmem<N, JG>& s, const StSqpArgs& A, int b) {
-  if constexpr (JG) return StJG<N>{GBuf::uniform(A.jws + (size_t)b * N * 48), s.J};
+  if constexpr (JG) return GBuf::uniform(A.jws + (size_t)b * N * 48);
   else return s.J;
 }
-
-// The J ring of a pass over the stages k0, k0 + d, k0 + 2d, ... (d = +-1), which reads stage k + d's
-// operands while it works on stage k: st_jring_prime puts stage k0 into the ring and starts the loads of
-// k0 + d and k0 + 2d into the two register buffers; st_jring_step(k), at stage k before the reads of
-// k + d, stores stage k + d from its buffer (p = the stage's parity from k0) and reuses the buffer for
-// k + 3d.  The slot k + d overwrites held k - 3d, read four stages ago (LDS operations of a wave execute
-// in order).  No-ops for LDS J.  Lanes 0..47 own element l = 8 r + c of a stage.
-template <int N, bool JG>
-__device__ __forceinline__ double st_jring_ld(StJP<N, JG> J, int k, int l) {
-  if constexpr (JG) return GBuf(J.g, N * 384).ld((uint32_t)(k * 384 + (l < 48 ? l : 0) * 8));
-  else return 0.0;
-}
-template <int N, bool JG>
-__device__ __forceinline__ void st_jring_st(StJP<N, JG> J, int k, int l, double v) {
-  if constexpr (JG) {
-    if (l < 48) J.ring[k & (ST_JRING - 1)].m[l >> 3][l & 7] = v;
-  }
-}
-template <int N, bool JG>
-__device__ __forceinline__ void st_jring_prime(StJP<N, JG> J, int k0, int d, int l, double (&rb)[2]) {
-  if constexpr (JG) {
-    st_jring_st<N, JG>(J, k0, l, st_jring_ld<N, JG>(J, k0, l));
-    const int k1 = k0 + d, k2 = k0 + 2 * d;
-    rb[0] = (k1 >= 0 && k1 < N) ? st_jring_ld<N, JG>(J, k1, l) : 0.0;  // uniform conditions
-    rb[1] = (k2 >= 0 && k2 < N) ? st_jring_ld<N, JG>(J, k2, l) : 0.0;
-  }
-}
-template <int N, bool JG>
-__device__ __forceinline__ void st_jring_step(StJP<N, JG> J, int k, int d, int p, int l, double (&rb)[2]) {
-  if constexpr (JG) {
-    const int kw = k + d, kl = k + 3 * d;
-    double& b = p ? rb[1] : rb[0];
-    if (kw >= 0 && kw < N) st_jring_st<N, JG>(J, kw, l, b);
-    if (kl >= 0 && kl < N) b = st_jring_ld<N, JG>(J, kl, l);
-  }
-}
-#define JR_PRIME(k0, d, rb) st_jring_prime<N, JG>(J, (k0), (d), l, rb)
-#define JR_STEP(k, d, p, rb) st_jring_step<N, JG>(J, (k), (d), (p), l, rb)
 
 template <int N, int TYRE, bool JG>
 __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
@@ -528,15 +480,12 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
           const int r = l < 6 ? l : 0;
           // rows kk + 1 (LDS) or kk + 1, kk + 2 (global J) loaded ahead of use
           constexpr int AH = 1;
-          double d = 0.0, jn[AH][6], rb[2];
-          JR_PRIME(0, 1, rb);
+          double d = 0.0, jn[AH][6];
 #pragma unroll
           for (int a = 0; a < AH; ++a)
 #pragma unroll
             for (int cc = 0; cc < 6; ++cc) jn[a][cc] = JLD(a < N - 2 ? a : N - 2, r, cc);
           for (int kk = 0; kk < N - 1; ++kk) {
-            if (kk & 1) JR_STEP(kk, 1, 1, rb);  // (uniform parity: the buffer index stays static)
-            else JR_STEP(kk, 1, 0, rb);
             double jc[6];
 #pragma unroll
             for (int cc = 0; cc < 6; ++cc) jc[cc] = jn[0][cc];
@@ -844,17 +793,13 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     auto factor = [&]() -> bool {
       bool ok = true;
       FacOps A0, B0;
-      double rb[2];
-      JR_PRIME(N - 1, -1, rb);
       fac_load(N - 1, A0);
 #pragma unroll 1
       for (int kk = N - 1; kk >= 0; kk -= 2) {
         const int k1 = kk >= 1 ? kk - 1 : 0, k2 = kk >= 2 ? kk - 2 : 0;
-        JR_STEP(kk, -1, 0, rb);
         fac_load(k1, B0);
         ok = fac_stage(kk, A0) && ok;
         if (kk >= 1) {  // uniform
-          JR_STEP(kk - 1, -1, 1, rb);
           fac_load(k2, A0);
           ok = fac_stage(kk - 1, B0) && ok;
         }
@@ -943,8 +888,6 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     // once the backward pass is done with it
     auto lq_solve = [&]() {
       BwdOps A1, B1;
-      double rb[2];
-      JR_PRIME(N - 1, -1, rb);
       bwd_load(N - 1, s.u.q.g, A1);
       double pv = 0.0;  // lanes 0..6: p_{k+1}
       auto bstage = [&](int kk, const BwdOps& o) {
@@ -957,11 +900,9 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
 #pragma unroll 1
       for (int kk = N - 1; kk >= 0; kk -= 2) {
         const int k1 = kk >= 1 ? kk - 1 : 0, k2 = kk >= 2 ? kk - 2 : 0;
-        JR_STEP(kk, -1, 0, rb);
         bwd_load(k1, s.u.q.g, B1);
         bstage(kk, A1);
         if (kk >= 1) {
-          JR_STEP(kk - 1, -1, 1, rb);
           bwd_load(k2, s.u.q.g, A1);
           bstage(kk - 1, B1);
         }
@@ -969,16 +910,13 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
       WSYNC();
       double X = 0.0;  // lanes 0..6: xt_k
       FwdOps A2, B2;
-      JR_PRIME(0, 1, rb);
       fwd_load(0, A2);
 #pragma unroll 1
       for (int kk = 0; kk < N; kk += 2) {
         const int k1 = kk + 1 < N ? kk + 1 : kk, k2 = kk + 2 < N ? kk + 2 : kk;
-        JR_STEP(kk, 1, 0, rb);
         fwd_load(k1, B2);
         X = fwd_stage(kk, A2, X);
         if (kk + 1 < N) {
-          JR_STEP(kk + 1, 1, 1, rb);
           fwd_load(k2, A2);
           X = fwd_stage(kk + 1, B2, X);
         }
@@ -996,8 +934,6 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
     // barrier gradient: scripts/st_obs_shoe_diag.py, the N = 60 obstacle runs of test_gpu_bands).
     auto dual_residual = [&](bool cl) -> double {
       BwdOps A3, B3;
-      double rb[2];
-      JR_PRIME(N - 1, -1, rb);
       bwd_load(N - 1, s.u.q.g, A3);
       double rho = 0.0, rmax = 0.0;
       auto rstage = [&](int kk, const BwdOps& o) {
@@ -1009,11 +945,9 @@ __global__ __launch_bounds__(WTH) void st_sqp_kernel(StSqpArgs A) {
 #pragma unroll 1
       for (int kk = N - 1; kk >= 0; kk -= 2) {
         const int k1 = kk >= 1 ? kk - 1 : 0, k2 = kk >= 2 ? kk - 2 : 0;
-        JR_STEP(kk, -1, 0, rb);
         bwd_load(k1, s.u.q.g, B3);
         rstage(kk, A3);
         if (kk >= 1) {
-          JR_STEP(kk - 1, -1, 1, rb);
           bwd_load(k2, s.u.q.g, A3);
           rstage(kk - 1, B3);
         }
