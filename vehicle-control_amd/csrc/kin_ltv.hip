@@ -62,6 +62,9 @@
 #ifndef KIN_DOT_CH
 #define KIN_DOT_CH 8  // terms per chunk of the residual dot products
 #endif
+#ifndef KIN_EARLY_SET
+#define KIN_EARLY_SET 0  // 1: a failed early attempt's corrected active set seeds the final polish (A/B)
+#endif
 #ifndef KIN_CHOL_CH
 #define KIN_CHOL_CH 8  // rows per trailing-update chunk, loaded one chunk ahead (4: +5 % factorisation time)
 #endif
@@ -1087,6 +1090,8 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
   double tol_cur = tol_early;
   bool polished = false, pchol_fail = false;
   int rounds = 0;
+  // KIN_EARLY_SET: the active set a failed early attempt ended with (its rounds' corrections applied)
+  bool e_alo_b = false, e_ahi_b = false, e_alo_c = false, e_ahi_c = false, have_early = false;
 #pragma unroll 1
   for (;;) {
   if (finite) {
@@ -1225,6 +1230,9 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
     bool ahi_b = guess(bx.hasHi, bx.lhi, bx.shi, (tapb >> 2) & 3);
     bool alo_c = guess(cs.hasLo, cs.llo, cs.slo, (tapb >> 4) & 3);
     bool ahi_c = guess(cs.hasHi, cs.lhi, cs.shi, (tapb >> 6) & 3);
+    if (KIN_EARLY_SET && have_early) {  // uniform
+      alo_b = e_alo_b; ahi_b = e_ahi_b; alo_c = e_alo_c; ahi_c = e_ahi_c;
+    }
     const int max_rounds = tol_cur > tol ? min(A.qp.polish, KIN_EARLY_ROUNDS) : A.qp.polish;
 #pragma unroll 1
     for (int round = 0; round < max_rounds; ++round) {
@@ -1399,6 +1407,10 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
           else ahi_c = true;
         }
       }
+    }
+    if (KIN_EARLY_SET && !polished && tol_cur > tol) {
+      e_alo_b = alo_b; e_ahi_b = ahi_b; e_alo_c = alo_c; e_ahi_c = ahi_c;
+      have_early = true;
     }
   }
 
