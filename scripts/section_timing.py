@@ -18,7 +18,7 @@ from vcmpc.workload import kinematic_batch  # noqa: E402
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 tol = float(sys.argv[2]) if len(sys.argv) > 2 else 1e-10
 names = ["S1 rollout", "setup", "resid", "build", "chol", "solve", "pol fact", "polish", "out", "S2 jac", "S3 sens", "S4 hess",
-         "pol AL", "AL passes"]
+         "pol AL", "AL passes", "upd rounds", "upd cyc", "drop rounds"]
 dev = torch.device("cuda:0")
 d = kinematic_batch(B, seed=31)
 t = {k: torch.from_numpy(v).to(dev) for k, v in d.items()}

@@ -44,6 +44,9 @@
 #ifndef KIN_EARLY_ROUNDS
 #define KIN_EARLY_ROUNDS 2  // active-set rounds of that attempt before the interior point resumes
 #endif
+#ifndef KIN_EARLY_MAX
+#define KIN_EARLY_MAX 2  // ... and up to this many while each further round's factor is a rank-one update
+#endif
 #ifndef KIN_TAPIA_F
 #define KIN_TAPIA_F 1.02  // ratio gap that makes the indicators decisive (else lambda > s)
 #endif
@@ -64,6 +67,9 @@
 #endif
 #ifndef KIN_EARLY_SET
 #define KIN_EARLY_SET 0  // 1: a failed early attempt's corrected active set seeds the final polish (A/B)
+#endif
+#ifndef KIN_UPDATE
+#define KIN_UPDATE 1  // polish rounds after the first update the factor by rank one where they can (0: refactor)
 #endif
 #ifndef KIN_CHOL_CH
 #define KIN_CHOL_CH 8  // rows per trailing-update chunk, loaded one chunk ahead (4: +5 % factorisation time)
@@ -163,8 +169,9 @@ __device__ __forceinline__ lds_cdouble* lds_opaque(const double* p) {
 #endif
 // T_SWEEP = the serial rollout S1; T_S2 / T_S3 / T_S4 the sweep's other three parts
 // T_UPDATE: the polish's matrix build + factorisation (part of T_POLISH); T_PAL its augmented-
-// Lagrangian passes (cycles), T_PPASS their count
-enum { T_SWEEP = 0, T_SETUP, T_RESID, T_BUILD, T_CHOL, T_SOLVE, T_UPDATE, T_POLISH, T_OUT, T_S2, T_S3, T_S4, T_PAL, T_PPASS, T_NSLOT };
+// Lagrangian passes (cycles), T_PPASS their count; T_NUPD the rounds whose factor came from
+// factor_update, T_UCYC those updates' cycles, T_NDROP the rounds ended by dropping a bound or row
+enum { T_SWEEP = 0, T_SETUP, T_RESID, T_BUILD, T_CHOL, T_SOLVE, T_UPDATE, T_POLISH, T_OUT, T_S2, T_S3, T_S4, T_PAL, T_PPASS, T_NUPD, T_UCYC, T_NDROP, T_NSLOT };
 
 
 template <int N>
@@ -757,6 +764,99 @@ __device__ bool factor_blocked(double (&Mr)[Dims<N>::n], d4 (&acc)[Tiles<N>::NT]
   return ok;
 }
 
+// Inclusive prefix sum over the wave (lane i: sum of v over lanes <= i): a DPP prefix within each
+// 16-lane row, then the earlier rows' totals from three readlanes.
+__device__ __forceinline__ double wave_prefix(double v, int lane) {
+  v += dpp_row_shr<1>(v, 0.0);
+  v += dpp_row_shr<2>(v, 0.0);
+  v += dpp_row_shr<4>(v, 0.0);
+  v += dpp_row_shr<8>(v, 0.0);
+  const double r0 = lane_bcast(v, 15), r1 = lane_bcast(v, 31), r2 = lane_bcast(v, 47);
+  return v + (lane >= 16 ? r0 : 0.0) + (lane >= 32 ? r1 : 0.0) + (lane >= 48 ? r2 : 0.0);
+}
+
+// The polish's next factor from the current one when a round changed the reduced matrix by a
+// rank-one term (KIN_UPDATE), instead of a build + factor_blocked (~17 K cycles per round):
+//   upd 1: variable j became fixed.  Its row / column turn into the identity; with
+//          M = [M11 . M13; . . .; M31 . M33] the new factor keeps L11 and L31, and its trailing
+//          block satisfies L33' L33'^T = L33 L33^T + z z^T, z = L[j+1:, j] -- a rank-one update
+//          of the columns after j (the state rows keep their weights, see the polish);
+//   upd 2: state row j became active with weight rho: M' = M + z z^T, z = sqrt(rho) g_F.
+// Both are updates (a dropped bound or row, a downdate, takes the full path).  The update is
+// Gill, Golub, Murray & Saunders' method C1 (Math. Comp. 28, 1974), stable for positive
+// updates, in the form that maps onto lanes: with y = L^-1 z (one forward sweep) and the prefix
+// sums t_k = 1 + sum_{i<=k} y_i^2 (one wave scan), column k of the new factor is
+//     L'_rk = (L_rk + c_k w_r) s_k,   w_r <- w_r - y_k L_rk (before),   c_k = y_k / t_k,
+//     s_k = sqrt(t_k / t_{k-1}),   L'_kk = L_kk s_k,
+// where w starts at z: the recurrence that sets every coefficient is the scan, and the column sweep
+// is lane-local (lane r runs along its own row), so no step waits on the previous one's pivot
+// (a textbook rotation sweep, one pivot chain per column, measured ~450 cycles per column).  Lane k's
+// w is zeroed at column k, so the entries on and above the diagonal stay 0.  (numpy check of both
+// cases against a fresh Cholesky: <= 9e-15 relative.)
+template <int N>
+__device__ bool factor_update(double (&Mr)[Dims<N>::n], Smem<N>& s, int upd, int j, bool fixed, double sqrho,
+                              int lane) {
+  constexpr int n = Dims<N>::n;
+  constexpr int DUMMY = Smem<N>::LC_DUMMY, ZERO = Smem<N>::LC_ZERO;
+  lane = lane_opaque(lane);
+  const int row = lane < n ? lane : 0;
+  // slot of L[lane][k] strictly below the diagonal, else the zero slot (loads) / the dummy (stores)
+  auto below = [&](int k, int other) { return lane > k && lane < n ? lc_base<n>(k) + lane : other; };
+  double z;
+  if (upd == 1) {  // uniform
+    z = s.Lc[below(j, ZERO)];  // column j below the diagonal, then the identity row / column j
+    wave_sync();
+    s.Lc[below(j, DUMMY)] = 0.0;
+    s.Lc[lane < j ? lc_base<n>(lane) + j : DUMMY] = 0.0;
+    s.Lc[lc_start<n>(j)] = 1.0;
+    s.dinv[j] = 1.0;
+  } else {
+    z = (lane < n && !fixed) ? sqrho * s.G[j][lane < n ? lane : n] : 0.0;
+  }
+  wave_sync();
+  // the rows from the stored columns (Mr is dead between rounds: the KKT check needs its registers)
+  {
+    lds_cdouble* L = lds_opaque(&s.Lc[0]);
+#pragma unroll
+    for (int k = 0; k < n; ++k) Mr[k] = L[below(k, ZERO)];
+  }
+  // y = L^-1 z (chol_solve's forward sweep)
+  const double dj = s.dinv[row];
+  double acc = z;
+#pragma unroll
+  for (int k = 0; k < n; ++k) acc -= Mr[k] * lane_bcast(acc * dj, k);
+  const double y = lane < n ? acc * dj : 0.0;
+  const double t = 1.0 + wave_prefix(y * y, lane);
+  const double sk = sqrt(t / (t - y * y)), ck = y / t;
+  const bool ok = __ballot(!(sk > 0.5 && sk < 1e150)) == 0ull;  // uniform: finite scalings (s_k >= 1 in exact arithmetic)
+  wave_sync();
+  if (lane < n) {
+    s.Lc[lc_start<n>(row)] *= sk;
+    s.dinv[row] = dj / sk;
+  }
+  s.tb2[2 * lane] = ck;  // (c_k, s_k) pairs: one 16-byte broadcast read per column
+  s.tb2[2 * lane + 1] = sk;
+  wave_sync();
+  {
+    using lds_cd2 = const __attribute__((address_space(3))) d2;
+    lds_cd2* cs = (lds_cd2*)lds_opaque(&s.tb2[0]);
+    double w = z;
+#pragma unroll
+    for (int k = 0; k < n - 1; ++k) {
+      const double yk = lane_bcast(y, k);
+      const d2 c = cs[k];
+      w = lane_put(w, 0.0, k);
+      const double l = Mr[k];
+      w = fma(-yk, l, w);
+      Mr[k] = fma(c.x, w, l) * c.y;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < n - 1; ++k) s.Lc[below(k, DUMMY)] = Mr[k];
+  wave_sync();  // factor and inverse pivots visible to the solves
+  return ok;
+}
+
 // inequality data of one lane role (box or state row): bounds lo <= y <= hi,
 // slacks slo = y - lo, shi = hi - y, multipliers llo, lhi.
 struct Side {
@@ -1233,7 +1333,16 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
     if (KIN_EARLY_SET && have_early) {  // uniform
       alo_b = e_alo_b; ahi_b = e_ahi_b; alo_c = e_alo_c; ahi_c = e_ahi_c;
     }
-    const int max_rounds = tol_cur > tol ? min(A.qp.polish, KIN_EARLY_ROUNDS) : A.qp.polish;
+    // the early attempt: KIN_EARLY_ROUNDS rounds, then more (up to KIN_EARLY_MAX) only while the next
+    // round's factor is a rank-one update of this one's (an added bound or row: ~7 K cycles against
+    // a rebuild's 18 K); a dropped one sends the problem back to the interior point
+    const bool early = tol_cur > tol;
+    const int max_rounds = early ? min(A.qp.polish, KIN_EARLY_MAX) : A.qp.polish;
+    // KIN_UPDATE: the weight the current factor holds for state row `lane` (0: none), and how the
+    // last round changed the active set (uniform; 1: variable upd_j fixed, 2: row upd_j added,
+    // 0: anything else -- a dropped bound or row, or no factor yet -- which refactors)
+    double rho_k = 0.0;
+    int upd = 0, upd_j = 0;
 #pragma unroll 1
     for (int round = 0; round < max_rounds; ++round) {
       no_hoist();
@@ -1256,14 +1365,29 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
           gn2 += gi * gi;
         }
       }
-      const double rho_c = (act && gn2 > 1e-28) ? AL_RHO * hdiag_max / gn2 : 0.0;
+      const double rho_new = (act && gn2 > 1e-28) ? AL_RHO * hdiag_max / gn2 : 0.0;
+      // a row the factor already holds keeps its weight (any positive weight has the same fixed
+      // point), so fixing a variable leaves the matrix one rank-one update away (factor_update)
+      const double rho_c = (KIN_UPDATE && rho_k > 0.0 && rho_new > 0.0) ? rho_k : rho_new;
       const double bnd_c = act ? ((alo_c ? cs.lo : cs.hi) - gfix) : 0.0;  // b' = b - G_X zfix
       const double base = (lane < n) ? -(gj + h_dot<N>(s, lane)) : 0.0;
       wave_sync();
       s.vc[lane] = rho_c;
       wave_sync();
       VC_TSTAMP(t_pf0)
-      {
+      bool updated = false;
+      if (KIN_UPDATE && upd != 0) {  // uniform
+        // every row but the added one kept its weight (else refactor)
+        const bool same = __ballot(lane < NC && rho_c != rho_k && !(upd == 2 && lane == upd_j)) == 0ull;
+        VC_TSTAMP(t_u0)
+        if (same) updated = factor_update<N>(Mr, s, upd, upd_j, fixed, sqrt(lane_bcast(rho_c, upd_j)), lane);
+#ifdef VC_TIMING
+        if (updated) tacc[T_NUPD] += 1;
+#endif
+        VC_TACC(T_UCYC, t_u0)
+      }
+      rho_k = rho_c;
+      if (!updated) {
         // the interior point's path: H + G' diag(rho_c) G in the accumulator tiles (s.vc =
         // rho_c; zero weights where no row is active), fixed rows / columns set to the identity
         // in the tiles -- D (H + G'WG) D + (I - D) with D the free-variable mask equals the
@@ -1271,7 +1395,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
         // updates) instead of the row-per-lane one
         d4 pacc[Tiles<N>::NT];
         build_normal_acc<N>(pacc, s, 0.0, hjj, lane);
-        const int plr = lane >> 4, plc = lane & 15;
+        const int pl = lane_opaque(lane), plr = pl >> 4, plc = pl & 15;  // not hoisted out of the rounds
 #pragma unroll
         for (int I = 0, t = 0; I < Tiles<N>::NB; ++I) {
 #pragma unroll
@@ -1396,6 +1520,13 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
       const double vb = dual ? dv_b : pv_b, vcr = dual ? dv_c : pv_c;
       const uint64_t who = __ballot(fmax(vb, vcr) == worst);
       const int sel = __builtin_ffsll((long long)who) - 1;
+      const bool sel_box = (__ballot(vb >= vcr) >> sel) & 1ull;
+      upd = dual ? 0 : (sel_box ? 1 : 2);  // an added bound fixes variable sel, an added row is row sel
+      upd_j = sel;
+      if (early && round + 1 >= KIN_EARLY_ROUNDS && (upd == 0 || !KIN_UPDATE)) break;  // uniform
+#ifdef VC_TIMING
+      if (dual) tacc[T_NDROP] += 1;
+#endif
       if (lane == sel) {
         if (vb >= vcr) {  // box constraint of input `lane`
           if (dual) { alo_b = false; ahi_b = false; }
