@@ -44,9 +44,6 @@
 #ifndef KIN_EARLY_ROUNDS
 #define KIN_EARLY_ROUNDS 2  // active-set rounds of that attempt before the interior point resumes
 #endif
-#ifndef KIN_EARLY_MAX
-#define KIN_EARLY_MAX 2  // ... and up to this many while each further round's factor is a rank-one update
-#endif
 #ifndef KIN_TAPIA_F
 #define KIN_TAPIA_F 1.02  // ratio gap that makes the indicators decisive (else lambda > s)
 #endif
@@ -65,11 +62,11 @@
 #ifndef KIN_DOT_CH
 #define KIN_DOT_CH 8  // terms per chunk of the residual dot products
 #endif
-#ifndef KIN_EARLY_SET
-#define KIN_EARLY_SET 0  // 1: a failed early attempt's corrected active set seeds the final polish (A/B)
-#endif
 #ifndef KIN_UPDATE
 #define KIN_UPDATE 1  // polish rounds after the first update the factor by rank one where they can (0: refactor)
+#endif
+#ifndef KIN_RSQ_HALLEY
+#define KIN_RSQ_HALLEY 1  // pivots' 1/sqrt by one third-order step (0: two Newton steps; C2 -0.8 %, C4 -1.2 %)
 #endif
 #ifndef KIN_CHOL_CH
 #define KIN_CHOL_CH 8  // rows per trailing-update chunk, loaded one chunk ahead (4: +5 % factorisation time)
@@ -291,9 +288,16 @@ __device__ double h_dot(const Smem<N>& s, int lane) {
 // dependent chain than IEEE sqrt followed by IEEE divide)
 __device__ __forceinline__ double rsq_nr(double d) {
   double inv = __builtin_amdgcn_rsq(d);
+#if KIN_RSQ_HALLEY
+  // one third-order step: with e = 1 - d y^2, 1/sqrt(d) = y (1 - e)^-1/2 = y (1 + e/2 + 3e^2/8 + O(e^3)):
+  // four dependent operations instead of two Newton steps' eight
+  const double e = fma(-d, inv * inv, 1.0);
+  return fma(inv * e, fma(0.375, e, 0.5), inv);
+#else
   inv = inv * (1.5 - 0.5 * d * inv * inv);
   inv = inv * (1.5 - 0.5 * d * inv * inv);
   return inv;
+#endif
 }
 
 // After a factorisation: row k of L (entries i < k) to Lc[k (k-1)/2 + i], packed rows, for the
@@ -306,108 +310,9 @@ template <int N>
 __device__ __forceinline__ void store_rows(const double (&Mr)[Dims<N>::n], Smem<N>& s, int lane) {
 }
 
-// In-place right-looking Cholesky of the SPD matrix whose row `lane` is Mr (the lower
-// part: entries above the diagonal are not kept).  On return s.Lc holds the columns of L,
-// s.dinv the inverse pivots 1/L_kk (uniform reads), and Mr row `lane` of L strictly below
-// the diagonal with zeros on and above it -- the form chol_solve's select-free forward sweep
-// reads.  Returns false (uniform) if a pivot is not positive.
-//
-// Two columns per step: the 2x2 diagonal block comes from lanes k, k+1 by readlane, both
-// pivots are taken in registers, both columns published to LDS, and one LDS round trip serves
-// the rank-2 trailing update.  Software-pipelined: the pivot block k+2, k+3 depends only on
-// the lookahead columns (chunk 0 of step k's update), so its chain -- readlanes, two rsq +
-// Newton, the column scaling and its LDS stores -- is split in three parts placed in the fence
-// regions of step k's update chunks 1, 2, 3, where the scheduler interleaves it with
-// independent FMAs.  Same operations in the same order as one column per step (bit-identical
-// factor).  The kernel is bound by instruction issue (every VALU instruction ~5 s_memtime
-// ticks at one wave per SIMD, scripts/ubench/thr.hip), so the layout keeps the count down:
-// both update columns load as ds_read_b128 at immediate offsets (lc_base), stores are
-// branch-free (dummy slot: lane-divergent ifs in this unrolled code make the allocator spill).
-template <int N>
-__device__ bool cholesky(double (&Mr)[Dims<N>::n], Smem<N>& s, int lane) {
-  constexpr int n = Dims<N>::n;
-  static_assert(n % 2 == 0, "two-column blocks");
-  constexpr int DUMMY = Smem<N>::LC_DUMMY;
-  lane = lane_opaque(lane);
-  bool ok = true;
-  double pa, pb, pc, pi1, pl21, pi2;  // chain state of the pending pivot block
-  auto part = [&](int p, int k) {
-    if (p == 0) {  // 2x2 diagonal block from lanes k, k+1; first inverse pivot
-      pa = lane_bcast(Mr[k], k);
-      pb = lane_bcast(Mr[k], k + 1);
-      pc = lane_bcast(Mr[k + 1], k + 1);
-      pi1 = rsq_nr(pa);
-    } else if (p == 1) {  // second pivot after column k's update
-      pl21 = pb * pi1;
-      const double d2 = fma(-pl21, pl21, pc);
-      pi2 = rsq_nr(d2);
-      ok = ok && (pa > 0.0) && (d2 > 0.0);
-    } else {  // columns k, k+1 of this lane's row, published
-      const double x = Mr[k] * pi1;  // lane k: a / sqrt(a)
-      const double y = fma(-x, pl21, Mr[k + 1]) * pi2;
-      Mr[k] = x;
-      Mr[k + 1] = y;
-      s.Lc[lane >= k && lane < n ? lc_base<n>(k) + lane : DUMMY] = x;
-      s.Lc[lane >= k + 1 && lane < n ? lc_base<n>(k + 1) + lane : DUMMY] = y;
-      s.dinv[k] = pi1;
-      s.dinv[k + 1] = pi2;
-    }
-  };
-  part(0, 0);
-  part(1, 0);
-  part(2, 0);
-#pragma unroll
-  for (int k = 0; k + 2 < n; k += 2) {
-    wave_sync();  // columns k, k+1 visible
-    fence();
-    const double x = Mr[k], y = Mr[k + 1];
-    // this lane's entries of columns k, k+1 are final: keep them strictly below the diagonal
-    // (lanes <= k hold the diagonal or the unkept upper part, which only the forward sweep reads)
-    Mr[k] = lane > k ? x : 0.0;
-    Mr[k + 1] = lane > k + 1 ? y : 0.0;
-    const double* c0 = &s.Lc[lc_base<n>(k)];      // c0[j] = L[j][k]
-    const double* c1 = &s.Lc[lc_base<n>(k + 1)];  // c1[j] = L[j][k+1]
-    constexpr int CH = KIN_CHOL_CH;
-    const int J0 = k + 2, NCH = (n - J0 + CH - 1) / CH;  // compile-time after unrolling
-    double u0[2][CH], u1[2][CH];
-    auto load = [&](int ch, int buf) {
-#pragma unroll
-      for (int q = 0; q < CH; ++q) {
-        const int j = J0 + ch * CH + q;
-        u0[buf][q] = j < n ? c0[j] : 0.0;
-        u1[buf][q] = j < n ? c1[j] : 0.0;
-      }
-    };
-    load(0, 0);
-#pragma unroll
-    for (int ch = 0; ch < NCH; ++ch) {
-      if (ch + 1 < NCH) load(ch + 1, (ch + 1) & 1);
-      fence();
-      // chunk 0 starts with columns k+2, k+3: the next block's pivots (lookahead)
-#pragma unroll
-      for (int q = 0; q < CH; ++q) {
-        const int j = J0 + ch * CH + q;
-        if (j < n) Mr[j] = fma(-y, u1[ch & 1][q], fma(-x, u0[ch & 1][q], Mr[j]));
-      }
-      if (ch >= 1 && ch <= 3) part(ch - 1, k + 2);
-      fence();
-    }
-#pragma unroll
-    for (int p = NCH - 1; p < 3; ++p) {  // parts no chunk was left to hide
-      part(p < 0 ? 0 : p, k + 2);
-      fence();
-    }
-  }
-  Mr[n - 2] = lane > n - 2 ? Mr[n - 2] : 0.0;
-  Mr[n - 1] = 0.0;
-  store_rows<N>(Mr, s, lane);
-  wave_sync();  // factor and inverse pivots visible to the solves
-  return ok;
-}
-
 // Solve (L L') x = b, lane j holding b_j; returns x_j.  Forward sweep: y_k = acc_k / L_kk is
 // broadcast from lane k, and every lane subtracts L[lane][k] y_k from its accumulator with the
-// row registers zero on and above the diagonal (cholesky), so lane k's accumulator stops
+// row registers zero on and above the diagonal (factor_blocked), so lane k's accumulator stops
 // changing once y_k is taken and y = acc / L_kk at the end -- no per-step select (a finite
 // factor times 0 subtracts exactly 0: the same values as collecting y_k per step).  Backward
 // sweep: lane i reads L[k][i] (row k of the packed rows, store_rows; or column i of the factor)
@@ -618,14 +523,23 @@ __device__ __forceinline__ void build_normal_mfma(double (&Mr)[Dims<N>::n], Smem
 // panels of 16 columns (the last one 8); for each, the panel's tiles (I, p), I >= p, are moved
 // to this lane's row registers (tile by tile through a 16 x 18 LDS buffer, select-free: lanes
 // outside block row I read the zero row), the panel is factored by the two-column pivot steps
-// of `cholesky` with the trailing update kept inside the panel, and the tiles to the right,
+// described below with the trailing update kept inside the panel, and the tiles to the right,
 // (I, J) with p < J <= I, take the panel's rank-16 update on the matrix cores
 // (v_mfma_f64_16x16x4_f64, operands = the just-stored factor columns from LDS): the trailing
 // update, 880 VALU FMAs + 380 broadcast reads in the row-per-lane factorisation, becomes
-// 16 MFMAs.  Output as `cholesky`'s: s.Lc columns, s.dinv, Mr = row `lane` of L strictly
+// 16 MFMAs.  Output: s.Lc columns, s.dinv (inverse pivots), Mr = row `lane` of L strictly
 // below the diagonal.  Buffers: panels 0, 1 use the factor storage of columns >= 16 (written
 // only by panel 1's own steps, after its transposes), panel 2 the broadcast vectors (tb2).
 // Returns false (uniform) if a pivot is not positive.
+// Pivot steps: two columns per step -- the 2x2 diagonal block comes from lanes k, k+1 by
+// readlane, both pivots are taken in registers (rsq_nr), both columns published to LDS, and one
+// LDS round trip serves the rank-2 update.  Software-pipelined: the pivot block k+2, k+3 depends
+// only on the lookahead columns (chunk 0 of step k's update), so its chain -- readlanes, two
+// rsq, the column scaling and its stores -- is split in three parts placed in the fence regions
+// of step k's update chunks 1, 2, 3, where the scheduler interleaves it with independent FMAs.
+// (A row-per-lane unblocked version of the same steps was the round-2/3 factorisation; the
+// second pivot from the block's determinant, both rsq chains in parallel, measured no gain in
+// round 6: the steps are bound by issue, not by the pivot chain.)
 template <int N>
 __device__ bool factor_blocked(double (&Mr)[Dims<N>::n], d4 (&acc)[Tiles<N>::NT], Smem<N>& s, int lane) {
   constexpr int n = Dims<N>::n, NB = Tiles<N>::NB;
@@ -1190,8 +1104,6 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
   double tol_cur = tol_early;
   bool polished = false, pchol_fail = false;
   int rounds = 0;
-  // KIN_EARLY_SET: the active set a failed early attempt ended with (its rounds' corrections applied)
-  bool e_alo_b = false, e_ahi_b = false, e_alo_c = false, e_ahi_c = false, have_early = false;
 #pragma unroll 1
   for (;;) {
   if (finite) {
@@ -1330,14 +1242,10 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
     bool ahi_b = guess(bx.hasHi, bx.lhi, bx.shi, (tapb >> 2) & 3);
     bool alo_c = guess(cs.hasLo, cs.llo, cs.slo, (tapb >> 4) & 3);
     bool ahi_c = guess(cs.hasHi, cs.lhi, cs.shi, (tapb >> 6) & 3);
-    if (KIN_EARLY_SET && have_early) {  // uniform
-      alo_b = e_alo_b; ahi_b = e_ahi_b; alo_c = e_alo_c; ahi_c = e_ahi_c;
-    }
-    // the early attempt: KIN_EARLY_ROUNDS rounds, then more (up to KIN_EARLY_MAX) only while the next
-    // round's factor is a rank-one update of this one's (an added bound or row: ~7 K cycles against
-    // a rebuild's 18 K); a dropped one sends the problem back to the interior point
-    const bool early = tol_cur > tol;
-    const int max_rounds = early ? min(A.qp.polish, KIN_EARLY_MAX) : A.qp.polish;
+    // (more early rounds, now that most rounds after the first are rank-one updates, lose: up to 3 / 4 / 6
+    // while each further round is an update, C2 +7 %, problem 260 adds a wrong bound and drops it again;
+    // profiles/r06/kin_ab/kin_polish_ab_c2_r06u.log)
+    const int max_rounds = tol_cur > tol ? min(A.qp.polish, KIN_EARLY_ROUNDS) : A.qp.polish;
     // KIN_UPDATE: the weight the current factor holds for state row `lane` (0: none), and how the
     // last round changed the active set (uniform; 1: variable upd_j fixed, 2: row upd_j added,
     // 0: anything else -- a dropped bound or row, or no factor yet -- which refactors)
@@ -1422,6 +1330,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
       // to the fixed point instead of at 0 (the fixed point does not depend on
       // the start: same certified z).  Rows the AL does not enforce (rho_c = 0) keep 0.
       double nu_c = (act && rho_c > 0.0) ? ((ahi_c ? cs.lhi : 0.0) - (alo_c ? cs.llo : 0.0)) : 0.0;
+
       // The passes are Richardson's iteration nu += R e on S dnu = e(nu), S = G_A M^-1 G_A' (M the
       // factored matrix, R = diag(rho_c)): it contracts by 1 - min eig(R S) per pass, up to 14 passes
       // on the slowest C2 problems (profiles/r04/sec_r04f.txt).  Conjugate gradients solve the same
@@ -1523,7 +1432,6 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
       const bool sel_box = (__ballot(vb >= vcr) >> sel) & 1ull;
       upd = dual ? 0 : (sel_box ? 1 : 2);  // an added bound fixes variable sel, an added row is row sel
       upd_j = sel;
-      if (early && round + 1 >= KIN_EARLY_ROUNDS && (upd == 0 || !KIN_UPDATE)) break;  // uniform
 #ifdef VC_TIMING
       if (dual) tacc[T_NDROP] += 1;
 #endif
@@ -1538,10 +1446,6 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
           else ahi_c = true;
         }
       }
-    }
-    if (KIN_EARLY_SET && !polished && tol_cur > tol) {
-      e_alo_b = alo_b; e_ahi_b = ahi_b; e_alo_c = alo_c; e_ahi_c = ahi_c;
-      have_early = true;
     }
   }
 
