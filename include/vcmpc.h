@@ -11,6 +11,9 @@
  *                    CascadedMPC.command (single-track, horizon_pm = 0)
  *                                                     controllers/mpc/cascaded_mpc.py:306-314 (opti.solve
  *                                                     at :308; NLP built at :17-39,91-179,279-304)
+ *   vc_solve_from    the same, with the warm start and u* in separate buffers (the reference passes
+ *                    its warm start in by opti.set_initial, kinematic_mpc.py:175-176, and reads u* back
+ *                    by sol.value, :163)
  *   vc_rollout       KinematicCar.spatial_transition  vehicle_control/models/kinematic_car.py:61-64,70-72,
  *                    applied along the horizon        (the dynamics rows of kinematic_mpc.py:95-99)
  *   vc_linearize     CasADi AD of the dynamics inside IPOPT ("expand": True, kinematic_mpc.py:51)
@@ -60,7 +63,7 @@
 extern "C" {
 #endif
 
-#define VCMPC_ABI_VERSION 12
+#define VCMPC_ABI_VERSION 13
 #define VC_MAX_OBSTACLES 16
 
 typedef struct vc_ctx vc_ctx;
@@ -240,6 +243,13 @@ int vc_synchronize(vc_ctx* ctx);
  * xbar is output only: the prediction is re-rolled from (x0, ubar). */
 int vc_solve(vc_ctx* ctx, int B, const void* x0, const void* kappa, const void* ds,
              void* xbar, void* ubar, void* u0, int32_t* status, int32_t* iters, int flags);
+
+/* vc_solve with the warm start read from ubar_in, which is left unchanged, and u* written to
+ * u_out (same shape; u_out == ubar_in is vc_solve).  The kinematic kernels read and write through
+ * the two pointers (no copy); the SQP contexts, which iterate in place, copy ubar_in to u_out
+ * first.  For callers that keep their warm start, e.g. a batch re-solved from the same guess. */
+int vc_solve_from(vc_ctx* ctx, int B, const void* x0, const void* kappa, const void* ds, const void* ubar_in,
+                  void* xbar, void* u_out, void* u0, int32_t* status, int32_t* iters, int flags);
 
 /* vc_solve plus per-problem solver diagnostics diag[B][4]:
  *   [0] final scaled KKT residual, [1] final scaled complementarity mu,

@@ -18,7 +18,7 @@ static int fails = 0;
   } while (0)
 
 int main() {
-  CHECK(vc_abi_version() == 12);
+  CHECK(vc_abi_version() == 13);
   CHECK(vc_params_sizeof() == (int)sizeof(vc_params));
   vc_params p;
   std::memset(&p, 0, sizeof(p));
@@ -43,6 +43,10 @@ int main() {
     int st[64] = {0}, it[64] = {0};
     CHECK(vc_solve(c, 65, x, k, ds, xb, u, u0, st, it, VC_HOST_PTRS) != 0);  // B > max_batch
     CHECK(vc_solve(c, -1, x, k, ds, xb, u, u0, st, it, VC_HOST_PTRS) != 0);
+    double uo[64 * 20 * 2] = {0};
+    CHECK(vc_solve_from(c, 65, x, k, ds, u, xb, uo, u0, st, it, VC_HOST_PTRS) != 0);  // ABI 13
+    CHECK(vc_solve_from(c, 4, x, k, ds, nullptr, xb, uo, u0, st, it, VC_HOST_PTRS) != 0);
+    CHECK(vc_solve_from(c, 4, x, k, ds, u, xb, nullptr, u0, st, it, VC_HOST_PTRS) != 0);
     CHECK(std::strlen(vc_last_error(c)) > 0);
     CHECK(vc_set_obstacles(c, -1, nullptr, nullptr, nullptr, 0.0) != 0);
     const double coef[4 * 4] = {0.0, 0.0, 0.0, 0.01, 0.0, 0.0, 0.0, 0.01, 0.0, 0.0, 0.0, 0.01, 0.0, 0.0, 0.0, 0.01};

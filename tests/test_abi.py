@@ -17,7 +17,7 @@ def _declared_symbols():
 
 def test_header_declares_expected_entry_points():
     syms = _declared_symbols()
-    for s in ("vc_create", "vc_destroy", "vc_solve", "vc_rollout", "vc_linearize", "vc_condense",
+    for s in ("vc_create", "vc_destroy", "vc_solve", "vc_solve_from", "vc_rollout", "vc_linearize", "vc_condense",
               "vc_plant_step", "vc_spatial_step", "vc_last_error", "vc_set_stream", "vc_synchronize",
               "vc_track_set", "vc_track_k", "vc_horizon", "vc_drive", "vc_simulate"):
         assert s in syms

@@ -239,6 +239,44 @@ def test_device_pointer_path(ctx, kin_golden):
     assert np.abs(ustar.cpu().numpy() - g["u_star"]).max() < U_TOL
 
 
+def test_solve_from_matches_in_place_solve(ctx, dyn_ctx, kin_golden):
+    """vc_solve_from (ABI 13): warm start read from ubar_in, left unchanged, u* into u_out --
+    bit-identical to vc_solve's in-place answer, on device pointers (the kinematic kernel reads
+    and writes through the two pointers) and host pointers, and on a dynamic context (which copies
+    ubar_in to u_out and solves in place)."""
+    import torch
+    from vcmpc.workload import dynamic_batch, kinematic_batch
+    dev = torch.device("cuda:0")
+    d = kinematic_batch(512, N=N, seed=41)
+    ref = ctx.solve(d["x0"], d["kappa"], d["ds"], d["ubar"].copy())
+    # host pointers
+    ub_in = d["ubar"].copy()
+    u_out = np.empty_like(ub_in)
+    got = ctx.solve_from(d["x0"], d["kappa"], d["ds"], ub_in, u_out)
+    assert np.array_equal(ub_in, d["ubar"])
+    for a, b in zip(ref, got):
+        assert np.array_equal(np.asarray(a), np.asarray(b))
+    # device pointers
+    t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in d.items()}
+    tu = torch.empty_like(t["ubar"])
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    try:
+        u0, xbar, uo, st, it = ctx.solve_from(t["x0"], t["kappa"], t["ds"], t["ubar"], tu)
+        torch.cuda.synchronize()
+    finally:
+        ctx.set_stream(None)
+    assert np.array_equal(t["ubar"].cpu().numpy(), d["ubar"])
+    assert np.array_equal(uo.cpu().numpy(), ref[2])
+    assert np.array_equal(st.cpu().numpy(), ref[3]) and np.array_equal(xbar.cpu().numpy(), ref[1])
+    # an SQP context
+    dd = {k: v.astype(np.float64) for k, v in dynamic_batch(64, N=40, seed=3).items()}
+    dref = dyn_ctx.solve(dd["x0"], dd["kappa"], dd["ds"], dd["ubar"].copy())
+    dub = dd["ubar"].copy()
+    dgot = dyn_ctx.solve_from(dd["x0"], dd["kappa"], dd["ds"], dub, np.empty_like(dub))
+    assert np.array_equal(dub, dd["ubar"])
+    assert np.array_equal(dgot[2], dref[2]) and np.array_equal(dgot[3], dref[3])
+
+
 def test_controller_drop_in_closed_loop(kin_cfg):
     """KinematicMPC(car, config).command(state) -> action, then car.drive: the
     reference's simulator step (kinracing.py:283-290) on a constant-curvature track."""

@@ -486,9 +486,31 @@ int vc_synchronize(vc_ctx* c) {
   return 0;
 }
 
+static int kin_solve(vc_ctx* c, int B, const void* x0, const void* kappa, const void* ds, void* xbar,
+                     const void* ubar_in, void* u_out, void* u0, int32_t* status, int32_t* iters, void* diag,
+                     int flags);
+
 int vc_solve(vc_ctx* c, int B, const void* x0, const void* kappa, const void* ds, void* xbar, void* ubar, void* u0,
              int32_t* status, int32_t* iters, int flags) {
   return vc_solve_diag(c, B, x0, kappa, ds, xbar, ubar, u0, status, iters, nullptr, flags);
+}
+
+int vc_solve_from(vc_ctx* c, int B, const void* x0, const void* kappa, const void* ds, const void* ubar_in,
+                  void* xbar, void* u_out, void* u0, int32_t* status, int32_t* iters, int flags) {
+  if (int r = check_common(c, B, flags)) return r;
+  if (!ubar_in || !u_out) return fail(c, VC_E_ARG, "null pointer");
+  if (ubar_in == u_out) return vc_solve(c, B, x0, kappa, ds, xbar, u_out, u0, status, iters, flags);
+  if (c->model == VC_MODEL_KINEMATIC && kin_solve_built(c)) {
+    if (!x0 || !kappa || !ds || !xbar || !u0 || !status || !iters) return fail(c, VC_E_ARG, "null pointer");
+    if (B == 0) return 0;
+    return kin_solve(c, B, x0, kappa, ds, xbar, ubar_in, u_out, u0, status, iters, nullptr, flags);
+  }
+  // the SQP contexts iterate in place: u_out <- ubar_in, then vc_solve on u_out
+  const int H = c->N + (c->model == VC_MODEL_CASCADED ? c->p.casc.horizon_pm : 0);
+  const size_t bytes = (size_t)B * H * 2 * (c->dtype == VC_F32 ? 4 : 8);
+  if (flags == VC_HOST_PTRS) std::memcpy(u_out, ubar_in, bytes);
+  else VC_HIP(c, hipMemcpyAsync(u_out, ubar_in, bytes, hipMemcpyDeviceToDevice, c->stream));
+  return vc_solve(c, B, x0, kappa, ds, xbar, u_out, u0, status, iters, flags);
 }
 
 int vc_solve_diag(vc_ctx* c, int B, const void* x0, const void* kappa, const void* ds, void* xbar, void* ubar,
@@ -502,6 +524,14 @@ int vc_solve_diag(vc_ctx* c, int B, const void* x0, const void* kappa, const voi
   if (B == 0) return 0;
   if (c->model == VC_MODEL_DYNAMIC) return dyn_solve(c, B, x0, kappa, ds, xbar, ubar, u0, status, iters, diag, flags);
   if (c->model == VC_MODEL_CASCADED) return casc_solve(c, B, x0, kappa, ds, xbar, ubar, u0, status, iters, diag, flags);
+  return kin_solve(c, B, x0, kappa, ds, xbar, ubar, ubar, u0, status, iters, diag, flags);
+}
+
+// The kinematic solve with the warm start read through ubar_in and u* written through u_out
+// (vc_solve: both the caller's ubar; vc_solve_from: two buffers).
+static int kin_solve(vc_ctx* c, int B, const void* x0, const void* kappa, const void* ds, void* xbar,
+                     const void* ubar_in, void* u_out, void* u0, int32_t* status, int32_t* iters, void* diag,
+                     int flags) {
   if (c->p.qp.elastic < 0.0 && c->p.qp.kin_sqp <= 0)
     return fail(c, VC_E_ARG, "vc_qp.elastic < 0 (elastic on failure) needs kin_sqp > 0; rho > 0 for one QP step");
   const int N = c->N, nx = 6, nu = 2;
@@ -517,7 +547,7 @@ int vc_solve_diag(vc_ctx* c, int B, const void* x0, const void* kappa, const voi
     slots = {{x0, nullptr, (size_t)B * nx * 8, nullptr},
              {kappa, nullptr, (size_t)B * N * 8, nullptr},
              {ds, nullptr, (size_t)B * N * 8, nullptr},
-             {ubar, ubar, (size_t)B * N * nu * 8, nullptr},
+             {ubar_in, u_out, (size_t)B * N * nu * 8, nullptr},
              {c->p.qp.ms ? xbar : nullptr, xbar, (size_t)B * (N + 1) * nx * 8, nullptr},
              {nullptr, u0, (size_t)B * nu * 8, nullptr},
              {nullptr, status, (size_t)B * 4, nullptr},
@@ -538,8 +568,8 @@ int vc_solve_diag(vc_ctx* c, int B, const void* x0, const void* kappa, const voi
     a.x0 = (const double*)x0;
     a.kappa = (const double*)kappa;
     a.ds = (const double*)ds;
-    a.ubar = (const double*)ubar;
-    a.u_out = (double*)ubar;
+    a.ubar = (const double*)ubar_in;
+    a.u_out = (double*)u_out;
     a.x_out = (double*)xbar;
     a.u0 = (double*)u0;
     a.status = status;
@@ -548,6 +578,11 @@ int vc_solve_diag(vc_ctx* c, int B, const void* x0, const void* kappa, const voi
   }
   a.x_in = a.x_out;  // multiple shooting (qp.ms): the warm-start states arrive in xbar
   const int S = c->p.qp.kin_sqp;
+  if (S > 0 && (const void*)a.ubar != (const void*)a.u_out) {
+    // the SQP iterates in place: start it on u_out
+    VC_HIP(c, hipMemcpyAsync(a.u_out, a.ubar, (size_t)B * N * nu * 8, hipMemcpyDeviceToDevice, c->stream));
+    a.ubar = a.u_out;
+  }
   if (S <= 0) {  // the LTV-QP contract: one QP step
     if (kin_condensed(c)) VC_HIP(c, vc::launch_kin_ltv(a, N, c->stream));
     else VC_HIP(c, vc::launch_kin_ric(a, N, c->stream));

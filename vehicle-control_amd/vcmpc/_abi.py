@@ -12,7 +12,7 @@ import os
 
 LIB_NAME = "libvcmpc.so"
 LIB_PATH = os.environ.get("VCMPC_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME))
-ABI_VERSION = 12
+ABI_VERSION = 13
 VC_MAX_OBSTACLES = 16
 OBS_MARGIN_MIN = 0.05  # VC_OBS_MARGIN_MIN (csrc/vc_kernels.hpp)
 
@@ -97,6 +97,7 @@ PROTOTYPES = {
     "vc_set_obstacles": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, C.c_double]),
     "vc_solve": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int]),
     "vc_solve_diag": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int]),
+    "vc_solve_from": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int]),
     "vc_solve_debug": (C.c_int, [_vp, C.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_int]),
     "vc_debug_stride": (C.c_int, []),
     "vc_debug_qp_fault": (C.c_int, [_vp, C.c_int, C.c_int]),

@@ -152,6 +152,32 @@ class Context:
         self._check(self.lib.vc_solve(self._h, B, *ptrs, flags))
         return u0, xbar, ubar, status, iters
 
+    def solve_from(self, x0, kappa, ds, ubar_in, u_out, xbar=None, u0=None, status=None, iters=None):
+        """``vc_solve_from``: ``solve`` with the warm start read from ``ubar_in``, which is left
+        unchanged, and u* written to ``u_out``; returns (u0, xbar, u_out, status, iters)."""
+        B, N, nx, f = self._batch(x0), self.NH, self.nx, _NP_DT[self.dtype]
+        NS = self.ns_solve
+        if xbar is None and self.model == _abi.VC_MODEL_KINEMATIC and self.params.qp.ms:
+            raise ValueError("vc_qp.ms: multiple shooting linearises at the state iterate; pass xbar")
+        if _is_torch(x0):
+            import torch
+            kw = dict(device=x0.device)
+            xbar = torch.empty((B, NS, nx), dtype=x0.dtype, **kw) if xbar is None else xbar
+            u0 = torch.empty((B, NU), dtype=x0.dtype, **kw) if u0 is None else u0
+            status = torch.empty((B,), dtype=torch.int32, **kw) if status is None else status
+            iters = torch.empty((B,), dtype=torch.int32, **kw) if iters is None else iters
+        else:
+            xbar = np.empty((B, NS, nx), f) if xbar is None else xbar
+            u0 = np.empty((B, NU), f) if u0 is None else u0
+            status = np.empty((B,), np.int32) if status is None else status
+            iters = np.empty((B,), np.int32) if iters is None else iters
+        bufs = [x0, kappa, ds, ubar_in, xbar, u_out, u0, status, iters]
+        shapes = [(B, nx), (B, N), (B, N), (B, N, NU), (B, NS, nx), (B, N, NU), (B, NU), (B,), (B,)]
+        dts = [f, f, f, f, f, f, f, np.int32, np.int32]
+        ptrs, flags = self._marshal(bufs, shapes, dts)
+        self._check(self.lib.vc_solve_from(self._h, B, *ptrs, flags))
+        return u0, xbar, u_out, status, iters
+
     def solve_debug(self, x0, kappa, ds, ubar):
         """``vc_solve_debug`` (dynamic contexts): the solve plus a dump of the first
         QP's internals (g, normal matrix, factor storage, predictor rhs and step)."""
