@@ -239,7 +239,7 @@ def test_device_pointer_path(ctx, kin_golden):
     assert np.abs(ustar.cpu().numpy() - g["u_star"]).max() < U_TOL
 
 
-def test_solve_from_matches_in_place_solve(ctx, dyn_ctx, kin_golden):
+def test_solve_from_matches_in_place_solve(ctx, kin_golden):
     """vc_solve_from (ABI 13): warm start read from ubar_in, left unchanged, u* into u_out --
     bit-identical to vc_solve's in-place answer, on device pointers (the kinematic kernel reads
     and writes through the two pointers) and host pointers, and on a dynamic context (which copies
@@ -268,11 +268,15 @@ def test_solve_from_matches_in_place_solve(ctx, dyn_ctx, kin_golden):
     assert np.array_equal(t["ubar"].cpu().numpy(), d["ubar"])
     assert np.array_equal(uo.cpu().numpy(), ref[2])
     assert np.array_equal(st.cpu().numpy(), ref[3]) and np.array_equal(xbar.cpu().numpy(), ref[1])
-    # an SQP context
+    # an SQP context (single-track, the C3 shape)
+    from vcmpc import Context, _abi
+    from vcmpc.config import load_config, make_params
+    params = make_params(dyn_car=load_config("dynamic_car"), dyn_mpc=load_config("dynamic_mpc"), tyre="linear")
     dd = {k: v.astype(np.float64) for k, v in dynamic_batch(64, N=40, seed=3).items()}
-    dref = dyn_ctx.solve(dd["x0"], dd["kappa"], dd["ds"], dd["ubar"].copy())
-    dub = dd["ubar"].copy()
-    dgot = dyn_ctx.solve_from(dd["x0"], dd["kappa"], dd["ds"], dub, np.empty_like(dub))
+    with Context(model=_abi.VC_MODEL_DYNAMIC, N=40, max_batch=64, dtype=_abi.VC_F64, params=params) as dc:
+        dref = dc.solve(dd["x0"], dd["kappa"], dd["ds"], dd["ubar"].copy())
+        dub = dd["ubar"].copy()
+        dgot = dc.solve_from(dd["x0"], dd["kappa"], dd["ds"], dub, np.empty_like(dub))
     assert np.array_equal(dub, dd["ubar"])
     assert np.array_equal(dgot[2], dref[2]) and np.array_equal(dgot[3], dref[3])
 

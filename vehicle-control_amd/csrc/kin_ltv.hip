@@ -68,9 +68,6 @@
 #ifndef KIN_RSQ_HALLEY
 #define KIN_RSQ_HALLEY 1  // pivots' 1/sqrt by one third-order step (0: two Newton steps; C2 -0.8 %, C4 -1.2 %)
 #endif
-#ifndef KIN_FAST_TRIG
-#define KIN_FAST_TRIG 0  // 1: S1's sincos by kin_sincos and its quotients by rcp_nr (A/B)
-#endif
 #ifndef KIN_CHOL_CH
 #define KIN_CHOL_CH 8  // rows per trailing-update chunk, loaded one chunk ahead (4: +5 % factorisation time)
 #endif
@@ -290,7 +287,9 @@ __device__ double h_dot(const Smem<N>& s, int lane) {
 // sin and cos of a small angle (the rollout's heading error and steering angle, |x| ~ 1): one
 // Cody-Waite step by pi/2 (a 33-bit head, exact in the fma for |n| < 2^20, and a 53-bit tail) and
 // fdlibm's kernels on [-pi/4, pi/4] (< 1 ulp), no large-argument path -- the library sincos
-// carries a Payne-Hanek branch and a three-part reduction on S1's serial chain (KIN_FAST_TRIG)
+// carries a Payne-Hanek branch and a three-part reduction on S1's serial chain.  With the quotients
+// below as num * rcp_nr(den): S1 26.6 K -> 22.1 K cycles, C2 -1.0 %, C4 -1.4 %, u* within 2.2e-10
+// (profiles/r06/kin_ab/kin_polish_ab_c2_r06y.log, kin_polish_sec_ft1_r06y.txt)
 __device__ __forceinline__ void kin_sincos(double x, double& sn, double& cs) {
   const double n = __builtin_rint(x * 6.36619772367581382433e-01);
   const double y = fma(-n, 6.07710050650619224932e-11, fma(-n, 1.57079632673412561417e+00, x));
@@ -862,11 +861,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
       // rho / cos(epsi) and q = rho / (v cos(epsi)) as one divide in lanes 0..3
       {
         double sn, cs;
-#if KIN_FAST_TRIG
         kin_sincos((lane & 1) ? x[1] : x[4], sn, cs);
-#else
-        vsincos((lane & 1) ? x[1] : x[4], sn, cs);
-#endif
         const double se = lane_bcast(sn, 0), ce = lane_bcast(cs, 0);
         const double sd = lane_bcast(sn, 1), cd = lane_bcast(cs, 1);
         const double kap = s.kap[k];
@@ -874,11 +869,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
         const int r4 = lane & 3;
         const double num = r4 == 0 ? se : (r4 == 1 ? sd : rho);
         const double den = r4 == 0 ? ce : (r4 == 1 ? cd * A.L : (r4 == 2 ? ce : x[0] * ce));
-#if KIN_FAST_TRIG
         const double quo = num * rcp_nr(den);  // correctly rounded 1/den, then one rounding more
-#else
-        const double quo = num / den;
-#endif
         const double te = lane_bcast(quo, 0), tdl = lane_bcast(quo, 1);
         const double rc = lane_bcast(quo, 2), q = lane_bcast(quo, 3);
         f[0] = q * u2[0];
@@ -1524,32 +1515,18 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
   double dx[KIN_NX] = {0, 0, 0, 0, 0, 0};
   double* xo = A.x_out + (size_t)b * (N + 1) * KIN_NX;
   if (lane < KIN_NX) xo[lane] = s.xb[0][lane];
-  // each step's LDS operands are read one step ahead (S3's pattern): the recursion's own chain is
-  // a few FMAs, and a rolled loop that loaded them in place waited on the LDS every step
-  // (11.9 K cycles for the 20 steps, round-6 section timing)
-  double jn[9], hn, an, wn, dan, dwn, xbn;
-  auto fetch = [&](int k) {
-#pragma unroll
-    for (int q = 0; q < 9; ++q) jn[q] = s.jac[k][q];
-    hn = s.ds[k]; an = s.ub[2 * k]; wn = s.ub[2 * k + 1];
-    dan = s.vz[2 * k]; dwn = s.vz[2 * k + 1];
-    xbn = s.xb[k + 1][lane < KIN_NX ? lane : KIN_NX];
-  };
-  fetch(0);
 #pragma unroll 1
   for (int k = 0; k < N; ++k) {
-    double J[9];
-#pragma unroll
-    for (int q = 0; q < 9; ++q) J[q] = jn[q];
-    const double h = hn, a = an, w = wn, da = dan, dw = dwn, xbk = xbn;
-    if (k + 1 < N) fetch(k + 1);
-    const double dq = J[1] * dx[0] + J[2] * dx[3] + J[3] * dx[4];
+    const double q = s.jac[k][0], qv = s.jac[k][1], qey = s.jac[k][2], qep = s.jac[k][3];
+    const double h = s.ds[k], a = s.ub[2 * k], w = s.ub[2 * k + 1];
+    const double da = s.vz[2 * k], dw = s.vz[2 * k + 1];
+    const double dq = qv * dx[0] + qey * dx[3] + qep * dx[4];
     double nx[KIN_NX];
-    nx[0] = dx[0] + h * (a * dq + J[0] * da);
-    nx[1] = dx[1] + h * (w * dq + J[0] * dw);
+    nx[0] = dx[0] + h * (a * dq + q * da);
+    nx[1] = dx[1] + h * (w * dq + q * dw);
     nx[2] = dx[2];
-    nx[3] = dx[3] + h * (J[4] * dx[3] + J[5] * dx[4]);
-    nx[4] = dx[4] + h * (J[6] * dx[1] + J[7] * dx[3] + J[8] * dx[4]);
+    nx[3] = dx[3] + h * (s.jac[k][4] * dx[3] + s.jac[k][5] * dx[4]);
+    nx[4] = dx[4] + h * (s.jac[k][6] * dx[1] + s.jac[k][7] * dx[3] + s.jac[k][8] * dx[4]);
     nx[5] = dx[5] + h * dq;
     double mine = 0.0;
 #pragma unroll
@@ -1557,8 +1534,10 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
       dx[i] = nx[i];
       if (i == lane) mine = nx[i];
     }
-    if (lane < KIN_NX) xo[(k + 1) * KIN_NX + lane] = xbk + mine;
+    if (lane < KIN_NX) xo[(k + 1) * KIN_NX + lane] = s.xb[k + 1][lane] + mine;
   }
+  // (reading each step's LDS operands a step ahead, S3's pattern, measured equal: C2 0.2090 vs
+  // 0.2097 ms, profiles/r06/kin_ab/kin_polish_ab_c2_r06z.log -- the section is not LDS-latency bound)
   VC_TACC(T_OUT, t_out0)
 #ifdef VC_TIMING
   // timing builds: diag is [B][4 + T_NSLOT]
