@@ -18,7 +18,7 @@ from vcmpc.workload import kinematic_batch  # noqa: E402
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 tol = float(sys.argv[2]) if len(sys.argv) > 2 else 1e-10
 names = ["S1 rollout", "setup", "resid", "build", "chol", "solve", "pol fact", "polish", "out", "S2 jac", "S3 sens", "S4 hess",
-         "pol AL", "AL passes", "upd rounds", "upd cyc", "drop rounds"]
+         "pol AL", "AL passes", "upd rounds", "upd cyc", "drop rounds", "early fail", "carry rm", "carry add"]
 dev = torch.device("cuda:0")
 d = kinematic_batch(B, seed=31)
 t = {k: torch.from_numpy(v).to(dev) for k, v in d.items()}
@@ -63,5 +63,13 @@ with Context(N=20, max_batch=B, params=p) as c:
         sel = its == k
         if sel.any():
             print(f"  iters {k:2d}: {sel.sum():4d} problems, total cycles mean {tot[sel].mean():.0f} max {tot[sel].max():.0f}")
+    ef = cyc[:, names.index("early fail")] > 0
+    if ef.any():
+        rm, ad = cyc[ef, names.index("carry rm")], cyc[ef, names.index("carry add")]
+        print(f"  failed early attempts: {int(ef.sum())}; final set vs the early factor: drops 0 in {int((rm == 0).sum())}, "
+              f"adds <= 1 / 2 / 3 with no drop: {int(((rm == 0) & (ad <= 1)).sum())} / {int(((rm == 0) & (ad <= 2)).sum())} / "
+              f"{int(((rm == 0) & (ad <= 3)).sum())}; slowest such problems: "
+              + ", ".join(f"{int(b)} (rm {int(cyc[b, names.index('carry rm')])}, add {int(cyc[b, names.index('carry add')])})"
+                          for b in order if ef[b])[:400])
     if os.environ.get("SEC_DUMP"):  # per-problem arrays for offline tail analysis
         np.savez(os.environ["SEC_DUMP"], cyc=cyc, its=its, rounds=dg[:, 3], tot=tot)

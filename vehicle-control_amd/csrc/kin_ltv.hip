@@ -167,8 +167,10 @@ __device__ __forceinline__ lds_cdouble* lds_opaque(const double* p) {
 // T_SWEEP = the serial rollout S1; T_S2 / T_S3 / T_S4 the sweep's other three parts
 // T_UPDATE: the polish's matrix build + factorisation (part of T_POLISH); T_PAL its augmented-
 // Lagrangian passes (cycles), T_PPASS their count; T_NUPD the rounds whose factor came from
-// factor_update, T_UCYC those updates' cycles, T_NDROP the rounds ended by dropping a bound or row
-enum { T_SWEEP = 0, T_SETUP, T_RESID, T_BUILD, T_CHOL, T_SOLVE, T_UPDATE, T_POLISH, T_OUT, T_S2, T_S3, T_S4, T_PAL, T_PPASS, T_NUPD, T_UCYC, T_NDROP, T_NSLOT };
+// factor_update, T_UCYC those updates' cycles, T_NDROP the rounds ended by dropping a bound or row;
+// T_CFAIL 1 after a failed early attempt, T_CRM / T_CADD how many bounds and rows the final attempt's
+// first set drops / adds against the early attempt's last factored one (a study of carrying that factor)
+enum { T_SWEEP = 0, T_SETUP, T_RESID, T_BUILD, T_CHOL, T_SOLVE, T_UPDATE, T_POLISH, T_OUT, T_S2, T_S3, T_S4, T_PAL, T_PPASS, T_NUPD, T_UCYC, T_NDROP, T_CFAIL, T_CRM, T_CADD, T_NSLOT };
 
 
 template <int N>
@@ -1126,6 +1128,11 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
   // Tapia guess 99.6 % of the C2 problems certify at 100 x tol, 1.15 interior-point iterations
   // earlier on average (scripts/early_polish_study.py).
   const double tol_early = KIN_EARLY_F > 0.0 ? fmax(tol, KIN_EARLY_F * tol) : tol;
+  int e_set = 0;  // per lane: 256 | the early attempt's last set (bits 0..3) | that set changed (bits 4..7)
+#ifdef VC_TIMING
+  uint64_t e_fmask = 0;
+  bool e_row = false, e_have = false;
+#endif
   double tol_cur = tol_early;
   bool polished = false, pchol_fail = false;
   int rounds = 0;
@@ -1267,6 +1274,15 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
     bool ahi_b = guess(bx.hasHi, bx.lhi, bx.shi, (tapb >> 2) & 3);
     bool alo_c = guess(cs.hasLo, cs.llo, cs.slo, (tapb >> 4) & 3);
     bool ahi_c = guess(cs.hasHi, cs.lhi, cs.shi, (tapb >> 6) & 3);
+    auto pack = [&]() { return int(alo_b) | (int(ahi_b) << 1) | (int(alo_c) << 2) | (int(ahi_c) << 3); };
+    // The final attempt's guess repeats the set the failed early attempt factored last (problems 153
+    // and 855 of the C2 batch): that round's outcome is known -- the equality-constrained optimum of
+    // a set does not depend on the interior-point iterate -- so start from the set it changed to
+    // (153: 388 K -> 360 K cycles, 855: 377 K -> 358 K; C2 -0.6 %; profiles/r06/kin_ab/kin_polish_*_r06za.*)
+    if (tol_cur <= tol && __ballot(e_set != 0 && pack() != (e_set & 15)) == 0ull && __ballot(e_set != 0) != 0ull) {
+      const int t = e_set >> 4;
+      alo_b = t & 1; ahi_b = (t >> 1) & 1; alo_c = (t >> 2) & 1; ahi_c = (t >> 3) & 1;
+    }
     // (more early rounds, now that most rounds after the first are rank-one updates, lose: up to 3 / 4 / 6
     // while each further round is an update, C2 +7 %, problem 260 adds a wrong bound and drops it again;
     // profiles/r06/kin_ab/kin_polish_ab_c2_r06u.log)
@@ -1279,6 +1295,17 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
 #pragma unroll 1
     for (int round = 0; round < max_rounds; ++round) {
       no_hoist();
+      const int set0 = pack();  // this round's set (bits 0..3), for the carry above
+#ifdef VC_TIMING
+      if (round == 0 && tol_cur <= tol && e_have) {
+        const bool fx = (lane < n) && (alo_b || ahi_b);
+        const uint64_t fm = __ballot(fx);
+        const bool ract = (lane < NC) && (alo_c || ahi_c);
+        tacc[T_CFAIL] = 1;
+        tacc[T_CRM] = __builtin_popcountll(e_fmask & ~fm) + __builtin_popcountll(__ballot(e_row && !ract));
+        tacc[T_CADD] = __builtin_popcountll(fm & ~e_fmask) + __builtin_popcountll(__ballot(ract && !e_row));
+      }
+#endif
       ++rounds;  // over both attempts (diag[3]; bench.py prices each round as an iteration)
       const bool fixed = (lane < n) && (alo_b || ahi_b);
       const double zfix = fixed ? (alo_b ? bx.lo : bx.hi) : 0.0;
@@ -1471,6 +1498,14 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
           else ahi_c = true;
         }
       }
+      if (tol_cur > tol) e_set = 256 | set0 | (pack() << 4);  // early attempt: this round's set and its change
+#ifdef VC_TIMING
+      if (tol_cur > tol) {  // the early attempt's last factored set (this round's)
+        e_fmask = fmask;
+        e_row = rho_k > 0.0;
+        e_have = true;
+      }
+#endif
     }
   }
 
