@@ -18,7 +18,7 @@ from vcmpc.workload import kinematic_batch  # noqa: E402
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 tol = float(sys.argv[2]) if len(sys.argv) > 2 else 1e-10
 names = ["S1 rollout", "setup", "resid", "build", "chol", "solve", "pol fact", "polish", "out", "S2 jac", "S3 sens", "S4 hess",
-         "pol AL", "AL passes", "upd rounds", "upd cyc", "drop rounds", "early fail", "carry rm", "carry add"]
+         "pol AL", "AL passes", "upd rounds", "upd cyc", "drop rounds", "early fail", "carry rm", "carry add", "r0 change"]
 dev = torch.device("cuda:0")
 d = kinematic_batch(B, seed=31)
 t = {k: torch.from_numpy(v).to(dev) for k, v in d.items()}
@@ -71,5 +71,18 @@ with Context(N=20, max_batch=B, params=p) as c:
               f"{int(((rm == 0) & (ad <= 3)).sum())}; slowest such problems: "
               + ", ".join(f"{int(b)} (rm {int(cyc[b, names.index('carry rm')])}, add {int(cyc[b, names.index('carry add')])})"
                           for b in order if ef[b])[:400])
+    r0 = cyc[:, names.index("r0 change")].astype(int)
+    if (r0 > 0).any():
+        kinds = ["box add", "row add", "drop"]
+        tap = ["undecided", "active", "inactive"]
+        from collections import Counter
+        rows = Counter()
+        for b in np.nonzero(r0 > 0)[0]:
+            c = r0[b] - 1
+            rows[(kinds[c % 3], tap[c // 3], "early fail" if ef[b] else "early ok")] += 1
+        print("  early attempts that changed a constraint in round 0 (kind, changed side's Tapia state, outcome): "
+              + "; ".join(f"{k}: {v}" for k, v in sorted(rows.items())))
+        print("  early-fail problems' first change: " + ", ".join(f"{int(b)}: {kinds[(r0[b] - 1) % 3]} / {tap[(r0[b] - 1) // 3]}"
+                                                          for b in np.nonzero(ef)[0]))
     if os.environ.get("SEC_DUMP"):  # per-problem arrays for offline tail analysis
         np.savez(os.environ["SEC_DUMP"], cyc=cyc, its=its, rounds=dg[:, 3], tot=tot)

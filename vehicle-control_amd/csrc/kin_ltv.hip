@@ -169,8 +169,9 @@ __device__ __forceinline__ lds_cdouble* lds_opaque(const double* p) {
 // Lagrangian passes (cycles), T_PPASS their count; T_NUPD the rounds whose factor came from
 // factor_update, T_UCYC those updates' cycles, T_NDROP the rounds ended by dropping a bound or row;
 // T_CFAIL 1 after a failed early attempt, T_CRM / T_CADD how many bounds and rows the final attempt's
-// first set drops / adds against the early attempt's last factored one (a study of carrying that factor)
-enum { T_SWEEP = 0, T_SETUP, T_RESID, T_BUILD, T_CHOL, T_SOLVE, T_UPDATE, T_POLISH, T_OUT, T_S2, T_S3, T_S4, T_PAL, T_PPASS, T_NUPD, T_UCYC, T_NDROP, T_CFAIL, T_CRM, T_CADD, T_NSLOT };
+// first set drops / adds against the early attempt's last factored one (a study of carrying that factor);
+// T_R0CHG the early attempt's first change: 1 + (0 box add, 1 row add, 2 drop) + 3 x its side's Tapia state
+enum { T_SWEEP = 0, T_SETUP, T_RESID, T_BUILD, T_CHOL, T_SOLVE, T_UPDATE, T_POLISH, T_OUT, T_S2, T_S3, T_S4, T_PAL, T_PPASS, T_NUPD, T_UCYC, T_NDROP, T_CFAIL, T_CRM, T_CADD, T_R0CHG, T_NSLOT };
 
 
 template <int N>
@@ -1498,6 +1499,15 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
           else ahi_c = true;
         }
       }
+#ifdef VC_TIMING
+      if (tol_cur > tol && round == 0) {
+        int tside = 0;
+        if (vb >= vcr) tside = (dual ? (ahi_b ? (tapb >> 2) : tapb) : (zp < bx.lo ? tapb : (tapb >> 2))) & 3;
+        else tside = (dual ? (ahi_c ? (tapb >> 6) : (tapb >> 4)) : (ypc < cs.lo ? (tapb >> 4) : (tapb >> 6))) & 3;
+        const int code = 1 + (dual ? 2 : (vb >= vcr ? 0 : 1)) + 3 * tside;
+        tacc[T_R0CHG] = (uint64_t)__builtin_amdgcn_readlane(code, sel);
+      }
+#endif
       if (tol_cur > tol) e_set = 256 | set0 | (pack() << 4);  // early attempt: this round's set and its change
 #ifdef VC_TIMING
       if (tol_cur > tol) {  // the early attempt's last factored set (this round's)
