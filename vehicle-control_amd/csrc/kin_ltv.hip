@@ -1500,15 +1500,23 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
         }
       }
 #ifdef VC_TIMING
+      int r0code = 0;
       if (tol_cur > tol && round == 0) {
         int tside = 0;
         if (vb >= vcr) tside = (dual ? (ahi_b ? (tapb >> 2) : tapb) : (zp < bx.lo ? tapb : (tapb >> 2))) & 3;
         else tside = (dual ? (ahi_c ? (tapb >> 6) : (tapb >> 4)) : (ypc < cs.lo ? (tapb >> 4) : (tapb >> 6))) & 3;
         const int code = 1 + (dual ? 2 : (vb >= vcr ? 0 : 1)) + 3 * tside;
-        tacc[T_R0CHG] = (uint64_t)__builtin_amdgcn_readlane(code, sel);
+        r0code = __builtin_amdgcn_readlane(code, sel);
+#ifdef VC_TIMING
+        tacc[T_R0CHG] = (uint64_t)r0code;
+#endif
       }
 #endif
       if (tol_cur > tol) e_set = 256 | set0 | (pack() << 4);  // early attempt: this round's set and its change
+      // (ending the early attempt after its first change by the change's kind and the changed side's
+      // Tapia state does not separate the attempts that fail: C2 +1 / +5 / +3 % for undecided adds / all
+      // adds / drops, profiles/r06/kin_ab/kin_polish_ab_c2_r06zd.log; on 16,384 problems 262 of 282
+      // first changes "box add, Tapia inactive" certify in the next round, kin_polish_sec16k_r06zd.txt)
 #ifdef VC_TIMING
       if (tol_cur > tol) {  // the early attempt's last factored set (this round's)
         e_fmask = fmask;
