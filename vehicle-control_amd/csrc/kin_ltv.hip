@@ -68,8 +68,8 @@
 #ifndef KIN_RSQ_HALLEY
 #define KIN_RSQ_HALLEY 1  // pivots' 1/sqrt by one third-order step (0: two Newton steps; C2 -0.8 %, C4 -1.2 %)
 #endif
-#ifndef KIN_CHOL_CH
-#define KIN_CHOL_CH 8  // rows per trailing-update chunk, loaded one chunk ahead (4: +5 % factorisation time)
+#ifndef KIN_PANEL_CH
+#define KIN_PANEL_CH 4  // columns per in-panel update chunk of factor_blocked, loaded one chunk ahead
 #endif
 
 namespace vc {
@@ -643,7 +643,7 @@ __device__ bool factor_blocked(double (&Mr)[Dims<N>::n], d4 (&acc)[Tiles<N>::NT]
       Mr[k + 1] = lane > k + 1 ? y : 0.0;
       const double* cA = &s.Lc[lc_base<n>(k)];
       const double* cB = &s.Lc[lc_base<n>(k + 1)];
-      constexpr int CH = 4;
+      constexpr int CH = KIN_PANEL_CH;
       const int J0 = k + 2, NCH = (c1 - J0 + CH - 1) / CH;
       double u0[2][CH], u1[2][CH];
       auto load = [&](int ch, int buf) {
