@@ -69,7 +69,8 @@
 #define KIN_RSQ_HALLEY 1  // pivots' 1/sqrt by one third-order step (0: two Newton steps; C2 -0.8 %, C4 -1.2 %)
 #endif
 #ifndef KIN_PANEL_CH
-#define KIN_PANEL_CH 4  // columns per in-panel update chunk of factor_blocked, loaded one chunk ahead
+#define KIN_PANEL_CH 6  // columns per in-panel update chunk of factor_blocked, loaded one chunk ahead (2 / 4 / 8:
+                        // C2 +1.2 / +1.0 / +0.8 %, bit-identical; profiles/r06/kin_ab/kin_polish_ab_c2_r06ze.log)
 #endif
 
 namespace vc {
