@@ -68,6 +68,10 @@
 #ifndef KIN_RSQ_HALLEY
 #define KIN_RSQ_HALLEY 1  // pivots' 1/sqrt by one third-order step (0: two Newton steps; C2 -0.8 %, C4 -1.2 %)
 #endif
+#ifndef KIN_SOLVE_CH
+#define KIN_SOLVE_CH 8  // backward-sweep steps per prefetched chunk of the triangular solves (divides 2N;
+                        // 4 / 10 within noise of 8, as KIN_DOT_CH 4 / 12: profiles/r06/kin_ab/kin_polish_ab_c2_r06zg.log)
+#endif
 #ifndef KIN_PANEL_CH
 #define KIN_PANEL_CH 6  // columns per in-panel update chunk of factor_blocked, loaded one chunk ahead (2 / 4 / 8:
                         // C2 +1.2 / +1.0 / +0.8 %, bit-identical; profiles/r06/kin_ab/kin_polish_ab_c2_r06ze.log)
@@ -353,7 +357,7 @@ __device__ __forceinline__ void store_rows(const double (&Mr)[Dims<N>::n], Smem<
 template <int N>
 __device__ double chol_solve(const double (&Lr)[Dims<N>::n], const Smem<N>& s, double b, int lane) {
   constexpr int n = Dims<N>::n;
-  constexpr int CH = 8;
+  constexpr int CH = KIN_SOLVE_CH;
   static_assert(n % CH == 0, "backward prefetch chunks");
   const int row = lane < n ? lane : 0;
   lds_cdouble* col = lds_opaque(&s.Lc[lc_base<n>(row)]);  // col[k] = L[k][row] for k > row
