@@ -68,6 +68,17 @@
 #ifndef KIN_RSQ_HALLEY
 #define KIN_RSQ_HALLEY 1  // pivots' 1/sqrt by one third-order step (0: two Newton steps; C2 -0.8 %, C4 -1.2 %)
 #endif
+#ifndef KIN_STAT_CHECK
+#define KIN_STAT_CHECK 0  // 1: the polish certificate also checks the free variables' stationarity (same time,
+                          // same certification at the shipped settings: profiles/r06/kin_ab/kin_polish_cert_st1_r06zj.log)
+#endif
+#ifndef KIN_STEP_F
+// interior point: fraction of the step to the boundary.  0.98 costs +0.6 iterations; 0.995 / 0.998 are
+// slower at C2 (+7 / +13 %) and expose two C4 problems (c4_shard seed 31: 9204 reported solved from an
+// unpolished interior point 3e-5 off, 6021 polish-certified 6.0 off the oracle's optimum along a flat
+// direction) that the oracle certificate catches (scripts/kin_hole_diag.py, profiles/r06/kin_ab/*_r06z[ijk].*)
+#define KIN_STEP_F 0.99
+#endif
 #ifndef KIN_SOLVE_CH
 #define KIN_SOLVE_CH 8  // backward-sweep steps per prefetched chunk of the triangular solves (divides 2N;
                         // 4 / 10 within noise of 8, as KIN_DOT_CH 4 / 12: profiles/r06/kin_ab/kin_polish_ab_c2_r06zg.log)
@@ -1234,7 +1245,7 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
           sm = sr * sr * sr * mu;  // sigma * mu with sigma = (mu_aff / mu)^3
           pp1 = d1 * d2; pp2 = d3 * d4; pp3 = e1 * e2; pp4 = e3 * e4;
         } else {
-          const double al = 0.99 * amax;
+          const double al = KIN_STEP_F * amax;
           {
             // Tapia indicators of this step (El-Bakry, Tapia, Tsuchiya, Zhang 1996): near the
             // solution an active side's slack shrinks by a factor the multiplier does not, an
@@ -1459,7 +1470,10 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
       wave_sync();
       const double grad = (lane < n) ? (h_dot<N>(s, lane) + gj + gt_dot<N>(s, lane)) : 0.0;
       const double ypc = grow_dot<N>(s, lane);
-      emax = wave_max(al_act ? fabs(ypc - bnd_al) : 0.0);  // the true violation, not CG's recurrence
+      // the true violation, not CG's recurrence -- and, with KIN_STAT_CHECK, the free variables'
+      // stationarity (the solves are trusted to make it ~0; a factor gone inaccurate must not certify)
+      emax = wave_max(fmax(al_act ? fabs(ypc - bnd_al) : 0.0,
+                           (KIN_STAT_CHECK && lane < n && !fixed) ? fabs(grad) : 0.0));
       // dual violations (> 0 is wrong-signed): box multiplier of an active bound is
       // -grad (upper) / grad (lower); state-row multiplier is nu (upper) / -nu (lower)
       const double dv_b = (lane < n) ? (ahi_b ? grad : (alo_b ? -grad : -1.0)) : -1.0;
