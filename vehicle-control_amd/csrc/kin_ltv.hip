@@ -1472,8 +1472,11 @@ __global__ __launch_bounds__(64) void kin_ltv_kernel(KinLtvArgs A) {
       const double ypc = grow_dot<N>(s, lane);
       // the true violation, not CG's recurrence -- and, with KIN_STAT_CHECK, the free variables'
       // stationarity (the solves are trusted to make it ~0; a factor gone inaccurate must not certify)
-      emax = wave_max(fmax(al_act ? fabs(ypc - bnd_al) : 0.0,
-                           (KIN_STAT_CHECK && lane < n && !fixed) ? fabs(grad) : 0.0));
+#if KIN_STAT_CHECK
+      emax = wave_max(fmax(al_act ? fabs(ypc - bnd_al) : 0.0, (lane < n && !fixed) ? fabs(grad) : 0.0));
+#else
+      emax = wave_max(al_act ? fabs(ypc - bnd_al) : 0.0);
+#endif
       // dual violations (> 0 is wrong-signed): box multiplier of an active bound is
       // -grad (upper) / grad (lower); state-row multiplier is nu (upper) / -nu (lower)
       const double dv_b = (lane < n) ? (ahi_b ? grad : (alo_b ? -grad : -1.0)) : -1.0;
